@@ -1,0 +1,139 @@
+/* hastar.h — C ABI of the MI355X-native Hybrid A* planner (path_planning_pkg_amd).
+ *
+ * This is the drop-in boundary for the reference's planner facade
+ * `planning::HybridAStar<T>` (reference: include/path_planning_pkg/HybridAStar.h:27-75,
+ * lib/HybridAStar.cpp:7-286).  Every entry point below replaces one public member
+ * function of that class; the C++ header include/path_planning_pkg/HybridAStar.h
+ * re-implements the class on top of these calls so src/local_planner.cpp links
+ * unchanged.
+ *
+ * Plain C: opaque handles, plain pointers and sizes, no torch/HIP types.
+ * All functions return 0 on success or a negative HASTAR_E* code.
+ * A handle is single-threaded like the reference object; the batch call runs many
+ * handles' searches concurrently on one GPU (one wavefront per planner).
+ *
+ * Arithmetic type: float (the reference's ROS node instantiates HybridAStar<float>,
+ * src/local_planner.cpp:509).
+ */
+#ifndef PATH_PLANNING_PKG_AMD_HASTAR_H
+#define PATH_PLANNING_PKG_AMD_HASTAR_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HASTAR_OK 0
+#define HASTAR_EINVAL (-22)     /* bad argument / handle */
+#define HASTAR_ENOSPC (-28)     /* output buffer too small: *len holds the length needed */
+#define HASTAR_ENOMEM (-12)     /* device allocation failed */
+#define HASTAR_EDEVICE (-5)     /* HIP runtime / kernel error (message via hastar_last_error) */
+#define HASTAR_EOVERFLOW (-75)  /* search exceeded the handle's arena (max_pops etc.) */
+
+/* Constructor arguments: the 20 parameters of HybridAStar<T>::HybridAStar
+ * (HybridAStar.h:33-38, called by src/local_planner.cpp:158-161), in the same order
+ * and meaning, plus arena limits for the device search. */
+typedef struct hastar_params {
+  int dubins_shot_interval;        /* pops between Dubins shots (HybridAStar.cpp:98) */
+  int dubins_shot_interval_decay;  /* interval decrement after a failed shot */
+  float grid_resolution;           /* metres per cell */
+  float obstacle_threshold;        /* occupancy probability threshold */
+  float obstacle_prob_min;         /* log-odds clamp, as probabilities */
+  float obstacle_prob_max;
+  float obstacle_prob_free;        /* decay step, as probability */
+  int grid_size;                   /* N (square N x N grid) */
+  int grid_2d_allow_diag_moves;    /* bool: 8- vs 4-connected holonomic A* */
+  float step_size;                 /* motion primitive length (m) */
+  float max_lat_acc;
+  float max_long_dec;
+  float wheelbase;
+  float rear_to_cg;
+  float apf_rep_constant;
+  float apf_active_angle;          /* radians */
+  int num_angle_bins;
+  int num_actions;
+  int num_steering;                /* length of steering[] and curvature_weights[] */
+  const float* steering;           /* radians */
+  const float* curvature_weights;
+  /* ---- extensions (0 = default) ---- */
+  int max_pops;                    /* arena: Hybrid A* pops per search (default 262144) */
+  int max_astar_nodes;             /* arena: holonomic A* nodes per inner search (default N*N) */
+  int max_dubins_samples;          /* arena: samples of one Dubins shot (default from N) */
+} hastar_params;
+
+typedef struct hastar_handle_s* hastar_handle;
+
+/* Per-search statistics (work units of the measurement in DESIGN.md). */
+typedef struct hastar_stats {
+  long long pops;              /* iterations of HybridAStar.cpp:107 (incl. re-expanded duplicates) */
+  long long successors;        /* successors that passed the bounds/occupancy filter (Grid3D.cpp:54-59) */
+  long long astar_pops;        /* pops of the lazy holonomic A* (AStar.cpp:127) */
+  long long astar_searches;    /* a_star_search() calls (memo misses) */
+  long long shots;             /* Dubins shots attempted */
+  long long closed_size;       /* Hybrid A* closed-set size at termination */
+  unsigned long long pop_digest;    /* ordered digest of (cell, bin, g bits) of every pop */
+  unsigned long long closed_digest; /* order-independent digest of the closed-set keys */
+  int via_shot;                /* success came from an analytic Dubins shot */
+  int status;                  /* 0 ok, HASTAR_EOVERFLOW if the arena overflowed */
+} hastar_stats;
+
+/* HybridAStar(...) (HybridAStar.cpp:7-24). device = HIP device ordinal. */
+int hastar_create_f32(const hastar_params* params, int device, hastar_handle* out);
+int hastar_destroy(hastar_handle h);
+
+/* update_goal(goal, start) (HybridAStar.cpp:55-59): goal/start = {x, y, heading}. */
+int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3]);
+
+/* reset() (HybridAStar.cpp:49-52): clears the holonomic A* memo. */
+int hastar_reset(hastar_handle h);
+
+/* update_obstacles(obstacles, confidence, apf_added_radius) (HybridAStar.cpp:29-33):
+ * boxes = n x {center_x, center_y, dimension_x, dimension_y} (Obstacle.h:16-21). */
+int hastar_update_boxes(hastar_handle h, const float* boxes, const float* confidence, int n,
+                        float apf_added_radius);
+
+/* update_obstacles(lines, confidence, line_width) (HybridAStar.cpp:36-40):
+ * lines = n x {x1, y1, x2, y2}. */
+int hastar_update_lines(hastar_handle h, const float* lines, const float* confidence, int n,
+                        float line_width);
+
+/* update_obstacles() (HybridAStar.cpp:43-46): free-space decay of every cell. */
+int hastar_decay(hastar_handle h);
+
+/* find_path(vel_init, start, path, curvature) (HybridAStar.cpp:68-88).
+ * xyh receives len x {x, y, heading} in the order the reference appends them
+ * (goal first, start last; HybridAStar.cpp:208-262), curv receives len curvatures.
+ * cap = capacity in poses.  On HASTAR_ENOSPC *len is the required length and the
+ * search state is kept (call hastar_copy_path with a bigger buffer).
+ * *cost / *ok are the reference's returned pair (FLT_MAX, 0 on failure).
+ * stats may be NULL. */
+int hastar_find_path(hastar_handle h, float vel_init, const float start[3], float* xyh, float* curv,
+                     int cap, int* len, float* cost, int* ok, hastar_stats* stats);
+
+/* Copy the path of the last find_path again (for a retry after HASTAR_ENOSPC). */
+int hastar_copy_path(hastar_handle h, float* xyh, float* curv, int cap, int* len);
+
+/* Batched find_path over n independent planners: one kernel launch, one wavefront per
+ * planner.  Arrays are indexed by planner; xyh is n x cap x 3, curv n x cap, len/cost/ok n.
+ * Returns the first error; per-planner status is in stats[i].status when stats != NULL. */
+int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel_init, const float* starts,
+                           float* xyh, float* curv, int cap, int* len, float* cost, int* ok,
+                           hastar_stats* stats);
+
+/* get_obstacles() (HybridAStar.cpp:62-65): copies the N x N log-odds map (row i = x cell). */
+int hastar_get_obstacles(hastar_handle h, float* out);
+
+/* Grid size N of the handle. */
+int hastar_grid_size(hastar_handle h);
+
+/* Last error message of this thread (static storage). */
+const char* hastar_last_error(void);
+
+/* ---- timing hooks used by bench.py (device time of the last search launch) ---- */
+/* Milliseconds of the last search kernel (HIP events on the launch stream). */
+float hastar_last_search_ms(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PATH_PLANNING_PKG_AMD_HASTAR_H */

@@ -1,0 +1,899 @@
+// hastar_oracle.cpp — TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference's
+// Hybrid A* hot path, used as the parity checker and as bench.py's cpu_baseline.
+// Nothing in path_planning_pkg_amd/ links, loads or calls this file; only tests/,
+// __graft_entry__.smoke() and bench.py's cpu_baseline leg do.
+//
+// The reference (ShehabAshraf101/path_planning_pkg) is UNBUILDABLE in this image: every
+// translation unit includes <boost/functional/hash.hpp> (Node2D.h:6, Node3D.h:7) and Boost
+// is not installed; making it build would need a stand-in header, which we do not write.
+// This restatement is pinned instead by the reference's own golden vectors
+// (tests/golden/, see tests/test_oracle_golden.py):
+//   * utils/hybrid_astar/plot.py:47-51  — 43-pose path of test_hybrid_astar.cpp (float)
+//   * utils/dubins_paths.py:6           — 73-pose RSL Dubins path (double)
+//   * utils/vehicle_mode.py:12          — 33 positions of VehicleModel::simulate_action (double)
+//
+// Semantics that decide the closed set are restated with the SAME library machinery
+// the reference uses, so they are faithful by construction:
+//   * open sets are std::set with the reference's non-strict-weak comparator
+//     (Node3D.h:50-54, Node2D.h:41-45): equal-f inserts are dropped, find() may hit
+//     an equal-f node of another cell, outcomes depend on the libstdc++ RB-tree shape;
+//   * closed sets are node-based hash sets keyed exactly by (x, y[, bin]) (the
+//     reference's hash caches codes, so Node3D::operator== comparing only the cell,
+//     Node3D.h:42, still yields (x, y, bin) membership); duplicates return the OLD
+//     element (HybridAStar.cpp:110-111);
+//   * float/double promotions follow the reference expressions (M_PI literals,
+//     std::fmod(float, double), std::pow(double, 2) -> x*x as GCC folds it);
+//   * transcendental calls go to the host glibc libm, like the reference.
+// Build: oracle/Makefile (g++ -O2 -ffp-contract=off, x86-64 baseline ISA).
+#include <cmath>
+#include <cfloat>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <set>
+#include <unordered_set>
+#include <vector>
+#include <algorithm>
+#include <numeric>
+#include <chrono>
+
+#include "../include/hastar.h"
+
+namespace orc {
+
+template <class T> struct P2 { T x, y; };
+template <class T> struct P3 { T x, y, h; };
+
+// common.h:15-29
+template <class T> T wrap_pi(T a) {
+  T w = std::fmod(a, 2 * M_PI);
+  if (w > M_PI) return w - 2 * M_PI;
+  if (w < -M_PI) return w + 2 * M_PI;
+  return w;
+}
+// common.h:8-12, 31-36
+template <class T> int heading_bin(T h, T prec) {
+  T r = std::round(h / prec) * prec;
+  return static_cast<int>((r + M_PI) / prec);
+}
+// common.h:55-61 (Vector2D::get_rotated_vector / rotate_vector)
+template <class T> P2<T> rot2(T x, T y, T ang) {
+  T c = std::cos(ang), s = std::sin(ang);
+  return {x * c + y * s, -x * s + y * c};
+}
+// common.h:162-169 (Vector3D::get_rotated_vector)
+template <class T> P3<T> rot3(P3<T> p, T ang) {
+  T c = std::cos(ang), s = std::sin(ang);
+  return {p.x * c + p.y * s, -p.x * s + p.y * c, wrap_pi<T>(p.h - ang)};
+}
+template <class T> T stl_max(T a, T b) { return (a < b) ? b : a; }
+template <class T> T stl_min(T a, T b) { return (b < a) ? b : a; }
+
+static inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+static inline uint32_t f32bits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+
+// ------------------------------------------------------------------ Dubins (Dubins.cpp)
+enum Word { RSR = 0, RSL = 1, LSR = 2, LSL = 3 };
+
+template <class T> struct DubinsCSC {
+  T r, step, ang_step;
+  T prm[4];
+  int word = RSR;
+  DubinsCSC(T r_min, T step_size) : r(r_min), step(step_size), ang_step(step_size / r_min) {
+    prm[0] = prm[1] = prm[2] = prm[3] = 0;
+  }
+  // Dubins.cpp:180-323 — one CSC word: fills q[4] and returns its length
+  T word_len(int w, P2<T> cs, P2<T> cg, const P3<T>& s, const P3<T>& g, T q[4]) const {
+    P2<T> d{cg.x - cs.x, cg.y - cs.y};
+    if (w == RSR || w == LSL) {
+      T th = std::atan2(d.y, d.x);
+      T sgn = (w == RSR) ? 1 : -1;
+      q[0] = sgn * M_PI_2 + s.h;
+      T t1 = sgn * M_PI_2 + th;
+      q[2] = t1;
+      T tg = sgn * M_PI_2 + g.h;
+      q[1] = t1 - q[0];
+      q[3] = tg - q[2];
+      if (w == RSR) {
+        if (q[1] > 0) q[1] -= 2 * M_PI;
+        if (q[3] > 0) q[3] -= 2 * M_PI;
+      } else {
+        if (q[1] < 0) q[1] += 2 * M_PI;
+        if (q[3] < 0) q[3] += 2 * M_PI;
+      }
+      T dst = std::sqrt(d.x * d.x + d.y * d.y);
+      return (w == RSR) ? dst + r * -(q[1] + q[3]) : dst + r * (q[1] + q[3]);
+    }
+    T dist = std::sqrt(d.x * d.x + d.y * d.y);
+    T th = std::atan2(d.y, d.x);
+    T t1;
+    if (w == RSL) {
+      q[0] = M_PI_2 + s.h;
+      t1 = std::acos(2 * r / dist) + th;
+      q[2] = t1 - M_PI;
+      T tg = -M_PI_2 + g.h;
+      q[1] = t1 - q[0];
+      if (q[1] > 0) q[1] -= 2 * M_PI;
+      q[3] = tg - q[2];
+      if (q[3] < 0) q[3] += 2 * M_PI;
+    } else {
+      q[0] = -M_PI_2 + s.h;
+      t1 = -std::acos(2 * r / dist) + th;
+      q[2] = t1 + M_PI;
+      T tg = M_PI_2 + g.h;
+      q[1] = t1 - q[0];
+      if (q[1] < 0) q[1] += 2 * M_PI;
+      q[3] = tg - q[2];
+      if (q[3] > 0) q[3] -= 2 * M_PI;
+    }
+    P2<T> a{cs.x, cs.y}, b{cg.x, cg.y};
+    a.x += r * std::cos(t1);
+    a.y += r * std::sin(t1);
+    b.x += r * std::cos(q[2]);
+    b.y += r * std::sin(q[2]);
+    P2<T> e{b.x - a.x, b.y - a.y};
+    T dst = std::sqrt(e.x * e.x + e.y * e.y);
+    return (w == RSL) ? dst + r * (-q[1] + q[3]) : dst + r * (q[1] - q[3]);
+  }
+  // Dubins.cpp:19-69 (+ centres, 76-87)
+  T shortest(const P3<T>& s, const P3<T>& g, P2<T> c[4]) {
+    c[0] = {s.x + r * std::sin(s.h), s.y - r * std::cos(s.h)};  // start right
+    c[1] = {s.x - r * std::sin(s.h), s.y + r * std::cos(s.h)};  // start left
+    c[2] = {g.x + r * std::sin(g.h), g.y - r * std::cos(g.h)};  // goal right
+    c[3] = {g.x - r * std::sin(g.h), g.y + r * std::cos(g.h)};  // goal left
+    static const int si[4] = {0, 0, 1, 1}, gi[4] = {2, 3, 2, 3};
+    T best = 0;
+    for (int w = 0; w < 4; ++w) {
+      T q[4];
+      T len = word_len(w, c[si[w]], c[gi[w]], s, g, q);
+      if (w == 0 || len < best) {
+        best = len;
+        word = w;
+        std::copy(q, q + 4, prm);
+      }
+    }
+    return best;
+  }
+  T shortest(const P3<T>& s, const P3<T>& g) {
+    P2<T> c[4];
+    return shortest(s, g, c);
+  }
+  // Dubins.cpp:326-563: three segments + final pose; first/second arc direction by word
+  void sample(P2<T> cs, P2<T> cg, std::vector<P3<T>>& out, std::vector<T>& curv) const {
+    const bool s_right = (word == RSR || word == RSL);
+    const bool g_right = (word == RSR || word == LSR);
+    P2<T> a = cs, b = cg;
+    a.x += r * std::cos(prm[0] + prm[1]);
+    a.y += r * std::sin(prm[0] + prm[1]);
+    b.x += r * std::cos(prm[2]);
+    b.y += r * std::sin(prm[2]);
+    P2<T> e{b.x - a.x, b.y - a.y};
+    T lst = std::sqrt(e.x * e.x + e.y * e.y);
+    int n1 = static_cast<int>(std::floor((s_right ? -prm[1] : prm[1]) / ang_step));
+    int n2 = n1 + static_cast<int>(std::floor(lst / step));
+    int n3 = n2 + static_cast<int>(std::floor((g_right ? -prm[3] : prm[3]) / ang_step));
+    out.resize(n3 + 1);
+    curv.resize(n3 + 1);
+    T th = prm[0], k = 1 / r;
+    for (int i = 0; i < n1; ++i) {
+      out[i].x = cs.x + r * std::cos(th);
+      out[i].y = cs.y + r * std::sin(th);
+      // wrap_pi(theta -/+ M_PI_2) deduces T = double in Dubins.cpp:417,477,537,597
+      out[i].h = static_cast<T>(s_right ? wrap_pi<double>(th - M_PI_2) : wrap_pi<double>(th + M_PI_2));
+      curv[i] = k;
+      if (s_right) th -= ang_step; else th += ang_step;
+    }
+    th = std::atan2(e.y, e.x);
+    T ct = std::cos(th), st = std::sin(th), dd = 0;
+    for (int i = n1; i < n2; ++i) {
+      out[i].x = a.x + dd * ct;
+      out[i].y = a.y + dd * st;
+      out[i].h = th;
+      curv[i] = 0;
+      dd += step;
+    }
+    th = prm[2];
+    for (int i = n2; i < n3; ++i) {
+      out[i].x = cg.x + r * std::cos(th);
+      out[i].y = cg.y + r * std::sin(th);
+      out[i].h = static_cast<T>(g_right ? wrap_pi<double>(th - M_PI_2) : wrap_pi<double>(th + M_PI_2));
+      curv[i] = k;
+      if (g_right) th -= ang_step; else th += ang_step;
+    }
+    out[n3].x = cg.x + r * std::cos(prm[2] + prm[3]);
+    out[n3].y = cg.y + r * std::sin(prm[2] + prm[3]);
+    out[n3].h = static_cast<T>(g_right ? wrap_pi<double>(prm[2] + prm[3] - M_PI_2)
+                                        : wrap_pi<double>(prm[2] + prm[3] + M_PI_2));
+    curv[n3] = 0;
+  }
+  // Dubins.cpp:125-153: returns {length, first arc longer than 90 deg}
+  std::pair<T, bool> path(const P3<T>& s, const P3<T>& g, std::vector<P3<T>>& out, std::vector<T>& curv) {
+    P2<T> c[4];
+    T len = shortest(s, g, c);
+    static const int si[4] = {0, 0, 1, 1}, gi[4] = {2, 3, 2, 3};
+    sample(c[si[word]], c[gi[word]], out, curv);
+    return {len, std::abs(prm[1]) > static_cast<T>(M_PI_2)};
+  }
+};
+
+// ------------------------------------------------------------ motion primitives
+// VehicleModel.cpp:7-47 and 147-164.  The table row for heading bin == num_angle_bins
+// (reached when a heading rounds to +pi, VehicleModel.cpp:145) reads past the end of
+// the reference's vector (UB); glibc hands it the next chunk's unused prev_size word,
+// i.e. (0, 0).  We store that (0, 0) row explicitly.
+template <class T> struct Motion {
+  T ts, a_lat, a_lat2, prec;
+  int na, bins, nsteer;
+  std::vector<T> curv_abs, curv_signed, cost, dth;
+  std::vector<P2<T>> off;  // nsteer x (bins + 1)
+  Motion(T ts_, T max_lat_acc, T wheelbase, T rear_to_cg, int bins_, int na_, const std::vector<T>& steer,
+         const std::vector<T>& w)
+      : ts(ts_), a_lat(max_lat_acc), a_lat2(max_lat_acc * max_lat_acc), prec(2 * M_PI / bins_), na(na_),
+        bins(bins_), nsteer((int)steer.size()) {
+    std::vector<T> beta(nsteer);
+    curv_signed.resize(nsteer);
+    for (int i = 0; i < nsteer; ++i) {
+      beta[i] = std::atan2(rear_to_cg * std::tan(steer[i]), wheelbase);
+      curv_signed[i] = std::cos(beta[i]) * std::tan(steer[i]) / wheelbase;
+    }
+    cost.resize(nsteer);
+    dth.resize(nsteer);
+    off.assign((size_t)nsteer * (bins + 1), P2<T>{0, 0});
+    for (int i = 0; i < nsteer; ++i) {
+      dth[i] = ts * curv_signed[i];
+      cost[i] = ts + w[i] * std::abs(curv_signed[i]);
+      for (int j = 0; j < bins; ++j) {
+        T head = -M_PI + j * prec;
+        // calculate_offset(): explicit Euler, dt = 1 ms
+        const T dt = static_cast<T>(0.001);
+        T ox = 0, oy = 0, hh = head;
+        int n = static_cast<int>(ts / dt);
+        for (int k = 0; k < n; ++k) {
+          ox += dt * std::cos(beta[i] + hh);
+          oy += dt * std::sin(beta[i] + hh);
+          hh += dt * curv_signed[i];
+        }
+        off[(size_t)i * (bins + 1) + j] = {ox, oy};
+      }
+    }
+    curv_abs.resize(nsteer);
+    for (int i = 0; i < nsteer; ++i) curv_abs[i] = std::abs(curv_signed[i]);
+  }
+  const P2<T>& offset(int a, int bin) const { return off[(size_t)a * (bins + 1) + bin]; }
+};
+
+// ------------------------------------------------------------------ nodes + sets
+template <class T> struct N3 {
+  P3<T> pose;
+  T g, f, vmin;
+  int ci, bin, cx, cy;
+  const N3* prev;
+};
+template <class T> struct N3Less {
+  bool operator()(const N3<T>& a, const N3<T>& b) const {
+    return (a.cx != b.cx || a.cy != b.cy || a.bin != b.bin) && a.f < b.f;
+  }
+};
+template <class T> struct N3Hash {
+  size_t operator()(const N3<T>& n) const {
+    return mix64(((uint64_t)(uint32_t)n.cx << 40) ^ ((uint64_t)(uint32_t)n.cy << 16) ^ (uint32_t)n.bin);
+  }
+};
+template <class T> struct N3Eq {
+  bool operator()(const N3<T>& a, const N3<T>& b) const {
+    return a.cx == b.cx && a.cy == b.cy && a.bin == b.bin;
+  }
+};
+template <class T> struct N2 {
+  int x, y;
+  T g, f;
+  const N2* prev;
+};
+template <class T> struct N2Less {
+  bool operator()(const N2<T>& a, const N2<T>& b) const { return (a.x != b.x || a.y != b.y) && a.f < b.f; }
+};
+template <class T> struct N2Hash {
+  size_t operator()(const N2<T>& n) const { return mix64(((uint64_t)(uint32_t)n.x << 32) | (uint32_t)n.y); }
+};
+template <class T> struct N2Eq {
+  bool operator()(const N2<T>& a, const N2<T>& b) const { return a.x == b.x && a.y == b.y; }
+};
+
+// ------------------------------------------------------------------ the planner
+template <class T> struct Planner {
+  // parameters
+  int shot_interval, shot_decay;
+  T res, thr, lp_min, lp_max, lp_free;
+  int N, n2, n45;
+  bool diag;
+  T apf_rep, apf_ang;
+  Motion<T> mv;
+  DubinsCSC<T> dub;
+  // Grid2D state (Grid2D.h:47-60)
+  T grid_heading = 0;
+  P2<T> goal2{0, 0};
+  std::vector<T> occ;      // log-odds, N*N, [i*N + j]
+  std::vector<T> nm_h, nm_f;
+  std::vector<int> act_dx, act_dy;
+  std::vector<T> act_cost;
+  // Grid3D state
+  P3<T> goal3{0, 0, 0};
+  struct Apf { T x, y, r; };
+  std::vector<Apf> apf;
+  // AStar state (AStar.h:63-72)
+  std::vector<uint8_t> visited;
+  N2<T> astar_goal{0, 0, 0, 0, nullptr};
+  std::set<N2<T>, N2Less<T>> op2;
+  std::unordered_set<N2<T>, N2Hash<T>, N2Eq<T>> cl2;
+  // HybridAStar state
+  N3<T> goal_node{};
+  std::set<N3<T>, N3Less<T>> op3;
+  std::unordered_set<N3<T>, N3Hash<T>, N3Eq<T>> cl3;
+  bool shot_ok = false;
+  std::vector<P3<T>> shot_path;
+  std::vector<T> shot_curv;
+  N3<T> terminal{};
+  // statistics
+  hastar_stats st{};
+
+  static std::vector<T> tovec(const float* p, int n) { return std::vector<T>(p, p + n); }
+
+  explicit Planner(const hastar_params& p)
+      : shot_interval(p.dubins_shot_interval), shot_decay(p.dubins_shot_interval_decay),
+        res(p.grid_resolution),
+        thr(std::log(static_cast<T>(p.obstacle_threshold) / (1.0 - static_cast<T>(p.obstacle_threshold)))),
+        lp_min(std::log(static_cast<T>(p.obstacle_prob_min) / (1.0 - static_cast<T>(p.obstacle_prob_min)))),
+        lp_max(std::log(static_cast<T>(p.obstacle_prob_max) / (1.0 - static_cast<T>(p.obstacle_prob_max)))),
+        lp_free(std::log(static_cast<T>(p.obstacle_prob_free) / (1.0 - static_cast<T>(p.obstacle_prob_free)))),
+        N(p.grid_size), n2(static_cast<int>(std::round(p.grid_size * 0.5))),
+        n45(static_cast<int>(std::round(p.grid_size * 0.8))), diag(p.grid_2d_allow_diag_moves != 0),
+        apf_rep(p.apf_rep_constant), apf_ang(p.apf_active_angle),
+        mv(p.step_size, p.max_lat_acc, p.wheelbase, p.rear_to_cg, p.num_angle_bins, p.num_actions,
+           tovec(p.steering, p.num_steering), tovec(p.curvature_weights, p.num_steering)),
+        dub(min_radius(p), p.step_size) {
+    occ.assign((size_t)N * N, 0);
+    nm_h.resize((size_t)N * N);
+    for (int i = 0; i < N; ++i) {  // Grid2D::compute_heuristic (Grid2D.cpp:303-316)
+      T dx = (n45 - i) * res;
+      T dx2 = dx * dx;
+      for (int j = 0; j < N; ++j) {
+        T dy = (n2 - j) * res;
+        T dy2 = dy * dy;
+        nm_h[(size_t)i * N + j] = std::sqrt(dx2 + dy2);
+      }
+    }
+    nm_f = nm_h;  // Node2D(i, j) then set_heuristic_cost: f = 0 + h
+    static const int d8x[8] = {0, 1, 1, 1, 0, -1, -1, -1}, d8y[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
+    static const int d4x[4] = {0, 1, 0, -1}, d4y[4] = {-1, 0, 1, 0};
+    int na = diag ? 8 : 4;
+    for (int k = 0; k < na; ++k) {
+      int ax = diag ? d8x[k] : d4x[k], ay = diag ? d8y[k] : d4y[k];
+      act_dx.push_back(ax);
+      act_dy.push_back(ay);
+      act_cost.push_back(res * std::sqrt(static_cast<T>(ax * ax + ay * ay)));
+    }
+    visited.assign((size_t)N * N, 0);
+  }
+  // HybridAStar.cpp:22-24 (tan_max over steering, HybridAStar.h:20-25)
+  static T min_radius(const hastar_params& p) {
+    T mx = *std::max_element(p.steering, p.steering + p.num_steering);
+    T tm = std::tan(mx);
+    return static_cast<T>(p.wheelbase) / (std::cos(std::atan2(static_cast<T>(p.rear_to_cg) * tm,
+                                                             static_cast<T>(p.wheelbase))) * tm);
+  }
+
+  bool inside(int i, int j) const { return i > -1 && i < N && j > -1 && j < N; }
+  T& cell(int i, int j) { return occ[(size_t)i * N + j]; }
+  void bump(int i, int j, T delta) {  // Grid2D.cpp:131-132
+    T& m = cell(i, j);
+    m += delta;
+    m = stl_max(stl_min(m, lp_max), lp_min);
+  }
+
+  // ---------------------------------------------------------------- map upkeep
+  // Grid2D::update_obstacles() (Grid2D.cpp:197-208)
+  void decay() {
+    for (auto& m : occ) {
+      m += lp_free;
+      m = stl_max(stl_min(m, lp_max), lp_min);
+    }
+  }
+  // Grid3D::update_obstacles(boxes) (Grid3D.cpp:22-44) + Grid2D boxes (Grid2D.cpp:99-139)
+  void boxes(const float* b, const float* conf, int n, T apf_r) {
+    apf.clear();
+    for (int k = 0; k < n; ++k) {
+      T ox = b[4 * k], oy = b[4 * k + 1], dx = b[4 * k + 2], dy = b[4 * k + 3];
+      P2<T> p = rot2<T>(ox - goal3.x, oy - goal3.y, grid_heading);
+      p.x += n45 * res;
+      p.y += n2 * res;
+      apf.push_back({p.x, p.y, std::max(dx, dy) / 2 + apf_r});
+    }
+    for (int k = 0; k < n; ++k) {
+      T ox = b[4 * k], oy = b[4 * k + 1], dx = b[4 * k + 2], dy = b[4 * k + 3];
+      P2<T> bl = rot2<T>((ox - dx / 2) - goal2.x, (oy - dy / 2) - goal2.y, grid_heading);
+      int si = static_cast<int>(std::round(bl.x / res) + n45);
+      int sj = static_cast<int>(std::round(bl.y / res) + n2);
+      int ei = static_cast<int>(std::ceil(dx / res)), ej = static_cast<int>(std::ceil(dy / res));
+      T lc = std::log(static_cast<T>(conf[k]) / (1.0 - static_cast<T>(conf[k])));
+      for (int i = 0; i < 2 * ei; ++i)
+        for (int j = 0; j < 2 * ej; ++j) {
+          P2<T> o = rot2<T>(i * 0.5, j * 0.5, grid_heading);
+          int ip = si + static_cast<int>(std::round(o.x));
+          int jp = sj + static_cast<int>(std::round(o.y));
+          if (inside(ip, jp)) bump(ip, jp, lc - lp_free);
+        }
+    }
+  }
+  // Grid2D::update_obstacles(lines) (Grid2D.cpp:142-194)
+  void lines(const float* L, const float* conf, int n, T width) {
+    for (int k = 0; k < n; ++k) {
+      P2<T> a = rot2<T>(static_cast<T>(L[4 * k]) - goal2.x, static_cast<T>(L[4 * k + 1]) - goal2.y, grid_heading);
+      P2<T> b = rot2<T>(static_cast<T>(L[4 * k + 2]) - goal2.x, static_cast<T>(L[4 * k + 3]) - goal2.y, grid_heading);
+      P2<T> d{b.x - a.x, b.y - a.y};
+      T len = std::hypot(d.x, d.y);
+      P2<T> nrm{-d.y / len, d.x / len};
+      d = {d.x / len, d.y / len};
+      T lc = std::log(static_cast<T>(conf[k]) / (1.0 - static_cast<T>(conf[k])));
+      T pl = 0;
+      for (size_t it = 0; pl <= len && it < 100; ++it, pl += res) {
+        P2<T> c{a.x + d.x * pl, a.y + d.y * pl};
+        for (T pw = 0; pw <= width; pw += res) {
+          P2<T> p1{c.x + nrm.x * pw, c.y + nrm.y * pw};
+          P2<T> p2{c.x - nrm.x * pw, c.y - nrm.y * pw};
+          int i1 = static_cast<int>(std::round(p1.x / res)) + n45, i2 = static_cast<int>(std::round(p2.x / res)) + n45;
+          int j1 = static_cast<int>(std::round(p1.y / res)) + n2, j2 = static_cast<int>(std::round(p2.y / res)) + n2;
+          if (inside(i1, j1)) bump(i1, j1, lc - lp_free);
+          if (inside(i2, j2)) bump(i2, j2, lc - lp_free);
+        }
+      }
+    }
+  }
+  // Grid3D::update_goal_heading + relocate_obstacles (Grid3D.cpp:102-124, 169-203)
+  void update_goal(const P3<T>& g, const P3<T>& s) {
+    T gh_prev = grid_heading;
+    P3<T> g3_prev = goal3;
+    goal2 = {g.x, g.y};
+    grid_heading = std::atan2(g.y - s.y, g.x - s.x);
+    goal3 = g;
+    // relocate
+    T dh = grid_heading - gh_prev;
+    P2<T> gp = rot2<T>(static_cast<T>(n45), static_cast<T>(n2), dh);
+    P2<T> gno = rot2<T>(g3_prev.x - goal3.x, g3_prev.y - goal3.y, grid_heading);
+    P2<T> org{static_cast<T>(n45) + gno.x / res, static_cast<T>(n2) + gno.y / res};
+    org = {org.x - gp.x, org.y - gp.y};
+    std::vector<T> nm((size_t)N * N, static_cast<T>(0));
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) {
+        P2<T> q = rot2<T>(static_cast<T>(i), static_cast<T>(j), dh);
+        q = {q.x + org.x, q.y + org.y};
+        int a = static_cast<int>(std::round(q.x)), b = static_cast<int>(std::round(q.y));
+        if (inside(a, b)) nm[(size_t)a * N + b] = occ[(size_t)i * N + j];
+      }
+    occ.swap(nm);
+    // goal node (Grid3D.cpp:115-123); AStar::update_goal_node takes the cell
+    goal_node = N3<T>{};
+    goal_node.pose = {n45 * res, n2 * res, wrap_pi<T>(g.h - grid_heading)};
+    goal_node.bin = heading_bin<T>(goal_node.pose.h, mv.prec);
+    goal_node.cx = n45;
+    goal_node.cy = n2;
+    astar_goal = {n45, n2, 0, nm_f[(size_t)n45 * N + n2], nullptr};
+  }
+  void reset() { std::fill(visited.begin(), visited.end(), 0); }
+
+  // ----------------------------------------------------- holonomic heuristic (AStar)
+  // AStar::update_visted + Grid2D::update_costs (AStar.cpp:209-218, Grid2D.cpp:219-227)
+  void memoise(T total, const N2<T>* last) {
+    for (const N2<T>* p = last; p; p = p->prev) visited[(size_t)p->x * N + p->y] = 1;
+    for (const N2<T>* p = last; p; p = p->prev) nm_f[(size_t)p->x * N + p->y] = total - p->g;
+  }
+  // AStar::find_path(int, int) (AStar.cpp:100-113) + a_star_search (118-186)
+  T holonomic(int si, int sj) {
+    if (visited[(size_t)si * N + sj]) return nm_f[(size_t)si * N + sj];
+    nm_f[(size_t)si * N + sj] = nm_h[(size_t)si * N + sj];  // Node2D::soft_reset
+    st.astar_searches++;
+    cl2.clear();
+    op2.clear();
+    op2.insert(N2<T>{si, sj, 0, nm_f[(size_t)si * N + sj], nullptr});
+    while (!op2.empty()) {
+      auto it = op2.begin();
+      const N2<T>* cur = &*cl2.insert(*it).first;
+      op2.erase(it);
+      st.astar_pops++;
+      if (cur->x == astar_goal.x && cur->y == astar_goal.y) {
+        astar_goal = *cur;
+        memoise(astar_goal.f, &astar_goal);
+        return astar_goal.f;
+      }
+      const T g0 = cur->g;
+      for (size_t k = 0; k < act_dx.size(); ++k) {
+        int i = cur->x + act_dx[k], j = cur->y + act_dy[k];
+        if (!inside(i, j) || !(occ[(size_t)i * N + j] < thr)) continue;  // Grid2D::get_neighbors
+        const size_t c = (size_t)i * N + j;
+        if (visited[c]) {
+          T tot = nm_f[c] + g0 + act_cost[k];
+          memoise(tot, cur);
+          return tot;
+        }
+        N2<T> probe{i, j, 0, nm_f[c], nullptr};
+        if (cl2.find(probe) != cl2.end()) continue;
+        auto hit = op2.find(probe);
+        const T gn = g0 + act_cost[k];
+        if (hit == op2.end()) {
+          nm_f[c] = gn + nm_h[c];  // Node2D::set_accumulated_cost
+          op2.insert(N2<T>{i, j, gn, nm_f[c], cur});
+        } else if (gn < hit->g) {
+          op2.erase(hit);
+          nm_f[c] = gn + nm_h[c];
+          op2.insert(N2<T>{i, j, gn, nm_f[c], cur});
+        }
+      }
+    }
+    return std::numeric_limits<T>::max();
+  }
+
+  // -------------------------------------------------------------- successors
+  // Grid3D::get_field_intensity (Grid3D.cpp:206-227)
+  T field(const P3<T>& p) const {
+    T acc = static_cast<T>(0.0);
+    for (const Apf& o : apf) {
+      T d = std::hypot(o.x - p.x, o.y - p.y);
+      T ang = std::abs(wrap_pi<T>(p.h - std::atan2(o.y - p.y, o.x - p.x)));
+      ang = stl_max<T>(apf_ang - ang, static_cast<T>(0.0));
+      T fp = 0;
+      if (d < o.r) {
+        double t = 1.0 / d - 1.0 / o.r;
+        fp = apf_rep * (t * t);  // std::pow(t, 2) is folded to t*t by GCC
+        fp = fp * ang / apf_ang;
+      }
+      acc = acc + fp;
+    }
+    return acc;
+  }
+  // VehicleModel::get_neighbors (VehicleModel.cpp:63-105) + Grid3D filter (Grid3D.cpp:47-74)
+  bool expand(const N3<T>& nd, std::vector<N3<T>>& out) {
+    out.clear();
+    int size = mv.nsteer;
+    int lo = nd.ci - mv.na;
+    lo = lo < 0 ? 0 : lo;
+    const bool slow = nd.vmin < static_cast<T>(1.0);
+    for (int i = lo; i < lo + 2 * mv.na + 1 && i < size; ++i) {
+      T vm = 0;
+      if (!slow) {
+        T lat = nd.vmin * mv.curv_abs[i];
+        if (lat > mv.a_lat) continue;
+        T al = std::sqrt(1.0 - ((lat * lat) / mv.a_lat2));
+        vm = nd.vmin - 2 * al * mv.ts;
+      }
+      const P2<T>& o = mv.offset(i, nd.bin);
+      N3<T> s;
+      s.pose = {nd.pose.x + o.x, nd.pose.y + o.y, wrap_pi<T>(nd.pose.h + mv.dth[i])};
+      s.g = nd.g + mv.cost[i];
+      s.f = s.g;
+      s.vmin = vm;
+      s.ci = i;
+      s.bin = heading_bin<T>(s.pose.h, mv.prec);
+      s.prev = &nd;
+      int ci = static_cast<int>(s.pose.x / res), cj = static_cast<int>(s.pose.y / res);
+      if (!(inside(ci, cj) && occ[(size_t)ci * N + cj] < thr)) continue;
+      T fc = field(s.pose);
+      s.g += fc;
+      s.f += fc;
+      s.cx = ci;
+      s.cy = cj;
+      out.push_back(s);
+    }
+    st.successors += (long long)out.size();
+    return slow;
+  }
+  // Grid3D::check_path (Grid3D.cpp:78-93)
+  bool free_path(const std::vector<P3<T>>& path) const {
+    for (const auto& q : path) {
+      int i = static_cast<int>(std::round(q.x / res)), j = static_cast<int>(std::round(q.y / res));
+      if (!inside(i, j) || occ[(size_t)i * N + j] >= thr) return false;
+    }
+    return true;
+  }
+
+  // ----------------------------------------------------------------- search
+  // HybridAStar::hybrid_a_star_search (HybridAStar.cpp:93-199)
+  std::pair<T, bool> search(const N3<T>& start) {
+    int counter = 0, interval = shot_interval;
+    bool shot_allowed = false;
+    shot_ok = false;
+    cl3.clear();
+    op3.clear();
+    op3.insert(start);
+    std::vector<N3<T>> nb;
+    uint64_t dig = 0x243f6a8885a308d3ull;
+    std::pair<T, bool> out{std::numeric_limits<T>::max(), false};
+    while (!op3.empty()) {
+      auto it = op3.begin();
+      const N3<T>* cur = &*cl3.insert(*it).first;
+      op3.erase(it);
+      st.pops++;
+      dig = mix64(dig ^ (((uint64_t)(uint32_t)cur->cx << 40) | ((uint64_t)(uint32_t)cur->cy << 16) |
+                         (uint64_t)(uint32_t)cur->bin)) + f32bits((float)cur->g);
+      if (cur->cx == goal_node.cx && cur->cy == goal_node.cy) {
+        terminal = *cur;
+        out = {terminal.g, true};
+        break;
+      }
+      if (shot_allowed) {
+        if (++counter == interval) {
+          st.shots++;
+          auto pr = dub.path(cur->pose, goal_node.pose, shot_path, shot_curv);
+          if (!pr.second && free_path(shot_path)) {
+            terminal = *cur->prev;
+            shot_ok = true;
+            out = {cur->g + pr.first, true};
+            break;
+          }
+          counter = 0;
+          interval = std::max(interval - shot_decay, 50);
+        }
+      }
+      shot_allowed = expand(*cur, nb);
+      for (auto& s : nb) {
+        if (cl3.find(s) != cl3.end()) continue;
+        auto hit = op3.find(s);
+        if (hit == op3.end()) {
+          T h1 = holonomic(s.cx, s.cy);
+          T h2 = dub.shortest(s.pose, goal_node.pose);
+          s.f += stl_max(h1, h2);
+          s.prev = cur;
+          op3.insert(s);
+        } else if (s.g < hit->g) {
+          op3.erase(hit);
+          T h1 = holonomic(s.cx, s.cy);
+          T h2 = dub.shortest(s.pose, goal_node.pose);
+          s.f += stl_max(h1, h2);
+          s.prev = cur;
+          op3.insert(s);
+        }
+      }
+    }
+    st.pop_digest = dig;
+    st.closed_size = (long long)cl3.size();
+    uint64_t cd = 0;
+    for (const auto& n : cl3)
+      cd += mix64(((uint64_t)(uint32_t)n.cx << 40) | ((uint64_t)(uint32_t)n.cy << 16) | (uint64_t)(uint32_t)n.bin);
+    st.closed_digest = cd;
+    st.via_shot = shot_ok ? 1 : 0;
+    return out;
+  }
+  // HybridAStar::find_path (HybridAStar.cpp:68-88) incl. Grid3D::set_start_node (127-160)
+  // and reconstruct_path (208-262).  Appends to empty path/curv vectors.
+  std::pair<T, bool> find_path(T vel, const P3<T>& start, std::vector<P3<T>>& path, std::vector<T>& curv) {
+    st = hastar_stats{};
+    P3<T> rel = rot3<T>(P3<T>{start.x - goal3.x, start.y - goal3.y, start.h}, grid_heading);
+    P3<T> pose{rel.x + n45 * res, rel.y + n2 * res, rel.h};
+    int i = static_cast<int>(pose.x / res), j = static_cast<int>(pose.y / res);
+    N3<T> s{};
+    if (inside(i, j)) {
+      nm_f[(size_t)i * N + j] = nm_h[(size_t)i * N + j];
+      s.pose = pose;
+      s.cx = i;
+      s.cy = j;
+    } else {
+      nm_f[0] = nm_h[0];
+      s.pose = {0, 0, 0};
+      s.cx = 0;
+      s.cy = 0;
+    }
+    s.ci = mv.nsteer / 2;
+    s.bin = heading_bin<T>(s.pose.h, mv.prec);
+    s.vmin = vel * vel;
+    s.f = std::numeric_limits<T>::max();
+    s.prev = nullptr;
+    auto res_pair = search(s);
+    if (res_pair.second) {
+      const P3<T> gg = goal_node.pose;
+      curv.push_back(static_cast<T>(0));
+      if (shot_ok) {
+        size_t D = shot_path.size();
+        path.resize(D);
+        curv.resize(D + 1);
+        for (size_t k = 0; k < D; ++k) {
+          size_t q = D - k - 1;
+          P3<T> p = rot3<T>(P3<T>{shot_path[q].x - gg.x, shot_path[q].y - gg.y, shot_path[q].h}, -grid_heading);
+          p.x += goal3.x;
+          p.y += goal3.y;
+          path[k] = p;
+          curv[k + 1] = shot_curv[q];
+        }
+      }
+      for (const N3<T>* n = &terminal; n; n = n->prev) {
+        P3<T> p = rot3<T>(P3<T>{n->pose.x - gg.x, n->pose.y - gg.y, n->pose.h}, -grid_heading);
+        p.x += goal3.x;
+        p.y += goal3.y;
+        path.push_back(p);
+        curv.push_back(mv.curv_abs[n->ci]);
+      }
+      curv.pop_back();
+    }
+    return res_pair;
+  }
+};
+
+}  // namespace orc
+
+// =================================================================== C interface
+using OP = orc::Planner<float>;
+
+extern "C" {
+
+void* orc_create(const hastar_params* p) { return new OP(*p); }
+void orc_destroy(void* h) { delete static_cast<OP*>(h); }
+void orc_update_goal(void* h, const float g[3], const float s[3]) {
+  static_cast<OP*>(h)->update_goal({g[0], g[1], g[2]}, {s[0], s[1], s[2]});
+}
+void orc_reset(void* h) { static_cast<OP*>(h)->reset(); }
+void orc_update_boxes(void* h, const float* b, const float* c, int n, float r) {
+  static_cast<OP*>(h)->boxes(b, c, n, r);
+}
+void orc_update_lines(void* h, const float* l, const float* c, int n, float w) {
+  static_cast<OP*>(h)->lines(l, c, n, w);
+}
+void orc_decay(void* h) { static_cast<OP*>(h)->decay(); }
+void orc_get_obstacles(void* h, float* out) {
+  auto* P = static_cast<OP*>(h);
+  std::memcpy(out, P->occ.data(), P->occ.size() * sizeof(float));
+}
+void orc_get_memo(void* h, float* f_out, unsigned char* visited_out) {
+  auto* P = static_cast<OP*>(h);
+  std::memcpy(f_out, P->nm_f.data(), P->nm_f.size() * sizeof(float));
+  std::memcpy(visited_out, P->visited.data(), P->visited.size());
+}
+int orc_apf_count(void* h) { return (int)static_cast<OP*>(h)->apf.size(); }
+void orc_get_apf(void* h, float* out) {
+  auto* P = static_cast<OP*>(h);
+  for (size_t k = 0; k < P->apf.size(); ++k) {
+    out[3 * k] = P->apf[k].x;
+    out[3 * k + 1] = P->apf[k].y;
+    out[3 * k + 2] = P->apf[k].r;
+  }
+}
+// Returns 0 or HASTAR_ENOSPC (then *len = required length).
+int orc_find_path(void* h, float vel, const float start[3], float* xyh, float* curv, int cap, int* len,
+                  float* cost, int* ok, hastar_stats* stats, double* wall_ms) {
+  auto* P = static_cast<OP*>(h);
+  std::vector<orc::P3<float>> path;
+  std::vector<float> cv;
+  auto t0 = std::chrono::steady_clock::now();
+  auto r = P->find_path(vel, {start[0], start[1], start[2]}, path, cv);
+  auto t1 = std::chrono::steady_clock::now();
+  if (wall_ms) *wall_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  *cost = r.first;
+  *ok = r.second ? 1 : 0;
+  if (stats) *stats = P->st;
+  *len = (int)path.size();
+  if ((int)path.size() > cap) return HASTAR_ENOSPC;
+  for (size_t k = 0; k < path.size(); ++k) {
+    xyh[3 * k] = path[k].x;
+    xyh[3 * k + 1] = path[k].y;
+    xyh[3 * k + 2] = path[k].h;
+    curv[k] = cv[k];
+  }
+  return 0;
+}
+// Closed-set keys (cx, cy, bin) of the last search, sorted; returns the count.
+int orc_closed_keys(void* h, int* out, int cap) {
+  auto* P = static_cast<OP*>(h);
+  std::vector<long long> k;
+  for (const auto& n : P->cl3) k.push_back(((long long)n.cx << 40) | ((long long)n.cy << 16) | n.bin);
+  std::sort(k.begin(), k.end());
+  int n = (int)k.size();
+  for (int i = 0; i < n && i < cap; ++i) {
+    out[3 * i] = (int)(k[i] >> 40);
+    out[3 * i + 1] = (int)((k[i] >> 16) & 0xffffff);
+    out[3 * i + 2] = (int)(k[i] & 0xffff);
+  }
+  return n;
+}
+
+// ---- unit-level hooks (the GPU library exposes the same operations as test kernels)
+// Motion-primitive tables: off (nsteer x (bins+1) x 2), dth, cost, curv_abs; returns precision.
+float orc_motion_tables(void* h, float* off, float* dth, float* cost, float* curv_abs) {
+  auto* P = static_cast<OP*>(h);
+  const auto& m = P->mv;
+  for (size_t k = 0; k < m.off.size(); ++k) {
+    off[2 * k] = m.off[k].x;
+    off[2 * k + 1] = m.off[k].y;
+  }
+  for (int i = 0; i < m.nsteer; ++i) {
+    dth[i] = m.dth[i];
+    cost[i] = m.cost[i];
+    curv_abs[i] = m.curv_abs[i];
+  }
+  return m.prec;
+}
+float orc_min_radius(void* h) { return static_cast<OP*>(h)->dub.r; }
+// APF field of n poses (xyh) against the planner's current obstacle list.
+void orc_field(void* h, const float* xyh, int n, float* out) {
+  auto* P = static_cast<OP*>(h);
+  for (int k = 0; k < n; ++k) out[k] = P->field({xyh[3 * k], xyh[3 * k + 1], xyh[3 * k + 2]});
+}
+// Dubins shortest length of n start poses to one goal pose (float).
+void orc_dubins_len(float r_min, float step, const float* starts, int n, const float goal[3], float* out,
+                    int* word) {
+  orc::DubinsCSC<float> d(r_min, step);
+  for (int k = 0; k < n; ++k) {
+    out[k] = d.shortest({starts[3 * k], starts[3 * k + 1], starts[3 * k + 2]}, {goal[0], goal[1], goal[2]});
+    if (word) word[k] = d.word;
+  }
+}
+// Dubins sampled path (double, golden vector utils/dubins_paths.py:6).
+int orc_dubins_path_d(double r_min, double step, const double s[3], const double g[3], double* xyh, int cap,
+                      double* length, int* word) {
+  orc::DubinsCSC<double> d(r_min, step);
+  std::vector<orc::P3<double>> p;
+  std::vector<double> c;
+  auto r = d.path({s[0], s[1], s[2]}, {g[0], g[1], g[2]}, p, c);
+  *length = r.first;
+  *word = d.word;
+  int n = (int)p.size();
+  for (int k = 0; k < n && k < cap; ++k) {
+    xyh[3 * k] = p[k].x;
+    xyh[3 * k + 1] = p[k].y;
+    xyh[3 * k + 2] = p[k].h;
+  }
+  return n;
+}
+// Dubins sampled path (float) for the shot kernel parity test.
+int orc_dubins_path_f(float r_min, float step, const float s[3], const float g[3], float* xyh, float* curv,
+                      int cap, float* length, int* first_arc_gt_90) {
+  orc::DubinsCSC<float> d(r_min, step);
+  std::vector<orc::P3<float>> p;
+  std::vector<float> c;
+  auto r = d.path({s[0], s[1], s[2]}, {g[0], g[1], g[2]}, p, c);
+  *length = r.first;
+  *first_arc_gt_90 = r.second ? 1 : 0;
+  int n = (int)p.size();
+  for (int k = 0; k < n && k < cap; ++k) {
+    xyh[3 * k] = p[k].x;
+    xyh[3 * k + 1] = p[k].y;
+    xyh[3 * k + 2] = p[k].h;
+    curv[k] = c[k];
+  }
+  return n;
+}
+// VehicleModel<double>::simulate_action chain (golden vector utils/vehicle_mode.py:12;
+// VehicleModel.cpp:108-136; inputs of utils/vehicle_dubins/test_vehicle_dubins.cpp:61-67).
+int orc_vehicle_chain_d(double ts, double a_lat, double wheelbase, double rear_to_cg, int bins, int na,
+                        const double* steer, const double* w, int nsteer, double vmin0, int ci0,
+                        const int* actions, int nact, double* xy_out) {
+  std::vector<double> sv(steer, steer + nsteer), wv(w, w + nsteer);
+  orc::Motion<double> m(ts, a_lat, wheelbase, rear_to_cg, bins, na, sv, wv);
+  double x = 0, y = 0, h = 0, vmin = vmin0;
+  int bin = orc::heading_bin<double>(0.0, 5.0 * M_PI / 180.0);
+  (void)ci0;
+  xy_out[0] = x;
+  xy_out[1] = y;
+  int n = 1;
+  for (int k = 0; k < nact; ++k) {
+    int a = actions[k];
+    double vm = 0;
+    if (vmin > 1.0) {
+      double lat = vmin * m.curv_abs[a];
+      if (lat > m.a_lat) break;
+      double al = std::sqrt(1.0 - ((lat * lat) / m.a_lat2));
+      vm = vmin - 2 * al * m.ts;
+    }
+    const auto& o = m.offset(a, bin);
+    x = x + o.x;
+    y = y + o.y;
+    h = orc::wrap_pi<double>(h + m.dth[a]);
+    bin = orc::heading_bin<double>(h, m.prec);
+    vmin = vm;
+    xy_out[2 * n] = x;
+    xy_out[2 * n + 1] = y;
+    ++n;
+  }
+  return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,200 @@
+"""ctypes wrapper of oracle/build/libhastar_oracle.so — TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as
+the checker.  The product (path_planning_pkg_amd) never imports this module.
+"""
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+from path_planning_pkg_amd.capi import HastarStats, fptr, iptr
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "build" / "libhastar_oracle.so"
+_lib = None
+
+
+def build(force=False):
+    if force or not LIB.exists() or LIB.stat().st_mtime < (HERE / "hastar_oracle.cpp").stat().st_mtime:
+        subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        L = C.CDLL(str(LIB))
+        vp, fp, ip, dp = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int), C.POINTER(C.c_double)
+        L.orc_create.restype = vp
+        L.orc_create.argtypes = [C.c_void_p]
+        for name in ("orc_destroy", "orc_reset", "orc_decay"):
+            getattr(L, name).argtypes = [vp]
+        L.orc_update_goal.argtypes = [vp, fp, fp]
+        L.orc_update_boxes.argtypes = [vp, fp, fp, C.c_int, C.c_float]
+        L.orc_update_lines.argtypes = [vp, fp, fp, C.c_int, C.c_float]
+        L.orc_get_obstacles.argtypes = [vp, fp]
+        L.orc_get_memo.argtypes = [vp, fp, C.POINTER(C.c_ubyte)]
+        L.orc_apf_count.argtypes = [vp]
+        L.orc_get_apf.argtypes = [vp, fp]
+        L.orc_find_path.argtypes = [vp, C.c_float, fp, fp, fp, C.c_int, ip, fp, ip, C.POINTER(HastarStats), dp]
+        L.orc_closed_keys.argtypes = [vp, ip, C.c_int]
+        L.orc_motion_tables.restype = C.c_float
+        L.orc_motion_tables.argtypes = [vp, fp, fp, fp, fp]
+        L.orc_min_radius.restype = C.c_float
+        L.orc_min_radius.argtypes = [vp]
+        L.orc_field.argtypes = [vp, fp, C.c_int, fp]
+        L.orc_dubins_len.argtypes = [C.c_float, C.c_float, fp, C.c_int, fp, fp, ip]
+        L.orc_dubins_path_d.argtypes = [C.c_double, C.c_double, dp, dp, dp, C.c_int, dp, ip]
+        L.orc_dubins_path_f.argtypes = [C.c_float, C.c_float, fp, fp, fp, fp, C.c_int, fp, ip]
+        L.orc_vehicle_chain_d.argtypes = [C.c_double, C.c_double, C.c_double, C.c_double, C.c_int, C.c_int,
+                                          dp, dp, C.c_int, C.c_double, C.c_int, ip, C.c_int, dp]
+        _lib = L
+    return _lib
+
+
+def _f32(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if shape is not None:
+        a = a.reshape(shape)
+    return a
+
+
+class OraclePlanner:
+    """CPU restatement of planning::HybridAStar<float> (same method names)."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self._params = cfg.struct()
+        self.N = cfg.grid_size
+        self.h = lib().orc_create(C.byref(self._params))
+
+    def close(self):
+        if self.h:
+            lib().orc_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def update_goal(self, goal, start):
+        lib().orc_update_goal(self.h, fptr(_f32(goal)), fptr(_f32(start)))
+
+    def reset(self):
+        lib().orc_reset(self.h)
+
+    def update_boxes(self, boxes, conf, apf_added_radius):
+        b = _f32(boxes, (-1, 4))
+        c = _f32(conf)
+        lib().orc_update_boxes(self.h, fptr(b), fptr(c), len(b), apf_added_radius)
+
+    def update_lines(self, lines, conf, width):
+        l = _f32(lines, (-1, 4))
+        c = _f32(conf)
+        lib().orc_update_lines(self.h, fptr(l), fptr(c), len(l), width)
+
+    def decay(self):
+        lib().orc_decay(self.h)
+
+    def get_obstacles(self):
+        out = np.empty((self.N, self.N), np.float32)
+        lib().orc_get_obstacles(self.h, fptr(out))
+        return out
+
+    def get_memo(self):
+        f = np.empty((self.N, self.N), np.float32)
+        v = np.empty((self.N, self.N), np.uint8)
+        lib().orc_get_memo(self.h, fptr(f), v.ctypes.data_as(C.POINTER(C.c_ubyte)))
+        return f, v
+
+    def apf(self):
+        n = lib().orc_apf_count(self.h)
+        out = np.empty((n, 3), np.float32)
+        if n:
+            lib().orc_get_apf(self.h, fptr(out))
+        return out
+
+    def find_path(self, vel, start, cap=1 << 16):
+        xyh = np.empty((cap, 3), np.float32)
+        curv = np.empty(cap, np.float32)
+        ln, ok = C.c_int(0), C.c_int(0)
+        cost = C.c_float(0)
+        st = HastarStats()
+        wall = C.c_double(0)
+        rc = lib().orc_find_path(self.h, vel, fptr(_f32(start)), fptr(xyh), fptr(curv), cap, C.byref(ln),
+                                 C.byref(cost), C.byref(ok), C.byref(st), C.byref(wall))
+        if rc != 0:
+            raise RuntimeError(f"oracle find_path rc={rc} len={ln.value}")
+        n = ln.value
+        return dict(cost=cost.value, ok=bool(ok.value), path=xyh[:n].copy(), curvature=curv[:n].copy(),
+                    stats=st.as_dict(), wall_ms=wall.value)
+
+    def closed_keys(self, cap=1 << 20):
+        out = np.empty((cap, 3), np.int32)
+        n = lib().orc_closed_keys(self.h, iptr(out), cap)
+        return out[:min(n, cap)].copy()
+
+    def motion_tables(self):
+        ns = len(self.cfg.steering)
+        bins = self.cfg.values["num_angle_bins"]
+        off = np.empty((ns, bins + 1, 2), np.float32)
+        dth = np.empty(ns, np.float32)
+        cost = np.empty(ns, np.float32)
+        ca = np.empty(ns, np.float32)
+        prec = lib().orc_motion_tables(self.h, fptr(off), fptr(dth), fptr(cost), fptr(ca))
+        return dict(offsets=off, dtheta=dth, cost=cost, curv_abs=ca, precision=prec)
+
+    def min_radius(self):
+        return lib().orc_min_radius(self.h)
+
+    def field(self, poses):
+        p = _f32(poses, (-1, 3))
+        out = np.empty(len(p), np.float32)
+        lib().orc_field(self.h, fptr(p), len(p), fptr(out))
+        return out
+
+
+def dubins_len(r_min, step, starts, goal):
+    s = _f32(starts, (-1, 3))
+    out = np.empty(len(s), np.float32)
+    word = np.empty(len(s), np.int32)
+    lib().orc_dubins_len(r_min, step, fptr(s), len(s), fptr(_f32(goal)), fptr(out), iptr(word))
+    return out, word
+
+
+def dubins_path_f(r_min, step, start, goal, cap=1 << 16):
+    xyh = np.empty((cap, 3), np.float32)
+    curv = np.empty(cap, np.float32)
+    length = C.c_float(0)
+    flag = C.c_int(0)
+    n = lib().orc_dubins_path_f(r_min, step, fptr(_f32(start)), fptr(_f32(goal)), fptr(xyh), fptr(curv), cap,
+                                C.byref(length), C.byref(flag))
+    return xyh[:n].copy(), curv[:n].copy(), length.value, bool(flag.value)
+
+
+def dubins_path_d(r_min, step, start, goal, cap=4096):
+    dp = C.POINTER(C.c_double)
+    out = np.empty((cap, 3), np.float64)
+    length = C.c_double(0)
+    word = C.c_int(0)
+    s = np.ascontiguousarray(start, np.float64)
+    g = np.ascontiguousarray(goal, np.float64)
+    n = lib().orc_dubins_path_d(r_min, step, s.ctypes.data_as(dp), g.ctypes.data_as(dp), out.ctypes.data_as(dp),
+                                cap, C.byref(length), C.byref(word))
+    return out[:n].copy(), length.value, word.value
+
+
+def vehicle_chain_d(ts, a_lat, wheelbase, rear_to_cg, bins, na, steering, weights, vmin0, ci0, actions):
+    dp = C.POINTER(C.c_double)
+    st = np.ascontiguousarray(steering, np.float64)
+    w = np.ascontiguousarray(weights, np.float64)
+    acts = np.ascontiguousarray(actions, np.int32)
+    out = np.empty((len(acts) + 1, 2), np.float64)
+    n = lib().orc_vehicle_chain_d(ts, a_lat, wheelbase, rear_to_cg, bins, na, st.ctypes.data_as(dp),
+                                  w.ctypes.data_as(dp), len(st), vmin0, ci0, iptr(acts), len(acts),
+                                  out.ctypes.data_as(dp))
+    return out[:n].copy()
+
+

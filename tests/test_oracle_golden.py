@@ -1,0 +1,60 @@
+"""The CPU oracle against the reference's own known-answer vectors.
+
+These pin the oracle: utils/hybrid_astar/plot.py:47-51, utils/dubins_paths.py:6 and
+utils/vehicle_mode.py:12 were printed by the reference with ostream's default %g; we
+compare at that precision, element by element.
+"""
+import json
+import math
+
+import numpy as np
+
+from tests.scenarios import GOLDEN, drive, harness
+
+
+def g6(v):
+    return float("%g" % v)
+
+
+def test_harness_path_matches_plot_py(oracle_lib):
+    cfg, proto, gold = harness()
+    o = oracle_lib.OraclePlanner(cfg)
+    drive(o, proto)
+    r = o.find_path(proto["vel"], proto["start"])
+    assert r["ok"]
+    assert "%g" % r["cost"] == "33.0305"
+    mine = [[g6(v) for v in row] for row in r["path"][::-1]]   # harness prints path.rbegin()..rend()
+    assert mine == gold["path_start_to_goal"]
+    assert len(r["curvature"]) == len(r["path"])
+
+
+def test_dubins_rsl_matches_dubins_paths_py(oracle_lib):
+    g = json.loads((GOLDEN / "dubins_rsl.json").read_text())
+    ms = 30.0 * math.pi / 180.0
+    beta = math.atan2(1.1 * math.tan(ms), 2.269)
+    rmin = 2.269 / (math.tan(ms) * math.cos(beta))
+    path, length, word = oracle_lib.dubins_path_d(rmin, 0.5, [0.0, 0.0, 0.0], [20.0, -20.0, math.pi / 2])
+    assert word == 1  # RSL
+    assert "%g" % rmin == "4.08106"
+    assert [[g6(v) for v in row] for row in path.tolist()] == g["path"]
+
+
+def test_vehicle_chain_matches_vehicle_mode_py(oracle_lib):
+    g = json.loads((GOLDEN / "vehicle_chain.json").read_text())
+    st = [d * math.pi / 180.0 for d in g["steering_deg"]]
+    pos = oracle_lib.vehicle_chain_d(0.5, 4.0, 2.269, 1.1, 72, 1, st, [0.0] * 7, 16.0, 3, g["actions"])
+    assert [[g6(v) for v in row] for row in pos.tolist()] == g["positions"]
+
+
+def test_equal_f_insert_is_dropped(oracle_lib):
+    """utils/node3D/test_node3D.cpp:29-65 semantics: the reference comparator drops equal-f
+    inserts; reproduced indirectly — the harness closed set is smaller than its pops."""
+    cfg, proto, _ = harness()
+    o = oracle_lib.OraclePlanner(cfg)
+    drive(o, proto)
+    r = o.find_path(proto["vel"], proto["start"])
+    st = r["stats"]
+    assert st["closed_size"] <= st["pops"]
+    keys = o.closed_keys()
+    assert len(keys) == st["closed_size"]
+    assert len({tuple(k) for k in keys.tolist()}) == len(keys)
