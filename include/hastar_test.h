@@ -1,0 +1,34 @@
+/* hastar_test.h — unit-level test and debug hooks of libhastar_amd.so.
+ *
+ * Not part of the reference's interface: these let the parity tests compare one
+ * building block at a time (libm ports, APF field, Dubins length/sampling, motion
+ * tables, memo and closed set) between the GPU and the CPU oracle.
+ */
+#ifndef PATH_PLANNING_PKG_AMD_HASTAR_TEST_H
+#define PATH_PLANNING_PKG_AMD_HASTAR_TEST_H
+#include "hastar.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* fn: 0 sinf, 1 cosf, 2 atan2f(a, b), 3 acosf, 4 hypotf(a, b), 5 wrap_pi, 6 heading index(a, prec b), 7 atanf */
+int hastar_test_math(int fn, const float* a, const float* b, float* out, int n);
+/* Grid3D::get_field_intensity of n poses (x, y, heading) against the handle's obstacle list. */
+int hastar_test_field(hastar_handle h, const float* poses, int n, float* out);
+/* Dubins::get_shortest_path_length of n start poses to one goal; word = 0 RSR, 1 RSL, 2 LSR, 3 LSL. */
+int hastar_test_dubins_len(float r_min, const float* starts, int n, const float goal[3], float* out, int* word);
+/* Dubins::get_shortest_path from start to the handle's goal pose (grid frame), sampled. */
+int hastar_test_dubins_path(hastar_handle h, const float start[3], float* xyh, float* curv, int cap, int* n,
+                            float* length, int* first_arc_gt_90);
+/* Copies of the device state. */
+int hastar_debug_memo(hastar_handle h, float* f_out, unsigned char* visited_out);
+int hastar_debug_apf(hastar_handle h, float* out, int cap);
+int hastar_debug_motion(hastar_handle h, float* off, float* dth, float* cost, float* curv_abs, float* prec,
+                        float* r_min);
+int hastar_debug_closed_keys(hastar_handle h, int* out, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -897,3 +897,21 @@ int orc_vehicle_chain_d(double ts, double a_lat, double wheelbase, double rear_t
 }
 
 }  // extern "C"
+
+// glibc reference values for the GPU libm-port test (fn numbering of hastar_test_math).
+extern "C" void orc_libm(int fn, const float* a, const float* b, float* out, int n) {
+  for (int i = 0; i < n; ++i) {
+    float v = 0.0f;
+    switch (fn) {
+      case 0: v = std::sin(a[i]); break;
+      case 1: v = std::cos(a[i]); break;
+      case 2: v = std::atan2(a[i], b[i]); break;
+      case 3: v = std::acos(a[i]); break;
+      case 4: v = std::hypot(a[i], b[i]); break;
+      case 5: v = orc::wrap_pi<float>(a[i]); break;
+      case 6: v = (float)orc::heading_bin<float>(a[i], b[i]); break;
+      default: v = std::atan(a[i]); break;
+    }
+    out[i] = v;
+  }
+}

@@ -52,6 +52,7 @@ def lib():
         L.orc_dubins_path_f.argtypes = [C.c_float, C.c_float, fp, fp, fp, fp, C.c_int, fp, ip]
         L.orc_vehicle_chain_d.argtypes = [C.c_double, C.c_double, C.c_double, C.c_double, C.c_int, C.c_int,
                                           dp, dp, C.c_int, C.c_double, C.c_int, ip, C.c_int, dp]
+        L.orc_libm.argtypes = [C.c_int, fp, fp, fp, C.c_int]
         _lib = L
     return _lib
 
@@ -198,3 +199,12 @@ def vehicle_chain_d(ts, a_lat, wheelbase, rear_to_cg, bins, na, steering, weight
     return out[:n].copy()
 
 
+
+
+def libm(fn, a, b=None):
+    """glibc values of the function numbered as in hastar_test_math."""
+    a = _f32(a)
+    bb = _f32(b) if b is not None else a
+    out = np.empty_like(a)
+    lib().orc_libm(fn, fptr(a), fptr(bb), fptr(out), len(a))
+    return out

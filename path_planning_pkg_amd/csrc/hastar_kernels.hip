@@ -1,0 +1,740 @@
+// hastar_kernels.hip — HIP kernels of the MI355X Hybrid A* planner (gfx950).
+//
+//   hastar_search_kernel   one wavefront (64 lanes) per planner: the reference's
+//                          sequential best-first loop (HybridAStar.cpp:93-199) with its
+//                          data-parallel inner work spread over the lanes:
+//                          successor APF fields (lanes over obstacles), the 4 Dubins
+//                          words of every successor, the holonomic A* neighbour probes,
+//                          Dubins-shot sampling + collision check, path reconstruction.
+//                          Throughput = many planners per launch (thousands of waves).
+//   map kernels            the HBM-bound O(N^2) upkeep of Grid2D/Grid3D: decay,
+//                          relocation (rotate + scatter), box/line rasterisation,
+//                          node-map (heuristic) initialisation.
+//   test kernels           unit-level hooks used by the parity tests.
+#include <hip/hip_runtime.h>
+#include "hastar_device.h"
+#include "hastar_kernels.h"
+
+namespace hastar {
+
+constexpr int MAXS = 16;   // max steering actions (checked at create)
+
+struct Succ {
+  float x, y, h, g, vmin;
+  int ci, bin, cx, cy;
+  float dub;
+};
+
+struct SearchCtx {
+  PlannerDev P;
+  int lane;
+  RBTree<Node3> o3;
+  RBTree<Node2> o2;
+  PoolState ps3, ps2;
+  int n_closed3, n_closed2;
+  uint32_t gen3, gen2;
+  long long pops, succ, apops, asearch, shots;
+  int status;
+};
+
+// ---------------------------------------------------------------- closed sets --------
+__device__ __forceinline__ uint32_t slot_hash(uint32_t k) {
+  k ^= k >> 16;
+  k *= 0x7feb352du;
+  k ^= k >> 15;
+  k *= 0x846ca68bu;
+  k ^= k >> 16;
+  return k;
+}
+
+// unordered_set<Node3D>::insert(*it).first (HybridAStar.cpp:110): existing record or a new
+// copy of the popped open node.
+__device__ int closed3_insert(SearchCtx& c, const Node3& n) {
+  const PlannerDev& P = c.P;
+  uint32_t h = slot_hash(n.key) & P.slots3_mask;
+  for (;;) {
+    Slot3* s = &P.slots3[h];
+    if (s->gen != c.gen3) {
+      if (c.n_closed3 >= P.closed3_cap) return NIL;
+      const int idx = c.n_closed3++;
+      Closed3* r = &P.closed3[idx];
+      r->key = n.key;
+      r->g = n.g;
+      r->f = n.f;
+      r->vmin = n.vmin;
+      r->x = n.x;
+      r->y = n.y;
+      r->h = n.h;
+      r->ci = n.ci;
+      r->prev = n.prev;
+      s->key = n.key;
+      s->idx = idx;
+      s->gen = c.gen3;
+      return idx;
+    }
+    if (s->key == n.key) return s->idx;
+    h = (h + 1) & P.slots3_mask;
+  }
+}
+
+__device__ bool closed3_contains(const SearchCtx& c, uint32_t key) {
+  const PlannerDev& P = c.P;
+  uint32_t h = slot_hash(key) & P.slots3_mask;
+  for (;;) {
+    const Slot3 s = P.slots3[h];
+    if (s.gen != c.gen3) return false;
+    if (s.key == key) return true;
+    h = (h + 1) & P.slots3_mask;
+  }
+}
+
+// -------------------------------------------------------- holonomic A* (AStar.cpp) -----
+// AStar::update_visted + Grid2D::update_costs (AStar.cpp:209-218, Grid2D.cpp:219-227)
+__device__ void memoise(SearchCtx& c, float total, int from) {
+  const PlannerDev& P = c.P;
+  for (int i = from; i != NIL; i = P.closed2[i].prev) {
+    const Closed2 r = P.closed2[i];
+    const size_t cell = (size_t)(r.key >> 16) * P.N + (r.key & 0xffffu);
+    P.visited[cell] = 1;
+    P.nm_f[cell] = total - r.g;
+  }
+}
+
+__device__ __forceinline__ bool insert2(SearchCtx& c, uint32_t key, float f, float g, int prev) {
+  bool left;
+  const int pos = c.o2.insert_pos(key, f, &left);
+  if (pos == -2) return true;  // equal-f "duplicate": dropped like std::set::insert
+  const int n = pool_alloc(c.P.open2, c.ps2, c.P.open2_cap);
+  if (n == NIL) return false;
+  Node2* d = &c.P.open2[n];
+  d->key = key;
+  d->f = f;
+  d->g = g;
+  d->prev = prev;
+  c.o2.link(left, n, pos);
+  return true;
+}
+
+// AStar::find_path(int, int) (AStar.cpp:100-113) + a_star_search (AStar.cpp:118-186)
+__device__ float holonomic(SearchCtx& c, int si, int sj) {
+  const PlannerDev& P = c.P;
+  const int lane = c.lane;
+  const size_t s_cell = (size_t)si * P.N + sj;
+  if (P.visited[s_cell]) return P.nm_f[s_cell];
+  const float h0 = euclid_h(P, si, sj);
+  P.nm_f[s_cell] = h0;  // Grid2D::set_start_node_grid -> Node2D::soft_reset
+  c.asearch++;
+  c.gen2++;
+  c.n_closed2 = 0;
+  c.o2.clear();
+  c.ps2.next = 1;
+  c.ps2.free = NIL;
+  if (!insert2(c, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL)) {
+    c.status = -75;
+    return FLT_MAX;
+  }
+  const int nact = P.diag ? 8 : 4;
+  // this lane's action (AStar actions, Grid2D.cpp:22-40)
+  int adx = 0, ady = 0;
+  float acost = 0.0f;
+  if (P.diag) {
+    const int tx[8] = {0, 1, 1, 1, 0, -1, -1, -1}, ty[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
+    if (lane < 8) {
+      adx = tx[lane];
+      ady = ty[lane];
+      acost = (adx != 0 && ady != 0) ? P.act_cost_diag : P.act_cost_axis;
+    }
+  } else {
+    const int tx[4] = {0, 1, 0, -1}, ty[4] = {-1, 0, 1, 0};
+    if (lane < 4) {
+      adx = tx[lane];
+      ady = ty[lane];
+      acost = P.act_cost_axis;
+    }
+  }
+  while (!c.o2.empty()) {
+    const int b = c.o2.begin();
+    const Node2 top = P.open2[b];
+    const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
+    const size_t tcell = (size_t)tx * P.N + ty;
+    int ci;
+    if (P.cgen2[tcell] == c.gen2) {
+      ci = P.cidx2[tcell];  // duplicate pop: the old closed element is expanded
+    } else {
+      if (c.n_closed2 >= P.closed2_cap) {
+        c.status = -75;
+        return FLT_MAX;
+      }
+      ci = c.n_closed2++;
+      Closed2* r = &P.closed2[ci];
+      r->key = top.key;
+      r->g = top.g;
+      r->f = top.f;
+      r->prev = top.prev;
+      P.cgen2[tcell] = c.gen2;
+      P.cidx2[tcell] = ci;
+    }
+    c.o2.unlink(b);
+    pool_free(P.open2, c.ps2, b);
+    c.apops++;
+    const Closed2 cur = P.closed2[ci];
+    const int cx = (int)(cur.key >> 16), cy = (int)(cur.key & 0xffffu);
+    if (cx == P.goal_cx && cy == P.goal_cy) {
+      memoise(c, cur.f, ci);
+      return cur.f;
+    }
+    const float g0 = cur.g;
+    // neighbour probes in parallel: lane k evaluates action k (Grid2D::get_neighbors)
+    const int ni = cx + adx, nj = cy + ady;
+    bool valid = false, vis = false;
+    float nf = 0.0f;
+    if (lane < nact && ni > -1 && ni < P.N && nj > -1 && nj < P.N) {
+      const size_t cell = (size_t)ni * P.N + nj;
+      if (P.occ[cell] < P.thr) {
+        valid = true;
+        vis = P.visited[cell] != 0;
+        nf = P.nm_f[cell];
+      }
+    }
+    const uint64_t vmask = __ballot(valid);
+    for (int k = 0; k < nact; ++k) {
+      if (!((vmask >> k) & 1ull)) continue;
+      const int ki = shfl_i(ni, k), kj = shfl_i(nj, k);
+      const bool kvis = shfl_i((int)vis, k) != 0;
+      const float kcost = shfl_f(acost, k);
+      const size_t cell = (size_t)ki * P.N + kj;
+      if (kvis) {
+        const float tot = shfl_f(nf, k) + g0 + kcost;
+        memoise(c, tot, ci);
+        return tot;
+      }
+      if (P.cgen2[cell] == c.gen2) continue;        // in the closed set
+      const uint32_t key = ((uint32_t)ki << 16) | (uint32_t)kj;
+      const float fprobe = P.nm_f[cell];           // stale _node_map f, as the reference
+      const int hit = c.o2.find(key, fprobe);
+      const float gn = g0 + kcost;
+      if (hit == 0) {
+        const float fn = gn + euclid_h(P, ki, kj);
+        P.nm_f[cell] = fn;                         // Node2D::set_accumulated_cost
+        if (!insert2(c, key, fn, gn, ci)) { c.status = -75; return FLT_MAX; }
+      } else if (gn < P.open2[hit].g) {
+        c.o2.unlink(hit);
+        pool_free(P.open2, c.ps2, hit);
+        const float fn = gn + euclid_h(P, ki, kj);
+        P.nm_f[cell] = fn;
+        if (!insert2(c, key, fn, gn, ci)) { c.status = -75; return FLT_MAX; }
+      }
+    }
+  }
+  return FLT_MAX;
+}
+
+__device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, int prev) {
+  bool left;
+  const uint32_t key = key3(s.cx, s.cy, s.bin);
+  const int pos = c.o3.insert_pos(key, f, &left);
+  if (pos == -2) return true;
+  const int n = pool_alloc(c.P.open3, c.ps3, c.P.open3_cap);
+  if (n == NIL) return false;
+  Node3* d = &c.P.open3[n];
+  d->key = key;
+  d->f = f;
+  d->g = s.g;
+  d->vmin = s.vmin;
+  d->x = s.x;
+  d->y = s.y;
+  d->h = s.h;
+  d->ci = s.ci;
+  d->prev = prev;
+  c.o3.link(left, n, pos);
+  return true;
+}
+
+// ------------------------------------------------------------------- the search -------
+__global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners,
+                                                           int max_pops) {
+  if ((int)blockIdx.x >= n_planners) return;
+  __shared__ Succ sl[MAXS];
+  SearchCtx c;
+  c.P = descs[blockIdx.x];
+  const PlannerDev& P = c.P;
+  const int lane = threadIdx.x;
+  c.lane = lane;
+  c.o3.t = P.open3;
+  c.o2.t = P.open2;
+  c.gen3 = P.gens[0] + 1;
+  c.gen2 = P.gens[1];
+  c.n_closed3 = 0;
+  c.n_closed2 = 0;
+  c.pops = c.succ = c.apops = c.asearch = c.shots = 0;
+  c.status = 0;
+  c.o3.clear();
+  c.ps3.next = 1;
+  c.ps3.free = NIL;
+
+  // Grid3D::set_start_node soft-resets the start cell's node (Grid3D.cpp:145-148 / 153-154)
+  P.nm_f[(size_t)P.start_cx * P.N + P.start_cy] = euclid_h(P, P.start_cx, P.start_cy);
+  {
+    Succ s0;
+    s0.x = P.start_x;
+    s0.y = P.start_y;
+    s0.h = P.start_h;
+    s0.g = 0.0f;
+    s0.vmin = P.start_vmin;
+    s0.ci = P.start_ci;
+    s0.bin = P.start_bin;
+    s0.cx = P.start_cx;
+    s0.cy = P.start_cy;
+    insert3(c, s0, FLT_MAX, NIL);
+  }
+  // goal circles are the same for every Dubins evaluation of this search
+  const float r = P.r_min;
+  int counter = 0, interval = P.shot_interval;
+  bool shot_allowed = false;
+  uint64_t dig = 0x243f6a8885a308d3ull;
+  int ok = 0, via_shot = 0, terminal = NIL, dub_n = 0;
+  float cost = FLT_MAX;
+  const int span = 2 * P.na + 1;
+
+  while (!c.o3.empty()) {
+    if (c.pops >= max_pops) { c.status = -75; break; }
+    const int b = c.o3.begin();
+    const Node3 top = P.open3[b];
+    const int ci = closed3_insert(c, top);
+    if (ci == NIL) { c.status = -75; break; }
+    c.o3.unlink(b);
+    pool_free(P.open3, c.ps3, b);
+    c.pops++;
+    const Closed3 cur = P.closed3[ci];
+    const int cx = key3_x(cur.key), cy = key3_y(cur.key), cbin = key3_bin(cur.key);
+    dig = mix64(dig ^ digest_key(cur.key)) + (uint64_t)fbits(cur.g);
+    // goal test: Node3D::operator== compares the cell only (Node3D.h:42)
+    if (cx == P.goal_cx && cy == P.goal_cy) {
+      terminal = ci;
+      cost = cur.g;
+      ok = 1;
+      break;
+    }
+    if (shot_allowed) {
+      if (++counter == interval) {
+        c.shots++;
+        int word = 0;
+        float prm[4];
+        // Dubins::get_shortest_path (Dubins.cpp:125-153)
+        const float L = dubins_shortest(r, cur.x, cur.y, cur.h, P.goal_x, P.goal_y, P.goal_h, &word, prm);
+        const Centres C = dubins_centres(r, cur.x, cur.y, cur.h, P.goal_x, P.goal_y, P.goal_h);
+        const int n = dubins_sample(P, C, word, prm, P.dub_xyh, P.dub_curv, P.dub_cap, lane);
+        if (n < 0) { c.status = -75; break; }
+        __syncthreads();
+        const bool first_arc_long = fabsf(prm[1]) > (float)M_PI_2;
+        if (!first_arc_long && path_is_free(P, P.dub_xyh, n, lane)) {
+          terminal = cur.prev;
+          cost = cur.g + L;
+          ok = 1;
+          via_shot = 1;
+          dub_n = n;
+          break;
+        }
+        counter = 0;
+        interval = max(interval - P.shot_decay, 50);
+      }
+    }
+    // ---- successors: VehicleModel::get_neighbors (VehicleModel.cpp:63-105) + Grid3D filter
+    shot_allowed = cur.vmin < 1.0f;
+    int lo = cur.ci - P.na;
+    lo = lo < 0 ? 0 : lo;
+    int ns = 0;
+    for (int i = lo; i < lo + span && i < P.nsteer; ++i) {
+      float vm = 0.0f;
+      if (!shot_allowed) {
+        const float lat = cur.vmin * P.curv_abs[i];
+        if (lat > P.a_lat) continue;
+        const float al = (float)sqrt(1.0 - (double)((lat * lat) / P.a_lat2));
+        vm = cur.vmin - 2.0f * al * P.ts;
+      }
+      const float* o = &P.off[2 * ((size_t)i * (P.bins + 1) + cbin)];
+      Succ s;
+      s.x = cur.x + o[0];
+      s.y = cur.y + o[1];
+      s.h = wrap_pi_f(cur.h + P.dth[i]);
+      s.g = cur.g + P.act_cost[i];
+      s.vmin = vm;
+      s.ci = i;
+      s.bin = heading_bin(s.h, P.prec);
+      s.cx = trunc_f(s.x / P.res);
+      s.cy = trunc_f(s.y / P.res);
+      if (!(s.cx > -1 && s.cx < P.N && s.cy > -1 && s.cy < P.N)) continue;
+      if (!(P.occ[(size_t)s.cx * P.N + s.cy] < P.thr)) continue;
+      s.dub = 0.0f;
+      if (lane == 0) sl[ns] = s;
+      ++ns;
+    }
+    __syncthreads();
+    c.succ += ns;
+    // APF field of every kept successor (lanes over obstacles)
+    for (int q = 0; q < ns; ++q) {
+      const float fc = apf_field(P, sl[q].x, sl[q].y, sl[q].h, lane);
+      __syncthreads();
+      if (lane == 0) sl[q].g = sl[q].g + fc;
+      __syncthreads();
+    }
+    // Dubins lengths: lane = 4 * successor + word
+    {
+      const int q = lane >> 2, w = lane & 3;
+      float len = 0.0f;
+      if (q < ns) {
+        const Centres C = dubins_centres(r, sl[q].x, sl[q].y, sl[q].h, P.goal_x, P.goal_y, P.goal_h);
+        float prm[4];
+        len = dubins_word(w, r, C, sl[q].h, P.goal_h, prm);
+      }
+      for (int s = 0; s < ns; ++s) {
+        float best = shfl_f(len, 4 * s);
+        for (int w2 = 1; w2 < 4; ++w2) {
+          const float v = shfl_f(len, 4 * s + w2);
+          if (v < best) best = v;
+        }
+        if (lane == 0) sl[s].dub = best;
+      }
+    }
+    __syncthreads();
+    // ---- HybridAStar.cpp:159-193
+    bool fail = false;
+    for (int q = 0; q < ns; ++q) {
+      const Succ s = sl[q];
+      const uint32_t key = key3(s.cx, s.cy, s.bin);
+      if (closed3_contains(c, key)) continue;
+      const int hit = c.o3.find(key, s.g);  // f == g before the heuristic is added
+      if (hit == 0) {
+        const float h1 = holonomic(c, s.cx, s.cy);
+        const float f = s.g + stl_max(h1, s.dub);
+        if (!insert3(c, s, f, ci)) { fail = true; break; }
+      } else if (s.g < P.open3[hit].g) {
+        c.o3.unlink(hit);
+        pool_free(P.open3, c.ps3, hit);
+        const float h1 = holonomic(c, s.cx, s.cy);
+        const float f = s.g + stl_max(h1, s.dub);
+        if (!insert3(c, s, f, ci)) { fail = true; break; }
+      }
+      if (c.status != 0) break;
+    }
+    __syncthreads();
+    if (fail) c.status = -75;
+    if (c.status != 0) break;
+  }
+  if (c.status != 0) ok = 0;
+
+  // ---- reconstruct_path (HybridAStar.cpp:208-262) into out_xyh / out_curv
+  int path_len = 0;
+  if (ok) {
+    int L = 0;
+    for (int i = terminal; i != NIL; i = P.closed3[i].prev) {
+      if (dub_n + L >= P.out_cap) { c.status = -28; break; }
+      if (lane == 0) P.out_chain[L] = i;
+      ++L;
+    }
+    __syncthreads();
+    if (c.status == 0) {
+      const float cs = P.rot_c, sn = P.rot_s, ang = -P.grid_heading;
+      path_len = dub_n + L;
+      for (int k = lane; k < path_len; k += 64) {
+        float px, py, ph, kc = 0.0f;
+        bool has_curv = true;
+        if (k < dub_n) {
+          const int q = dub_n - 1 - k;
+          px = P.dub_xyh[3 * q];
+          py = P.dub_xyh[3 * q + 1];
+          ph = P.dub_xyh[3 * q + 2];
+          kc = P.dub_curv[q];
+        } else {
+          const int m = k - dub_n;
+          const Closed3 nd = P.closed3[P.out_chain[m]];
+          px = nd.x;
+          py = nd.y;
+          ph = nd.h;
+          kc = P.curv_abs[nd.ci];
+          has_curv = (m < L - 1);
+        }
+        const float x0 = px - P.goal_x, y0 = py - P.goal_y;
+        float xr = x0 * cs + y0 * sn;
+        float yr = -x0 * sn + y0 * cs;
+        const float hr = wrap_pi_f(ph - ang);
+        xr += P.world_goal_x;
+        yr += P.world_goal_y;
+        P.out_xyh[3 * k] = xr;
+        P.out_xyh[3 * k + 1] = yr;
+        P.out_xyh[3 * k + 2] = hr;
+        if (has_curv) P.out_curv[k + 1] = kc;
+      }
+      if (lane == 0) P.out_curv[0] = 0.0f;
+    } else {
+      ok = 0;
+    }
+  }
+
+  // ---- statistics: closed-set digest (order independent) and counters
+  uint64_t cd = 0;
+  for (int i = lane; i < c.n_closed3; i += 64) cd += mix64(digest_key(P.closed3[i].key));
+  cd = wave_sum_u64(cd);
+  __syncthreads();
+  if (lane == 0) {
+    SearchResult* R = P.result;
+    R->pops = c.pops;
+    R->successors = c.succ;
+    R->astar_pops = c.apops;
+    R->astar_searches = c.asearch;
+    R->shots = c.shots;
+    R->closed_size = c.n_closed3;
+    R->pop_digest = dig;
+    R->closed_digest = cd;
+    R->ok = ok;
+    R->via_shot = via_shot;
+    R->status = c.status;
+    R->path_len = ok ? path_len : 0;
+    R->cost = ok ? cost : FLT_MAX;
+    R->terminal = terminal;
+    R->dubins_len = dub_n;
+    P.gens[0] = c.gen3;
+    P.gens[1] = c.gen2;
+  }
+}
+
+// ------------------------------------------------------------------ map kernels -------
+// Grid2D ctor + compute_heuristic (Grid2D.cpp:7-62, 303-316): _node_map f = h.
+__global__ void k_init_nodemap(PlannerDev P) {
+  const size_t NN = (size_t)P.N * P.N;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t / P.N), j = (int)(t % P.N);
+    P.nm_f[t] = euclid_h(P, i, j);
+  }
+}
+
+// Grid2D::update_obstacles() (Grid2D.cpp:197-208), float4-vectorised.
+__global__ void k_decay(float* __restrict__ occ, size_t NN, float lp_free, float lp_min, float lp_max) {
+  const size_t n4 = NN / 4;
+  float4* o4 = reinterpret_cast<float4*>(occ);
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n4; t += (size_t)gridDim.x * blockDim.x) {
+    float4 v = o4[t];
+    v.x = stl_max(stl_min(v.x + lp_free, lp_max), lp_min);
+    v.y = stl_max(stl_min(v.y + lp_free, lp_max), lp_min);
+    v.z = stl_max(stl_min(v.z + lp_free, lp_max), lp_min);
+    v.w = stl_max(stl_min(v.w + lp_free, lp_max), lp_min);
+    o4[t] = v;
+  }
+  for (size_t t = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x)
+    occ[t] = stl_max(stl_min(occ[t] + lp_free, lp_max), lp_min);
+}
+
+// Grid3D::relocate_obstacles (Grid3D.cpp:169-203), pass 1: every source cell claims its
+// destination; the reference's row-major loop lets the LAST writer win, i.e. the
+// largest linear source index — atomicMax makes that order-independent.
+__global__ void k_relocate_claim(int N, float c, float s, float ox, float oy, int* __restrict__ winner) {
+  const size_t NN = (size_t)N * N;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x) {
+    const float fi = (float)(int)(t / N), fj = (float)(int)(t % N);
+    float x = fi * c + fj * s;
+    float y = -fi * s + fj * c;
+    x = x + ox;
+    y = y + oy;
+    const int a = trunc_f(roundf(x)), b = trunc_f(roundf(y));
+    if (a > -1 && a < N && b > -1 && b < N) atomicMax(&winner[(size_t)a * N + b], (int)t);
+  }
+}
+// pass 2: gather (cells nobody claimed become 0, the fresh map's value)
+__global__ void k_relocate_gather(size_t NN, const float* __restrict__ src, int* __restrict__ winner,
+                                  float* __restrict__ dst) {
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x) {
+    const int w = winner[t];
+    dst[t] = (w >= 0) ? src[w] : 0.0f;
+    winner[t] = -1;
+  }
+}
+
+// Grid2D::update_obstacles(boxes) (Grid2D.cpp:99-139).  Boxes are applied in order (one
+// workgroup walks them); inside one box every sub-sample adds the same delta and clamps,
+// so a cell hit m times gets that step m times — counted with atomics, applied once per
+// cell.  rp: per box {start_i, start_j, 2*end_i, 2*end_j}; dl: per box delta.
+__global__ __launch_bounds__(1024) void k_raster_boxes(float* __restrict__ occ, int* __restrict__ cnt, int N,
+                                                       const int* __restrict__ rp, const float* __restrict__ dl,
+                                                       int nbox, float c, float s, float lp_min, float lp_max) {
+  for (int k = 0; k < nbox; ++k) {
+    const int si = rp[4 * k], sj = rp[4 * k + 1], ni = rp[4 * k + 2], nj = rp[4 * k + 3];
+    const float d = dl[k];
+    const int total = ni * nj;
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int t = threadIdx.x; t < total; t += blockDim.x) {
+        const int i = t / nj, j = t % nj;
+        const float x0 = (float)(i * 0.5), y0 = (float)(j * 0.5);
+        const float x = x0 * c + y0 * s;
+        const float y = -x0 * s + y0 * c;
+        const int ip = si + trunc_f(roundf(x)), jp = sj + trunc_f(roundf(y));
+        if (ip > -1 && ip < N && jp > -1 && jp < N) {
+          const size_t cell = (size_t)ip * N + jp;
+          if (pass == 0) {
+            atomicAdd(&cnt[cell], 1);
+          } else {
+            const int m = atomicExch(&cnt[cell], 0);
+            float v = occ[cell];
+            for (int q = 0; q < m; ++q) {
+              v += d;
+              v = stl_max(stl_min(v, lp_max), lp_min);
+            }
+            if (m) occ[cell] = v;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Grid2D::update_obstacles(lines) (Grid2D.cpp:142-194).  lp: per line {ax, ay, dx, dy,
+// nx, ny, delta, n_len, n_wid}; seq_len / seq_wid: the reference's float-accumulated
+// progress values (prog_length / prog_width) computed on the host.
+__global__ __launch_bounds__(1024) void k_raster_lines(float* __restrict__ occ, int* __restrict__ cnt, int N, int n45,
+                                                       int n2, float res, const float* __restrict__ lp,
+                                                       const float* __restrict__ seq_len,
+                                                       const float* __restrict__ seq_wid, int seq_stride, int nline,
+                                                       float lp_min, float lp_max) {
+  for (int k = 0; k < nline; ++k) {
+    const float* L = lp + 9 * k;
+    const float ax = L[0], ay = L[1], dx = L[2], dy = L[3], nx = L[4], ny = L[5], d = L[6];
+    const int nlen = (int)L[7], nwid = (int)L[8];
+    const float* sl = seq_len + (size_t)k * seq_stride;
+    const int total = nlen * nwid;
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int t = threadIdx.x; t < total; t += blockDim.x) {
+        const int a = t / nwid, b = t % nwid;
+        const float pl = sl[a], pw = seq_wid[b];
+        const float cx = ax + dx * pl, cy = ay + dy * pl;
+        const float p1x = cx + nx * pw, p1y = cy + ny * pw;
+        const float p2x = cx - nx * pw, p2y = cy - ny * pw;
+        const int i1 = trunc_f(roundf(p1x / res)) + n45, i2 = trunc_f(roundf(p2x / res)) + n45;
+        const int j1 = trunc_f(roundf(p1y / res)) + n2, j2 = trunc_f(roundf(p2y / res)) + n2;
+        for (int e = 0; e < 2; ++e) {
+          const int ii = e ? i2 : i1, jj = e ? j2 : j1;
+          if (ii > -1 && ii < N && jj > -1 && jj < N) {
+            const size_t cell = (size_t)ii * N + jj;
+            if (pass == 0) {
+              atomicAdd(&cnt[cell], 1);
+            } else {
+              const int m = atomicExch(&cnt[cell], 0);
+              float v = occ[cell];
+              for (int q = 0; q < m; ++q) {
+                v += d;
+                v = stl_max(stl_min(v, lp_max), lp_min);
+              }
+              if (m) occ[cell] = v;
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------- test kernels -------
+__global__ void k_test_math(int fn, const float* a, const float* b, float* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = 0.0f;
+  switch (fn) {
+    case 0: v = g_sinf(a[i]); break;
+    case 1: v = g_cosf(a[i]); break;
+    case 2: v = g_atan2f(a[i], b[i]); break;
+    case 3: v = g_acosf(a[i]); break;
+    case 4: v = g_hypotf(a[i], b[i]); break;
+    case 5: v = wrap_pi_f(a[i]); break;
+    case 6: v = (float)heading_bin(a[i], b[i]); break;
+    default: v = g_atanf(a[i]); break;
+  }
+  out[i] = v;
+}
+
+__global__ __launch_bounds__(64) void k_test_field(PlannerDev P, const float* poses, int n, float* out) {
+  for (int q = blockIdx.x; q < n; q += gridDim.x) {
+    const float f = apf_field(P, poses[3 * q], poses[3 * q + 1], poses[3 * q + 2], threadIdx.x);
+    if (threadIdx.x == 0) out[q] = f;
+  }
+}
+
+__global__ void k_test_dubins_len(float r, const float* starts, int n, float gx, float gy, float gh, float* out,
+                                  int* word) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int w = 0;
+  float prm[4];
+  out[i] = dubins_shortest(r, starts[3 * i], starts[3 * i + 1], starts[3 * i + 2], gx, gy, gh, &w, prm);
+  word[i] = w;
+}
+
+__global__ __launch_bounds__(64) void k_test_dubins_path(PlannerDev P, float sx, float sy, float sh, float* xyh,
+                                                         float* curv, int cap, int* n_out, float* len_out,
+                                                         int* flag_out) {
+  int word = 0;
+  float prm[4];
+  const float len = dubins_shortest(P.r_min, sx, sy, sh, P.goal_x, P.goal_y, P.goal_h, &word, prm);
+  const Centres C = dubins_centres(P.r_min, sx, sy, sh, P.goal_x, P.goal_y, P.goal_h);
+  const int n = dubins_sample(P, C, word, prm, xyh, curv, cap, threadIdx.x);
+  if (threadIdx.x == 0) {
+    *n_out = n;
+    *len_out = len;
+    *flag_out = fabsf(prm[1]) > (float)M_PI_2;
+  }
+}
+
+// ------------------------------------------------------------- launch wrappers -------
+hipError_t launch_search(const PlannerDev* d_descs, int n, int max_pops, hipStream_t st) {
+  hipLaunchKernelGGL(hastar_search_kernel, dim3(n), dim3(64), 0, st, d_descs, n, max_pops);
+  return hipGetLastError();
+}
+hipError_t launch_init_nodemap(const PlannerDev& P, hipStream_t st) {
+  hipLaunchKernelGGL(k_init_nodemap, dim3(1024), dim3(256), 0, st, P);
+  return hipGetLastError();
+}
+hipError_t launch_decay(float* occ, size_t NN, float fr, float mn, float mx, hipStream_t st) {
+  const int blocks = (int)((NN / 4 + 255) / 256 < 2048 ? (NN / 4 + 255) / 256 + 1 : 2048);
+  hipLaunchKernelGGL(k_decay, dim3(blocks), dim3(256), 0, st, occ, NN, fr, mn, mx);
+  return hipGetLastError();
+}
+hipError_t launch_relocate(int N, float c, float s, float ox, float oy, const float* src, float* dst, int* winner,
+                           hipStream_t st) {
+  const size_t NN = (size_t)N * N;
+  const int blocks = (int)((NN + 255) / 256 < 4096 ? (NN + 255) / 256 : 4096);
+  hipLaunchKernelGGL(k_relocate_claim, dim3(blocks), dim3(256), 0, st, N, c, s, ox, oy, winner);
+  hipLaunchKernelGGL(k_relocate_gather, dim3(blocks), dim3(256), 0, st, NN, src, winner, dst);
+  return hipGetLastError();
+}
+hipError_t launch_raster_boxes(float* occ, int* cnt, int N, const int* rp, const float* dl, int nbox, float c,
+                               float s, float mn, float mx, hipStream_t st) {
+  hipLaunchKernelGGL(k_raster_boxes, dim3(1), dim3(1024), 0, st, occ, cnt, N, rp, dl, nbox, c, s, mn, mx);
+  return hipGetLastError();
+}
+hipError_t launch_raster_lines(float* occ, int* cnt, int N, int n45, int n2, float res, const float* lp,
+                               const float* seq_len, const float* seq_wid, int stride, int nline, float mn, float mx,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(k_raster_lines, dim3(1), dim3(1024), 0, st, occ, cnt, N, n45, n2, res, lp, seq_len, seq_wid,
+                     stride, nline, mn, mx);
+  return hipGetLastError();
+}
+hipError_t launch_test_math(int fn, const float* a, const float* b, float* out, int n, hipStream_t st) {
+  hipLaunchKernelGGL(k_test_math, dim3((n + 255) / 256), dim3(256), 0, st, fn, a, b, out, n);
+  return hipGetLastError();
+}
+hipError_t launch_test_field(const PlannerDev& P, const float* poses, int n, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_test_field, dim3(n < 4096 ? n : 4096), dim3(64), 0, st, P, poses, n, out);
+  return hipGetLastError();
+}
+hipError_t launch_test_dubins_len(float r, const float* starts, int n, float gx, float gy, float gh, float* out,
+                                  int* word, hipStream_t st) {
+  hipLaunchKernelGGL(k_test_dubins_len, dim3((n + 63) / 64), dim3(64), 0, st, r, starts, n, gx, gy, gh, out, word);
+  return hipGetLastError();
+}
+hipError_t launch_test_dubins_path(const PlannerDev& P, float sx, float sy, float sh, float* xyh, float* curv,
+                                   int cap, int* n_out, float* len_out, int* flag_out, hipStream_t st) {
+  hipLaunchKernelGGL(k_test_dubins_path, dim3(1), dim3(64), 0, st, P, sx, sy, sh, xyh, curv, cap, n_out, len_out,
+                     flag_out);
+  return hipGetLastError();
+}
+
+}  // namespace hastar

@@ -1,0 +1,121 @@
+// hastar_layout.h — device-resident state of one planner, shared by the HIP kernels
+// (hastar_kernels.hip) and the host runtime (hastar_capi.cpp).
+//
+// One planner == one reference HybridAStar<float> object (HybridAStar.h:61-74 and the
+// Grid3D/Grid2D/AStar/VehicleModel/Dubins members it owns).  Everything the search
+// touches lives in HBM in flat, index-linked arrays (no pointers inside records), so a
+// batch of planners is just an array of PlannerDev descriptors, one wavefront each.
+#pragma once
+#include <stdint.h>
+
+namespace hastar {
+
+constexpr int NIL = -1;
+constexpr int RB_RED = 0;
+constexpr int RB_BLACK = 1;
+
+// Open-set (std::set<Node3D<float>>, HybridAStar.h:72) tree node.  Index 0 of the pool
+// is the libstdc++ header: p = root, l = leftmost, r = rightmost, color = red.
+// key = cell x << 20 | cell y << 8 | angle bin  (Node3D::operator!=, Node3D.h:44-47).
+struct alignas(16) Node3 {
+  int l, r, p, color;     // tree links (pool indices, NIL = null)
+  uint32_t key;           // (x, y, bin)
+  float f;                // _cost_f: the comparator's order key
+  float g;                // _cost_g
+  float vmin;             // _vmin_sqr
+  float x, y, h;          // _pose2D (grid frame)
+  int ci;                 // _curvature_index
+  int prev;               // closed-record index of the predecessor (NIL for the start)
+  int pad0, pad1, pad2;
+};
+
+// Closed-set record (unordered_set<Node3D>, HybridAStar.h:73-74): a copy of the popped
+// open node.  Records never move, so prev links stay valid like the reference's
+// pointers into the node-based hash set.
+struct alignas(16) Closed3 {
+  uint32_t key;
+  float g, f, vmin;
+  float x, y, h;
+  int ci;
+  int prev;
+  int pad0, pad1, pad2;
+};
+
+// Holonomic A* open-set node (std::set<Node2D<float>>, AStar.h:70).
+// key = x << 16 | y (Node2D::operator!=, Node2D.h:35-38).
+struct alignas(16) Node2 {
+  int l, r, p, color;
+  uint32_t key;
+  float f;
+  float g;
+  int prev;               // index into the A* closed records of the current search
+};
+
+// Holonomic A* closed record (unordered_set<Node2D>, AStar.h:71-72).
+struct alignas(16) Closed2 {
+  uint32_t key;
+  float g, f;
+  int prev;
+};
+
+// Closed-set hash slot (open addressing; generation-stamped so clear() is O(1)).
+struct Slot3 {
+  uint32_t gen;
+  uint32_t key;
+  int idx;
+  int pad;
+};
+
+// Per-search result block (written by the search kernel, read by the host).
+struct SearchResult {
+  long long pops, successors, astar_pops, astar_searches, shots, closed_size;
+  unsigned long long pop_digest, closed_digest;
+  int ok, via_shot, status, path_len;
+  float cost;
+  int terminal;           // closed record index the path is rebuilt from
+  int dubins_len;         // samples of the successful shot
+  int pad;
+};
+
+// Descriptor of one planner: constants + device pointers.  Lives in HBM; the kernel
+// reads it once into scalar registers.
+struct PlannerDev {
+  // --- grid / vehicle constants (Grid2D.cpp:7-62, VehicleModel.cpp:7-47, HybridAStar.cpp:7-24)
+  int N, n2, n45, diag;
+  int bins, nsteer, na, shot_interval;
+  int shot_decay, n_apf, pad_i0, pad_i1;
+  float res, thr, apf_rep, apf_ang;
+  float ts, a_lat, a_lat2, prec;
+  float r_min, step, ang_step, act_cost_diag;   // Dubins radius/step; 2D diagonal move cost
+  float act_cost_axis, pad_f0, pad_f1, pad_f2;
+  // --- goal (grid frame) and world transform for path reconstruction
+  float goal_x, goal_y, goal_h;                // _goal_node._pose2D
+  int goal_cx, goal_cy, goal_bin;
+  float world_goal_x, world_goal_y;            // _goal_location3D
+  float rot_c, rot_s, grid_heading, pad_f3;    // cos/sin(-grid_heading)
+  // --- start node of the next search (Grid3D::set_start_node, Grid3D.cpp:127-160)
+  float start_x, start_y, start_h, start_vmin;
+  int start_cx, start_cy, start_bin, start_ci;
+  // --- state arrays
+  float* occ;            // N*N log-odds (_obstacle_map), row i = x cell
+  float* nm_f;           // N*N Node2D::_cost_f of _node_map (A* memo + stale f)
+  uint8_t* visited;      // N*N AStar::_visted
+  float* apf;            // n_apf x {x, y, r} (Grid3D::_apf_obstacles)
+  float* off;            // nsteer x (bins + 1) x {dx, dy} (VehicleModel::_offset_xy + zero row)
+  float* dth;            // nsteer  _offset_heading
+  float* act_cost;       // nsteer  _actions_cost
+  float* curv_abs;       // nsteer  _abs_curvatures
+  // --- arenas
+  Node3* open3;   int open3_cap;  int pad_a0;
+  Closed3* closed3; int closed3_cap; int pad_a1;
+  Slot3* slots3;  uint32_t slots3_mask; int pad_a7;
+  Node2* open2;   int open2_cap;  int pad_a2;
+  Closed2* closed2; int closed2_cap; int pad_a3;
+  uint32_t* cgen2; int* cidx2;
+  uint32_t* gens;        // [0] closed-set generation, [1] A* closed generation (kernel-owned)
+  float* dub_xyh; float* dub_curv; int dub_cap; int pad_a5;
+  float* out_xyh; float* out_curv; int* out_chain; int out_cap; int pad_a6;
+  SearchResult* result;
+};
+
+}  // namespace hastar

@@ -1,0 +1,237 @@
+"""Python mirror of planning::HybridAStar<float> over the MI355X C ABI (include/hastar.h).
+
+Method names and argument meaning follow the reference class (HybridAStar.h:33-50):
+update_goal, reset, update_obstacles (three overloads, dispatched on arguments),
+get_obstacles, find_path.  find_path returns the reference's (cost, success) pair plus
+the path/curvature lists the reference fills in place, and the search statistics.
+
+There is no CPU implementation behind this class: if libhastar_amd.so or a HIP device is
+missing, construction raises.
+"""
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+from .capi import HastarStats, PlannerConfig, fptr, iptr
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libhastar_amd.so"
+_lib = None
+
+HASTAR_ENOSPC = -28
+HASTAR_EOVERFLOW = -75
+
+
+class HastarError(RuntimeError):
+    def __init__(self, rc, msg):
+        super().__init__(f"hastar rc={rc}: {msg}")
+        self.rc = rc
+
+
+def load_library():
+    """Load libhastar_amd.so (in-tree build).  Raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise FileNotFoundError(f"{LIB_PATH} missing: run __graft_entry__.build() (make -C path_planning_pkg_amd/csrc)")
+    L = C.CDLL(str(LIB_PATH))
+    vp, fp, ip = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int)
+    L.hastar_create_f32.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+    L.hastar_destroy.argtypes = [vp]
+    L.hastar_update_goal.argtypes = [vp, fp, fp]
+    L.hastar_reset.argtypes = [vp]
+    L.hastar_update_boxes.argtypes = [vp, fp, fp, C.c_int, C.c_float]
+    L.hastar_update_lines.argtypes = [vp, fp, fp, C.c_int, C.c_float]
+    L.hastar_decay.argtypes = [vp]
+    L.hastar_find_path.argtypes = [vp, C.c_float, fp, fp, fp, C.c_int, ip, fp, ip, C.POINTER(HastarStats)]
+    L.hastar_copy_path.argtypes = [vp, fp, fp, C.c_int, ip]
+    L.hastar_find_path_batch.argtypes = [C.POINTER(C.c_void_p), C.c_int, fp, fp, fp, fp, C.c_int, ip, fp, ip,
+                                         C.POINTER(HastarStats)]
+    L.hastar_get_obstacles.argtypes = [vp, fp]
+    L.hastar_grid_size.argtypes = [vp]
+    L.hastar_last_error.restype = C.c_char_p
+    L.hastar_last_search_ms.restype = C.c_float
+    L.hastar_test_math.argtypes = [C.c_int, fp, fp, fp, C.c_int]
+    L.hastar_test_field.argtypes = [vp, fp, C.c_int, fp]
+    L.hastar_test_dubins_len.argtypes = [C.c_float, fp, C.c_int, fp, fp, ip]
+    L.hastar_test_dubins_path.argtypes = [vp, fp, fp, fp, C.c_int, ip, fp, ip]
+    L.hastar_debug_memo.argtypes = [vp, fp, C.POINTER(C.c_ubyte)]
+    L.hastar_debug_apf.argtypes = [vp, fp, C.c_int]
+    L.hastar_debug_motion.argtypes = [vp, fp, fp, fp, fp, fp, fp]
+    L.hastar_debug_closed_keys.argtypes = [vp, ip, C.c_int]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc < 0:
+        raise HastarError(rc, load_library().hastar_last_error().decode(errors="replace"))
+    return rc
+
+
+def _f32(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    return a.reshape(shape) if shape is not None else a
+
+
+class HybridAStar:
+    """GPU planner handle with the reference's member functions."""
+
+    def __init__(self, cfg: PlannerConfig, device: int = 0):
+        self.cfg = cfg
+        self._params = cfg.struct()
+        self.N = cfg.grid_size
+        h = C.c_void_p()
+        _check(load_library().hastar_create_f32(C.byref(self._params), device, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            load_library().hastar_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # HybridAStar::update_goal (HybridAStar.cpp:55-59)
+    def update_goal(self, goal, start):
+        _check(load_library().hastar_update_goal(self.h, fptr(_f32(goal)), fptr(_f32(start))))
+
+    # HybridAStar::reset (HybridAStar.cpp:49-52)
+    def reset(self):
+        _check(load_library().hastar_reset(self.h))
+
+    # the three update_obstacles overloads (HybridAStar.cpp:29-46)
+    def update_obstacles(self, items=None, confidence=None, size=None, kind="boxes"):
+        if items is None:
+            return self.decay()
+        if kind == "boxes":
+            return self.update_boxes(items, confidence, size)
+        return self.update_lines(items, confidence, size)
+
+    def update_boxes(self, boxes, confidence, apf_added_radius):
+        b = _f32(boxes, (-1, 4))
+        c = _f32(confidence)
+        _check(load_library().hastar_update_boxes(self.h, fptr(b), fptr(c), len(b), float(apf_added_radius)))
+
+    def update_lines(self, lines, confidence, line_width):
+        l = _f32(lines, (-1, 4))
+        c = _f32(confidence)
+        _check(load_library().hastar_update_lines(self.h, fptr(l), fptr(c), len(l), float(line_width)))
+
+    def decay(self):
+        _check(load_library().hastar_decay(self.h))
+
+    def get_obstacles(self):
+        out = np.empty((self.N, self.N), np.float32)
+        _check(load_library().hastar_get_obstacles(self.h, fptr(out)))
+        return out
+
+    # HybridAStar::find_path (HybridAStar.cpp:68-88)
+    def find_path(self, vel_init, start, cap=4096):
+        L = load_library()
+        st = HastarStats()
+        ln, ok = C.c_int(0), C.c_int(0)
+        cost = C.c_float(0)
+        xyh = np.empty((max(cap, 1), 3), np.float32)
+        curv = np.empty(max(cap, 1), np.float32)
+        rc = L.hastar_find_path(self.h, float(vel_init), fptr(_f32(start)), fptr(xyh), fptr(curv), cap, C.byref(ln),
+                                C.byref(cost), C.byref(ok), C.byref(st))
+        if rc == HASTAR_ENOSPC:
+            cap = ln.value
+            xyh = np.empty((cap, 3), np.float32)
+            curv = np.empty(cap, np.float32)
+            rc = L.hastar_copy_path(self.h, fptr(xyh), fptr(curv), cap, C.byref(ln))
+        _check(rc)
+        n = ln.value
+        return dict(cost=cost.value, ok=bool(ok.value), path=xyh[:n].copy(), curvature=curv[:n].copy(),
+                    stats=st.as_dict())
+
+    # ---- debug / unit hooks (include/hastar_test.h)
+    def memo(self):
+        f = np.empty((self.N, self.N), np.float32)
+        v = np.empty((self.N, self.N), np.uint8)
+        _check(load_library().hastar_debug_memo(self.h, fptr(f), v.ctypes.data_as(C.POINTER(C.c_ubyte))))
+        return f, v
+
+    def apf(self, cap=1 << 16):
+        out = np.empty((cap, 3), np.float32)
+        n = _check(load_library().hastar_debug_apf(self.h, fptr(out), cap))
+        return out[:n].copy()
+
+    def motion_tables(self):
+        ns = len(self.cfg.steering)
+        bins = self.cfg.values["num_angle_bins"]
+        off = np.empty((ns, bins + 1, 2), np.float32)
+        dth, cost, ca = (np.empty(ns, np.float32) for _ in range(3))
+        prec, rmin = C.c_float(0), C.c_float(0)
+        _check(load_library().hastar_debug_motion(self.h, fptr(off), fptr(dth), fptr(cost), fptr(ca), C.byref(prec),
+                                                  C.byref(rmin)))
+        return dict(offsets=off, dtheta=dth, cost=cost, curv_abs=ca, precision=prec.value, r_min=rmin.value)
+
+    def closed_keys(self, cap=1 << 20):
+        out = np.empty((cap, 3), np.int32)
+        n = _check(load_library().hastar_debug_closed_keys(self.h, iptr(out), cap))
+        return out[:min(n, cap)].copy()
+
+    def field(self, poses):
+        p = _f32(poses, (-1, 3))
+        out = np.empty(len(p), np.float32)
+        _check(load_library().hastar_test_field(self.h, fptr(p), len(p), fptr(out)))
+        return out
+
+    def dubins_path(self, start, cap=1 << 15):
+        xyh = np.empty((cap, 3), np.float32)
+        curv = np.empty(cap, np.float32)
+        n, flag = C.c_int(0), C.c_int(0)
+        length = C.c_float(0)
+        _check(load_library().hastar_test_dubins_path(self.h, fptr(_f32(start)), fptr(xyh), fptr(curv), cap,
+                                                      C.byref(n), C.byref(length), C.byref(flag)))
+        k = n.value
+        return xyh[:max(k, 0)].copy(), curv[:max(k, 0)].copy(), length.value, bool(flag.value)
+
+
+def find_path_batch(planners, vels, starts, cap=4096):
+    """hastar_find_path_batch: one launch, one wavefront per planner."""
+    L = load_library()
+    n = len(planners)
+    hs = (C.c_void_p * n)(*[p.h.value for p in planners])
+    v = _f32(vels)
+    s = _f32(starts, (n, 3))
+    xyh = np.empty((n, cap, 3), np.float32)
+    curv = np.empty((n, cap), np.float32)
+    ln = np.zeros(n, np.int32)
+    ok = np.zeros(n, np.int32)
+    cost = np.zeros(n, np.float32)
+    stats = (HastarStats * n)()
+    rc = L.hastar_find_path_batch(hs, n, fptr(v), fptr(s), fptr(xyh), fptr(curv), cap, iptr(ln), fptr(cost),
+                                  iptr(ok), stats)
+    _check(rc)
+    out = []
+    for i in range(n):
+        k = int(ln[i])
+        out.append(dict(cost=float(cost[i]), ok=bool(ok[i]), path=xyh[i, :k].copy(), curvature=curv[i, :k].copy(),
+                        stats=stats[i].as_dict()))
+    return out, float(L.hastar_last_search_ms())
+
+
+def gpu_math(fn, a, b=None):
+    """Evaluate one libm port on the GPU (hastar_test_math)."""
+    a = _f32(a)
+    bb = _f32(b) if b is not None else a
+    out = np.empty_like(a)
+    _check(load_library().hastar_test_math(fn, fptr(a), fptr(bb), fptr(out), len(a)))
+    return out
+
+
+def gpu_dubins_len(r_min, starts, goal):
+    s = _f32(starts, (-1, 3))
+    out = np.empty(len(s), np.float32)
+    word = np.empty(len(s), np.int32)
+    _check(load_library().hastar_test_dubins_len(float(r_min), fptr(s), len(s), fptr(_f32(goal)), fptr(out),
+                                                 iptr(word)))
+    return out, word

@@ -1,0 +1,249 @@
+"""GPU (libhastar_amd.so on gfx950) vs the CPU oracle: bit-exact parity.
+
+Parity bar (north_star + SURVEY.md §8): identical closed-set membership, identical
+goal-reached decision, path cost within 1e-4 relative.  We test a stricter bar: every
+float the planner produces (obstacle map, APF list, memo, path, curvature, cost) is
+bit-identical, and the ordered pop digest (cell, bin, g of every pop) plus the closed-set
+digest are identical, i.e. the GPU replays the reference's exact search trajectory.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from tests.scenarios import drive, harness, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    a = np.ascontiguousarray(a, np.float32)
+    b = a.view(np.uint32).copy()
+    b[np.isnan(a)] = 0x7FC00000  # NaN == NaN regardless of payload
+    return b
+
+
+def assert_bits_equal(x, y, what):
+    bx, by = bits(x), bits(y)
+    assert bx.shape == by.shape, f"{what}: shape {bx.shape} vs {by.shape}"
+    bad = np.nonzero(bx != by)
+    assert len(bad[0]) == 0, f"{what}: {len(bad[0])} mismatches, first at {tuple(i[0] for i in bad)}: " \
+                             f"{np.asarray(x)[tuple(i[0] for i in bad)]} vs {np.asarray(y)[tuple(i[0] for i in bad)]}"
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    from path_planning_pkg_amd import planner
+    planner.load_library()
+    return planner
+
+
+def both(cfg, gpu, oracle_lib):
+    return gpu.HybridAStar(cfg), oracle_lib.OraclePlanner(cfg)
+
+
+def compare_results(rg, ro, what):
+    assert rg["ok"] == ro["ok"], f"{what}: success {rg['ok']} vs {ro['ok']}"
+    assert_bits_equal(np.float32(rg["cost"]), np.float32(ro["cost"]), f"{what} cost")
+    sg, so = rg["stats"], ro["stats"]
+    assert sg["status"] == 0, f"{what}: device status {sg['status']}"
+    for k in ("pops", "successors", "astar_pops", "astar_searches", "shots", "closed_size", "pop_digest",
+              "closed_digest", "via_shot"):
+        assert sg[k] == so[k], f"{what}: stats[{k}] {sg[k]} vs {so[k]}"
+    assert_bits_equal(rg["path"], ro["path"], f"{what} path")
+    assert_bits_equal(rg["curvature"], ro["curvature"], f"{what} curvature")
+
+
+# ------------------------------------------------------------------ building blocks --
+def test_libm_ports_on_gpu(gpu, oracle_lib):
+    rng = np.random.default_rng(7)
+    n = 1 << 20
+    x = rng.uniform(-8, 8, n).astype(np.float32)
+    x[:16] = [0, -0.0, 1e-40, 1e-7, 3.1415927, -3.1415927, 1.5707964, 120.0, -200.5, 1e6, 7.8539818e-01, 2.0,
+              0.5, -0.5, 4.0, 1e30]
+    y = rng.uniform(-8, 8, n).astype(np.float32)
+    u = rng.uniform(-1, 1, n).astype(np.float32)
+    u[:6] = [1.0, -1.0, 0.5, -0.5, 0.0, 2.9e-8]
+    for fn, a, b in ((0, x, None), (1, x, None), (2, y, x), (3, u, None), (4, y, x), (5, x * 2.0, None), (7, x, None)):
+        assert_bits_equal(gpu.gpu_math(fn, a, b), oracle_lib.libm(fn, a, b), f"libm fn {fn}")
+    prec = np.full(n, np.float32(2 * math.pi / 72), np.float32)
+    h = rng.uniform(-3.1416, 3.1416, n).astype(np.float32)
+    h[:4] = [np.float32(math.pi), np.float32(-math.pi), 0.0, np.float32(3.1415925)]
+    assert_bits_equal(gpu.gpu_math(6, h, prec), oracle_lib.libm(6, h, prec), "heading index")
+
+
+def test_motion_tables(gpu, oracle_lib):
+    cfg, _, _ = harness()
+    g, o = both(cfg, gpu, oracle_lib)
+    tg, to = g.motion_tables(), o.motion_tables()
+    for k in ("offsets", "dtheta", "cost", "curv_abs"):
+        assert_bits_equal(tg[k], to[k], k)
+    assert_bits_equal(np.float32(tg["precision"]), np.float32(to["precision"]), "precision")
+    assert_bits_equal(np.float32(tg["r_min"]), np.float32(o.min_radius()), "r_min")
+
+
+def test_map_upkeep_harness(gpu, oracle_lib):
+    cfg, proto, _ = harness()
+    g, o = both(cfg, gpu, oracle_lib)
+    for p in (g, o):
+        p.update_goal(proto["goal"], proto["start"])
+    assert_bits_equal(g.get_obstacles(), o.get_obstacles(), "map after update_goal")
+    for cyc in range(proto["cycles"]):
+        for p in (g, o):
+            p.decay()
+        assert_bits_equal(g.get_obstacles(), o.get_obstacles(), f"map after decay {cyc}")
+        for p in (g, o):
+            p.update_lines(proto["lines"], [proto["line_conf"]] * 4, proto["line_width"])
+        assert_bits_equal(g.get_obstacles(), o.get_obstacles(), f"map after lines {cyc}")
+        for p in (g, o):
+            p.update_boxes(proto["boxes"], [proto["box_conf"]] * 3, proto["apf_r"])
+        assert_bits_equal(g.get_obstacles(), o.get_obstacles(), f"map after boxes {cyc}")
+    assert_bits_equal(g.apf(), o.apf(), "APF list")
+    # a goal change relocates the map (rotate + scatter, Grid3D.cpp:169-203)
+    for p in (g, o):
+        p.update_goal([30.0, 30.0, 0.7], [10.0, 14.0, 0.0])
+    assert_bits_equal(g.get_obstacles(), o.get_obstacles(), "map after relocation")
+
+
+def test_apf_field_and_dubins_units(gpu, oracle_lib):
+    cfg, proto, _ = harness()
+    g, o = both(cfg, gpu, oracle_lib)
+    for p in (g, o):
+        drive(p, proto)
+    rng = np.random.default_rng(3)
+    apf = o.apf()
+    poses = []
+    for ox, oy, r in apf:
+        for _ in range(200):
+            a, d = rng.uniform(0, 2 * math.pi), rng.uniform(0, 1.2 * r)
+            poses.append([ox + d * math.cos(a), oy + d * math.sin(a), rng.uniform(-math.pi, math.pi)])
+    poses = np.array(poses, np.float32)
+    assert_bits_equal(g.field(poses), o.field(poses), "APF field")
+    rmin = o.min_radius()
+    starts = np.stack([rng.uniform(0, 30, 4000), rng.uniform(0, 30, 4000), rng.uniform(-math.pi, math.pi, 4000)],
+                      1).astype(np.float32)
+    goal = [24.0, 15.0, 0.3]
+    lg, wg = gpu.gpu_dubins_len(rmin, starts, goal)
+    lo, wo = oracle_lib.dubins_len(rmin, 0.75, starts, goal)
+    assert_bits_equal(lg, lo, "Dubins length")
+    assert (wg == wo).all()
+    # the handle's goal pose in the grid frame: (n45*res, n2*res, wrap_pi(goal.h - grid_heading))
+    gh = oracle_lib.libm(2, np.float32([36.0 - 18.0]), np.float32([26.0 - 18.0]))[0]
+    goal_grid = [48 * 0.5, 30 * 0.5, float(oracle_lib.libm(5, np.float32([np.float32(0.0) - gh]))[0])]
+    for s in starts[:40]:
+        xg, cg, Lg, fg = g.dubins_path(s)
+        xo, co, Lo, fo = oracle_lib.dubins_path_f(rmin, 0.75, s, goal_grid)
+        assert_bits_equal(np.float32(Lg), np.float32(Lo), "shot length")
+        assert fg == fo
+        assert_bits_equal(xg, xo, "shot samples")
+        assert_bits_equal(cg, co, "shot curvature")
+
+
+# ----------------------------------------------------------------------- full path --
+def test_harness_search_parity_and_golden(gpu, oracle_lib):
+    cfg, proto, gold = harness()
+    g, o = both(cfg, gpu, oracle_lib)
+    for p in (g, o):
+        drive(p, proto)
+    rg = g.find_path(proto["vel"], proto["start"])
+    ro = o.find_path(proto["vel"], proto["start"])
+    compare_results(rg, ro, "harness")
+    assert [[float("%g" % v) for v in row] for row in rg["path"][::-1]] == gold["path_start_to_goal"]
+    fg, vg = g.memo()
+    fo, vo = o.get_memo()
+    assert_bits_equal(fg, fo, "memo f")
+    assert (vg == vo).all()
+    assert (g.closed_keys() == o.closed_keys()).all()
+
+
+@pytest.mark.parametrize("N,bins,K,seed", [(256, 36, 10, s) for s in (1, 2, 3, 4)] + [(512, 72, 50, 1), (512, 72, 50, 2)])
+def test_synthetic_parity(gpu, oracle_lib, N, bins, K, seed):
+    cfg, proto = synthetic(N, bins, K, seed)
+    g, o = both(cfg, gpu, oracle_lib)
+    for p in (g, o):
+        drive(p, proto)
+    assert_bits_equal(g.get_obstacles(), o.get_obstacles(), "map")
+    rg = g.find_path(proto["vel"], proto["start"])
+    ro = o.find_path(proto["vel"], proto["start"])
+    compare_results(rg, ro, f"N{N} K{K} seed{seed}")
+    fg, vg = g.memo()
+    fo, vo = o.get_memo()
+    assert_bits_equal(fg, fo, "memo f")
+    assert (vg == vo).all()
+
+
+def test_replans_without_reset(gpu, oracle_lib):
+    """L3 semantics (local_planner.cpp:204-205,241,316): memo and stale node-map f carry over."""
+    cfg, proto = synthetic(256, 36, 10, 5)
+    g, o = both(cfg, gpu, oracle_lib)
+    for p in (g, o):
+        drive(p, proto)
+    rng = np.random.default_rng(11)
+    boxes = proto["boxes"].copy()
+    start = list(proto["start"])
+    for tick in range(6):
+        r = [p.find_path(2.0, start) for p in (g, o)]
+        compare_results(r[0], r[1], f"tick {tick}")
+        boxes[:, :2] += rng.uniform(-0.2, 0.2, (len(boxes), 2)).astype(np.float32)
+        start[0] += 1.5
+        for p in (g, o):
+            p.decay()
+            p.update_boxes(boxes, [0.75] * len(boxes), 2.5)
+
+
+def test_batch_equals_single(gpu, oracle_lib):
+    cases = [synthetic(256, 36, 10, s) for s in (6, 7, 8)] + [harness()[:2]]
+    planners, oracles = [], []
+    for cfg, proto in cases:
+        g, o = both(cfg, gpu, oracle_lib)
+        drive(g, proto)
+        drive(o, proto)
+        planners.append(g)
+        oracles.append(o)
+    res, ms = gpu.find_path_batch(planners, [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases])
+    assert ms > 0
+    for i, (cfg, proto) in enumerate(cases):
+        compare_results(res[i], oracles[i].find_path(proto["vel"], proto["start"]), f"batch {i}")
+
+
+def test_edge_cases(gpu, oracle_lib):
+    # start outside the grid -> cell (0, 0) with pose (0, 0, 0) (Grid3D.cpp:153-159)
+    cfg, proto = synthetic(128, 36, 4, 9)
+    g, o = both(cfg, gpu, oracle_lib)
+    for p in (g, o):
+        drive(p, proto)
+    far = [-500.0, 300.0, 1.0]
+    compare_results(g.find_path(1.0, far), o.find_path(1.0, far), "start outside")
+    # goal cell fully walled in: search fails on both (small grid, bounded flood)
+    cfg, proto = synthetic(48, 36, 0, 1)
+    proto["boxes"] = np.array([[0.0, 0.0, 4.0, 4.0]], np.float32)
+    proto["start"] = [-14.0, 0.0, 0.0]
+    g, o = both(cfg, gpu, oracle_lib)
+    for p in (g, o):
+        drive(p, proto)
+    rg, ro = g.find_path(2.0, proto["start"]), o.find_path(2.0, proto["start"])
+    compare_results(rg, ro, "blocked goal")
+    assert not rg["ok"]
+    # lines only, no boxes, num_actions = 2, 4-connected holonomic A*
+    from path_planning_pkg_amd.capi import PlannerConfig, steering_from_degrees
+    cfg = PlannerConfig(grid_size=80, num_angle_bins=72, num_actions=2, grid_2d_allow_diag_moves=False,
+                        steering=steering_from_degrees([-30, -20, -10, 0, 10, 20, 30]),
+                        curvature_weights=[0.5, 0.2, 0.1, 0.0, 0.1, 0.2, 0.5])
+    proto = dict(goal=[5.0, 3.0, -0.4], start=[-20.0, -6.0, 0.3], vel=3.0, cycles=3,
+                 lines=np.array([[-10, -10, -10, 2], [-2, 0, 3, 12]], np.float32), line_conf=0.7, line_width=1.0,
+                 boxes=np.zeros((0, 4), np.float32), box_conf=0.75, apf_r=2.5)
+    g, o = both(cfg, gpu, oracle_lib)
+    for p in (g, o):
+        drive(p, proto)
+    assert_bits_equal(g.get_obstacles(), o.get_obstacles(), "lines-only map")
+    compare_results(g.find_path(3.0, proto["start"]), o.find_path(3.0, proto["start"]), "lines only")
+
+
+def test_small_output_buffer(gpu):
+    from path_planning_pkg_amd import planner
+    cfg, proto, _ = harness()
+    g = gpu.HybridAStar(cfg)
+    drive(g, proto)
+    r = g.find_path(proto["vel"], proto["start"], cap=5)   # wrapper retries after HASTAR_ENOSPC
+    assert r["ok"] and len(r["path"]) == 43
+    assert planner.HASTAR_ENOSPC == -28
