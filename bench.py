@@ -1,0 +1,217 @@
+"""bench.py — Hybrid A* node expansions/sec on the 1024x1024x72 grid (BASELINE.json configs[2]).
+
+Workload (one "step"): a batch of B independent planners (SURVEY.md §8d synthetic
+generator: N = 1024, 72 angle bins, K = 200 box obstacles, seed = query id; the reference's
+only motion mode: forward Dubins), each already set up in HBM (update_goal, 5 x {decay,
+boxes}); the step resets the holonomic memo of every planner (HybridAStar::reset) and runs
+ONE batched find_path launch — one wavefront per planner.
+value = total pops of all planners on all ranks / wall time of the K timed steps (max over
+ranks).  One rank per GPU (torch.distributed over RCCL for the barrier/reductions only):
+planners are sharded across ranks with no data-path collective -> weak scaling.
+
+Extra fields: plan latency of a single query (median of single-planner searches),
+roofline of the search kernel (algorithmic bytes of SURVEY.md §8d per launch / kernel time
+from HIP events on the launch stream), and the CPU oracle timed on the host (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(st, K):
+    """B = 40 P + 44 S + 208 A + 12 K per plan."""
+    return 40 * st["pops"] + 44 * st["successors"] + 208 * st["astar_pops"] + 12 * K
+
+
+def build_planners(gpu, cfgs, device):
+    from tests.scenarios import drive
+    planners = []
+    for cfg, proto in cfgs:
+        p = gpu.HybridAStar(cfg, device=device)
+        drive(p, proto)
+        planners.append(p)
+    return planners
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("HASTAR_BENCH_BATCH", "512")),
+                    help="planners (queries) per GPU")
+    ap.add_argument("--grid", type=int, default=1024)
+    ap.add_argument("--bins", type=int, default=72)
+    ap.add_argument("--obstacles", type=int, default=200)
+    ap.add_argument("--max-pops", type=int, default=65536)
+    ap.add_argument("--max-astar-nodes", type=int, default=262144)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-oracle baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--latency-queries", type=int, default=3)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_mod
+        dist = dist_mod
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    device = local_rank
+
+    from path_planning_pkg_amd import planner as gpu
+    from path_planning_pkg_amd.capi import PlannerConfig
+    from tests.scenarios import synthetic
+
+    B = args.batch
+    def cfg_for(q):
+        cfg, proto = synthetic(args.grid, args.bins, args.obstacles, seed=q + 1)
+        cfg.values["max_pops"] = args.max_pops
+        cfg.values["max_astar_nodes"] = args.max_astar_nodes
+        return cfg, proto
+
+    qids = [rank * B + i for i in range(B)]
+    cfgs = [cfg_for(q) for q in qids]
+    t_setup = time.perf_counter()
+    planners = build_planners(gpu, cfgs, device)
+    t_setup = time.perf_counter() - t_setup
+    vels = [c[1]["vel"] for c in cfgs]
+    starts = [c[1]["start"] for c in cfgs]
+
+    def step():
+        for p in planners:
+            p.reset()
+        res, kms = gpu.find_path_batch(planners, vels, starts, cap=8192)
+        return res, kms
+
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    pops = 0
+    kernel_ms = []
+    alg_bytes = []
+    statuses = set()
+    oks = 0
+    last = None
+    for _ in range(args.steps):
+        res, kms = step()
+        kernel_ms.append(kms)
+        pops += sum(r["stats"]["pops"] for r in res)
+        alg_bytes.append(sum(algorithmic_bytes(r["stats"], args.obstacles) for r in res))
+        statuses |= {r["stats"]["status"] for r in res}
+        oks += sum(r["ok"] for r in res)
+        last = res
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed, float(pops), float(sum(kernel_ms))], dtype=torch.float64, device=f"cuda:{device}")
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+        elapsed, pops_all = float(tmax[0]), float(t[1])
+    else:
+        pops_all = float(pops)
+
+    out = None
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = pops_all / elapsed
+        avg_kernel_ms = float(np.mean(kernel_ms))
+        achieved = float(np.mean(alg_bytes)) / (avg_kernel_ms * 1e-3) / 1e9
+        # single-query plan latency (the second half of the metric)
+        lat = []
+        for p, c in list(zip(planners, cfgs))[: args.latency_queries]:
+            p.reset()
+            r, kms = gpu.find_path_batch([p], [c[1]["vel"]], [c[1]["start"]], cap=8192)
+            lat.append(kms)
+        traffic = None
+        pmc = ROOT / "profiles" / "pmc_search_summary.json"
+        if pmc.exists():
+            try:
+                pm = json.loads(pmc.read_text())
+                if pm.get("batch") == B and pm.get("grid") == args.grid:
+                    traffic = pm.get("hbm_bytes_per_launch")
+            except (ValueError, OSError):
+                traffic = None
+        out = {
+            "metric": "Hybrid A* node expansions/sec + plan latency, 1024x1024x72 grid",
+            "value": value,
+            "unit": "expansions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (SURVEY.md §8d generator; seeds = query ids)",
+            "config": {"workload": f"cfg3: {args.grid}x{args.grid}x{args.bins} grid, {args.obstacles} box obstacles, "
+                                   f"batch of {B} independent queries per GPU, forward Dubins",
+                       "grid": args.grid, "angle_bins": args.bins, "obstacles": args.obstacles,
+                       "queries_per_gpu": B, "global_batch": B * world, "parallelism": f"query-sharded x{world}"},
+            "plan_latency_ms": float(np.median(lat)) if lat else None,
+            "pops_per_step": pops_all / args.steps,
+            "success_rate": oks / (B * args.steps),
+            "search_status": sorted(statuses),
+            "setup_s_per_gpu": t_setup,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         "kernel": "hastar_search_kernel", "kernel_ms": avg_kernel_ms,
+                         "alg_bytes_per_launch": float(np.mean(alg_bytes))},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfgs, last, args.cpu_seconds)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    if out is not None:
+        print(json.dumps(out))
+
+
+def cpu_baseline(cfgs, gpu_results, budget_s):
+    """The oracle (CPU restatement, 'port') on the host: single thread, find_path only,
+    as the reference harness times it (test_hybrid_astar.cpp:123-126).  Also re-checks
+    parity of the sampled queries against the GPU results of the last timed step."""
+    from oracle.pyoracle import OraclePlanner
+    from tests.scenarios import drive
+    pops = 0
+    wall = 0.0
+    n = 0
+    parity = True
+    for i, (cfg, proto) in enumerate(cfgs):
+        o = OraclePlanner(cfg)
+        drive(o, proto)
+        r = o.find_path(proto["vel"], proto["start"])
+        pops += r["stats"]["pops"]
+        wall += r["wall_ms"] * 1e-3
+        n += 1
+        g = gpu_results[i]
+        parity &= (r["stats"]["pop_digest"] == g["stats"]["pop_digest"] and r["ok"] == g["ok"]
+                   and np.float32(r["cost"]).tobytes() == np.float32(g["cost"]).tobytes())
+        o.close()
+        if wall >= budget_s:
+            break
+    return {"value": pops / wall if wall > 0 else None, "unit": "expansions/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} queries of the GPU batch, find_path only, 1 thread (oracle/hastar_oracle.cpp)",
+            "mean_plan_ms": wall / n * 1e3 if n else None, "parity_with_gpu": bool(parity)}
+
+
+if __name__ == "__main__":
+    main()

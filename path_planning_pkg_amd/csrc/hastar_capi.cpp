@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "../../include/hastar.h"
@@ -68,6 +69,38 @@ hipError_t dalloc(T** p, size_t n) {
   return hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(n, 1) * sizeof(T));
 }
 
+// Map-update scratch shared by every planner of a device (relocation target + claim
+// table, raster hit counters): N*N floats/ints each, grown to the largest grid seen.
+// Map updates of different handles on one device are serialised by its mutex.
+struct DeviceScratch {
+  std::mutex mu;
+  size_t cap = 0;
+  float* tmp = nullptr;
+  int* winner = nullptr;  // kept at -1 between uses
+  int* cnt = nullptr;     // kept at 0 between uses
+};
+DeviceScratch g_scratch[64];
+
+int scratch_acquire(int dev, size_t NN, hipStream_t st, DeviceScratch** out) {
+  DeviceScratch& S = g_scratch[dev & 63];
+  if (S.cap < NN) {
+    if (S.tmp) hipFree(S.tmp);
+    if (S.winner) hipFree(S.winner);
+    if (S.cnt) hipFree(S.cnt);
+    S.tmp = nullptr;
+    S.winner = S.cnt = nullptr;
+    S.cap = 0;
+    if (dalloc(&S.tmp, NN) != hipSuccess || dalloc(&S.winner, NN) != hipSuccess || dalloc(&S.cnt, NN) != hipSuccess)
+      return fail(HASTAR_ENOMEM, "map scratch allocation failed");
+    if (hipMemsetAsync(S.winner, 0xff, NN * sizeof(int), st) != hipSuccess ||
+        hipMemsetAsync(S.cnt, 0, NN * sizeof(int), st) != hipSuccess)
+      return fail(HASTAR_EDEVICE, "map scratch init failed");
+    S.cap = NN;
+  }
+  *out = &S;
+  return 0;
+}
+
 }  // namespace
 
 struct hastar_handle_s {
@@ -83,9 +116,6 @@ struct hastar_handle_s {
   float grid_heading = 0, goal2x = 0, goal2y = 0, goal3x = 0, goal3y = 0, goal3h = 0;
   bool goal_set = false;
   // device buffers not referenced by the descriptor
-  float* occ_tmp = nullptr;
-  int* winner = nullptr;
-  int* cnt = nullptr;
   int apf_cap = 0;
   int* d_rp = nullptr;
   float* d_dl = nullptr;
@@ -242,11 +272,8 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   }
 #define OWN(ptr, n) do { if ((rc = own_alloc(h, &(ptr), (n))) != 0) { free_handle(h); return rc; } } while (0)
   OWN(D.occ, NN);
-  OWN(h->occ_tmp, NN);
   OWN(D.nm_f, NN);
   OWN(D.visited, NN);
-  OWN(h->winner, NN);
-  OWN(h->cnt, NN);
   OWN(D.off, off.size());
   OWN(D.dth, (size_t)ns);
   OWN(D.act_cost, (size_t)ns);
@@ -272,8 +299,6 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   hipStream_t st = h->stream;
   he = hipMemsetAsync(D.occ, 0, NN * sizeof(float), st);
   if (he == hipSuccess) he = hipMemsetAsync(D.visited, 0, NN, st);
-  if (he == hipSuccess) he = hipMemsetAsync(h->winner, 0xff, NN * sizeof(int), st);
-  if (he == hipSuccess) he = hipMemsetAsync(h->cnt, 0, NN * sizeof(int), st);
   if (he == hipSuccess) he = hipMemsetAsync(D.slots3, 0, (size_t)slots * sizeof(Slot3), st);
   if (he == hipSuccess) he = hipMemsetAsync(D.cgen2, 0, NN * sizeof(uint32_t), st);
   if (he == hipSuccess) he = hipMemsetAsync(D.gens, 0, 4 * sizeof(uint32_t), st);
@@ -318,8 +343,15 @@ int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3
   const V2 gno = rot2(g3px - h->goal3x, g3py - h->goal3y, gh);
   V2 org{(float)D.n45 + gno.x / D.res, (float)D.n2 + gno.y / D.res};
   org = {org.x - gp.x, org.y - gp.y};
-  HIPCHK(launch_relocate(D.N, g_cosf(dh), g_sinf(dh), org.x, org.y, D.occ, h->occ_tmp, h->winner, h->stream));
-  std::swap(D.occ, h->occ_tmp);
+  {
+    std::lock_guard<std::mutex> lk(g_scratch[h->device & 63].mu);
+    DeviceScratch* S = nullptr;
+    const size_t NN = (size_t)D.N * D.N;
+    if (int rc = scratch_acquire(h->device, NN, h->stream, &S)) return rc;
+    HIPCHK(launch_relocate(D.N, g_cosf(dh), g_sinf(dh), org.x, org.y, D.occ, S->tmp, S->winner, h->stream));
+    HIPCHK(hipMemcpyAsync(D.occ, S->tmp, NN * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
   // the goal node (Grid3D.cpp:115-123)
   D.goal_x = D.n45 * D.res;
   D.goal_y = D.n2 * D.res;
@@ -404,8 +436,12 @@ int hastar_update_boxes(hastar_handle h, const float* boxes, const float* conf, 
     HIPCHK(hipMemcpyAsync(D.apf, apf.data(), (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->d_rp, rp.data(), (size_t)n * 4 * sizeof(int), hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->d_dl, dl.data(), (size_t)n * sizeof(float), hipMemcpyHostToDevice, h->stream));
-    HIPCHK(launch_raster_boxes(D.occ, h->cnt, D.N, h->d_rp, h->d_dl, n, g_cosf(gh), g_sinf(gh), h->lp_min,
+    std::lock_guard<std::mutex> lk(g_scratch[h->device & 63].mu);
+    DeviceScratch* S = nullptr;
+    if (int rc = scratch_acquire(h->device, (size_t)D.N * D.N, h->stream, &S)) return rc;
+    HIPCHK(launch_raster_boxes(D.occ, S->cnt, D.N, h->d_rp, h->d_dl, n, g_cosf(gh), g_sinf(gh), h->lp_min,
                                h->lp_max, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
   }
   HIPCHK(hipStreamSynchronize(h->stream));
   return HASTAR_OK;
@@ -469,9 +505,14 @@ int hastar_update_lines(hastar_handle h, const float* lines, const float* conf, 
   HIPCHK(hipMemcpyAsync(h->d_seq, seq.data(), seq.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
   if (!wid.empty())
     HIPCHK(hipMemcpyAsync(h->d_wid, wid.data(), wid.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
-  if (!wid.empty())
-    HIPCHK(launch_raster_lines(D.occ, h->cnt, D.N, D.n45, D.n2, D.res, h->d_lp, h->d_seq, h->d_wid, stride, n,
+  if (!wid.empty()) {
+    std::lock_guard<std::mutex> lk(g_scratch[h->device & 63].mu);
+    DeviceScratch* S = nullptr;
+    if (int rc = scratch_acquire(h->device, (size_t)D.N * D.N, h->stream, &S)) return rc;
+    HIPCHK(launch_raster_lines(D.occ, S->cnt, D.N, D.n45, D.n2, D.res, h->d_lp, h->d_seq, h->d_wid, stride, n,
                                h->lp_min, h->lp_max, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
   HIPCHK(hipStreamSynchronize(h->stream));
   return HASTAR_OK;
 }
@@ -721,6 +762,19 @@ int hastar_debug_motion(hastar_handle h, float* off, float* dth, float* cost, fl
   HIPCHK(hipMemcpy(curv_abs, D.curv_abs, ns * sizeof(float), hipMemcpyDeviceToHost));
   *prec = D.prec;
   *r_min = D.r_min;
+  return HASTAR_OK;
+}
+
+int hastar_debug_cycles(hastar_handle h, unsigned long long* out8) {
+  if (!h || !h->have_last) return fail(HASTAR_EINVAL, "no search result");
+  for (int q = 0; q < 8; ++q) out8[q] = h->last.cycles[q];
+  return HASTAR_OK;
+}
+
+int hastar_debug_astar_modes(hastar_handle h, long long* out2) {
+  if (!h || !h->have_last) return fail(HASTAR_EINVAL, "no search result");
+  out2[0] = h->last.astar_migrations;
+  out2[1] = h->last.astar_pops_hbm;
   return HASTAR_OK;
 }
 

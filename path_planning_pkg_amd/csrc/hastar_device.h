@@ -13,6 +13,44 @@
 namespace hastar {
 using namespace gmath;
 
+// Pointers loaded from the descriptor are generic (flat) to the compiler; every access
+// through them would be a flat_load/flat_store with vmcnt+lgkmcnt waits.  They all point
+// to hipMalloc'ed HBM, so the kernels view them as address_space(1) (global).
+#define GAS __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ GAS T* gp(T* p) {
+  return (GAS T*)p;
+}
+// whole-record copies to/from HBM in 16-byte pieces (records are 16-byte aligned)
+typedef int v4i __attribute__((ext_vector_type(4)));
+template <class T>
+__device__ __forceinline__ T gload(const GAS T* p) {
+  static_assert(sizeof(T) % 16 == 0, "record size");
+  union U { T v; v4i q[sizeof(T) / 16]; } u;
+  const GAS v4i* src = (const GAS v4i*)p;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 16); ++i) u.q[i] = src[i];
+  return u.v;
+}
+template <class T>
+__device__ __forceinline__ void gstore(GAS T* p, const T& v) {
+  static_assert(sizeof(T) % 16 == 0, "record size");
+  union U { T v; v4i q[sizeof(T) / 16]; } u;
+  u.v = v;
+  GAS v4i* dst = (GAS v4i*)p;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 16); ++i) dst[i] = u.q[i];
+}
+// the same for LDS / generic pointers
+template <class T>
+__device__ __forceinline__ T gload(const T* p) {
+  return *p;
+}
+template <class T>
+__device__ __forceinline__ void gstore(T* p, const T& v) {
+  *p = v;
+}
+
 // common.h:15-29 for T = float: fmod in double, compare against M_PI in double.
 __device__ __forceinline__ float wrap_pi_f(float a) {
   const float w = (float)fmod_2pi((double)a);
@@ -183,7 +221,8 @@ __device__ __forceinline__ float apf_field(const PlannerDev& P, float px, float 
     float term = 0.0f;
     bool near = false;
     if (k < P.n_apf) {
-      const float ox = P.apf[3 * k], oy = P.apf[3 * k + 1], orad = P.apf[3 * k + 2];
+      const GAS float* apf = gp(P.apf);
+      const float ox = apf[3 * k], oy = apf[3 * k + 1], orad = apf[3 * k + 2];
       const float dx = ox - px, dy = oy - py;
       const float d = g_hypotf(dx, dy);
       if (d < orad) {
@@ -210,8 +249,8 @@ __device__ __forceinline__ float apf_field(const PlannerDev& P, float px, float 
 // Angles and distances accumulate sequentially exactly like the reference loops; each
 // lane keeps the value of its own sample index.  Returns the sample count or -1 when
 // the scratch is too small.
-__device__ inline int dubins_sample(const PlannerDev& P, const Centres& C, int word, const float prm[4], float* xyh,
-                                    float* curv, int cap, int lane) {
+__device__ inline int dubins_sample(const PlannerDev& P, const Centres& C, int word, const float prm[4], GAS float* xyh,
+                                    GAS float* curv, int cap, int lane) {
   const float r = P.r_min, as = P.ang_step, st = P.step;
   const bool s_right = (word == 0 || word == 1), g_right = (word == 0 || word == 2);
   const float csx = s_right ? C.srx : C.slx, csy = s_right ? C.sry : C.sly;
@@ -290,12 +329,12 @@ __device__ inline int dubins_sample(const PlannerDev& P, const Centres& C, int w
 
 // Grid3D::check_path (Grid3D.cpp:78-93), wave-parallel.  Reads samples written by other
 // lanes: caller must order (block barrier) before calling.
-__device__ __forceinline__ bool path_is_free(const PlannerDev& P, const float* xyh, int n, int lane) {
+__device__ __forceinline__ bool path_is_free(const PlannerDev& P, const GAS float* xyh, int n, int lane) {
   bool bad = false;
   for (int i = lane; i < n; i += 64) {
     const int ci = trunc_f(roundf(xyh[3 * i] / P.res));
     const int cj = trunc_f(roundf(xyh[3 * i + 1] / P.res));
-    if (ci < 0 || ci >= P.N || cj < 0 || cj >= P.N || P.occ[(size_t)ci * P.N + cj] >= P.thr) bad = true;
+    if (ci < 0 || ci >= P.N || cj < 0 || cj >= P.N || gp(P.occ)[(size_t)ci * P.N + cj] >= P.thr) bad = true;
   }
   return __ballot(bad) == 0;
 }

@@ -12,12 +12,26 @@
 //                          node-map (heuristic) initialisation.
 //   test kernels           unit-level hooks used by the parity tests.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include "hastar_device.h"
 #include "hastar_kernels.h"
 
 namespace hastar {
 
 constexpr int MAXS = 16;   // max steering actions (checked at create)
+
+// Diagnostic build only (-DHASTAR_STAMPS): cycles per phase of the search loop,
+// 0 pop+closed insert, 1 successors+APF+Dubins, 2 open/closed bookkeeping, 3 holonomic A*,
+// 4 Dubins shot, 5 reconstruct+stats, 6 whole loop.
+#ifdef HASTAR_STAMPS
+#define STAMP_T unsigned long long
+#define STAMP_NOW() __builtin_amdgcn_s_memtime()
+#define STAMP_ADD(slot, t0) (c.cyc[slot] += __builtin_amdgcn_s_memtime() - (t0))
+#else
+#define STAMP_T int
+#define STAMP_NOW() 0
+#define STAMP_ADD(slot, t0) ((void)(t0))
+#endif
 
 struct Succ {
   float x, y, h, g, vmin;
@@ -26,15 +40,17 @@ struct Succ {
 };
 
 struct SearchCtx {
-  PlannerDev P;
+  const PlannerDev* __restrict__ P;   // descriptor in HBM (uniform, read-only: scalar loads)
   int lane;
-  RBTree<Node3> o3;
-  RBTree<Node2> o2;
+  RBTree<Node3, GAS Node3*> o3;
   PoolState ps3, ps2;
   int n_closed3, n_closed2;
   uint32_t gen3, gen2;
-  long long pops, succ, apops, asearch, shots;
+  long long pops, succ, apops, asearch, shots, amigr, apops_g;
   int status;
+#ifdef HASTAR_STAMPS
+  unsigned long long cyc[8];
+#endif
 };
 
 // ---------------------------------------------------------------- closed sets --------
@@ -49,15 +65,15 @@ __device__ __forceinline__ uint32_t slot_hash(uint32_t k) {
 
 // unordered_set<Node3D>::insert(*it).first (HybridAStar.cpp:110): existing record or a new
 // copy of the popped open node.
-__device__ int closed3_insert(SearchCtx& c, const Node3& n) {
-  const PlannerDev& P = c.P;
+__device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n) {
+  const PlannerDev& P = *c.P;
   uint32_t h = slot_hash(n.key) & P.slots3_mask;
   for (;;) {
-    Slot3* s = &P.slots3[h];
+    auto s = &gp(P.slots3)[h];
     if (s->gen != c.gen3) {
       if (c.n_closed3 >= P.closed3_cap) return NIL;
       const int idx = c.n_closed3++;
-      Closed3* r = &P.closed3[idx];
+      auto r = &gp(P.closed3)[idx];
       r->key = n.key;
       r->g = n.g;
       r->f = n.f;
@@ -77,11 +93,11 @@ __device__ int closed3_insert(SearchCtx& c, const Node3& n) {
   }
 }
 
-__device__ bool closed3_contains(const SearchCtx& c, uint32_t key) {
-  const PlannerDev& P = c.P;
+__device__ __forceinline__ bool closed3_contains(const SearchCtx& c, uint32_t key) {
+  const PlannerDev& P = *c.P;
   uint32_t h = slot_hash(key) & P.slots3_mask;
   for (;;) {
-    const Slot3 s = P.slots3[h];
+    const Slot3 s = gload(&gp(P.slots3)[h]);
     if (s.gen != c.gen3) return false;
     if (s.key == key) return true;
     h = (h + 1) & P.slots3_mask;
@@ -89,144 +105,214 @@ __device__ bool closed3_contains(const SearchCtx& c, uint32_t key) {
 }
 
 // -------------------------------------------------------- holonomic A* (AStar.cpp) -----
+// Each lazy A* search (AStar::find_path(int, int), AStar.cpp:100-113) starts with its open
+// tree, closed records and a cell -> closed-record hash in LDS (16 KiB per wavefront).
+// Most searches stop after a few dozen pops at the first memoised neighbour; a search
+// that outgrows LDS is migrated once (same pool indices, plain copies) to the HBM arena
+// and continues there.  Both modes run the same templated loop.
+constexpr int A_CAP = 256;   // LDS open-tree nodes (index 0 = header)
+constexpr int A_CCAP = 256;  // LDS closed records
+constexpr int A_HS = 512;    // LDS hash slots (power of two, load factor <= 1/2)
+
+struct AStarLds {
+  Node2 open[A_CAP];
+  Closed2 closed[A_CCAP];
+  uint32_t hkey[A_HS];  // cell + 1, 0 = empty
+  int hidx[A_HS];
+};
+
+__device__ __forceinline__ uint32_t cell_hash(uint32_t cell) { return (cell * 0x9E3779B1u) >> 23; }  // 9 bits
+
+// returns the closed index of cell or NIL (LDS mode)
+__device__ __forceinline__ int lds_closed_find(const AStarLds& L, uint32_t cell) {
+  uint32_t h = cell_hash(cell) & (A_HS - 1);
+  for (;;) {
+    const uint32_t k = L.hkey[h];
+    if (k == 0) return NIL;
+    if (k == cell + 1) return L.hidx[h];
+    h = (h + 1) & (A_HS - 1);
+  }
+}
+__device__ __forceinline__ void lds_closed_put(AStarLds& L, uint32_t cell, int idx) {
+  uint32_t h = cell_hash(cell) & (A_HS - 1);
+  while (L.hkey[h] != 0) h = (h + 1) & (A_HS - 1);
+  L.hkey[h] = cell + 1;
+  L.hidx[h] = idx;
+}
+
 // AStar::update_visted + Grid2D::update_costs (AStar.cpp:209-218, Grid2D.cpp:219-227)
-__device__ void memoise(SearchCtx& c, float total, int from) {
-  const PlannerDev& P = c.P;
-  for (int i = from; i != NIL; i = P.closed2[i].prev) {
-    const Closed2 r = P.closed2[i];
+template <bool G, class CP>
+__device__ __forceinline__ void memoise(SearchCtx& c, CP cl, float total, int from) {
+  const PlannerDev& P = *c.P;
+  for (int i = from; i != NIL; i = cl[i].prev) {
+    const Closed2 r = gload(&cl[i]);
     const size_t cell = (size_t)(r.key >> 16) * P.N + (r.key & 0xffffu);
-    P.visited[cell] = 1;
-    P.nm_f[cell] = total - r.g;
+    gp(P.visited)[cell] = 1;
+    gp(P.nm_f)[cell] = total - r.g;
   }
 }
 
-__device__ __forceinline__ bool insert2(SearchCtx& c, uint32_t key, float f, float g, int prev) {
+template <class NP>
+__device__ __forceinline__ bool insert2(SearchCtx& c, RBTree<Node2, NP>& tr, int cap, uint32_t key, float f, float g,
+                                        int prev) {
   bool left;
-  const int pos = c.o2.insert_pos(key, f, &left);
+  const int pos = tr.insert_pos(key, f, &left);
   if (pos == -2) return true;  // equal-f "duplicate": dropped like std::set::insert
-  const int n = pool_alloc(c.P.open2, c.ps2, c.P.open2_cap);
+  const int n = pool_alloc(tr.t, c.ps2, cap);
   if (n == NIL) return false;
-  Node2* d = &c.P.open2[n];
+  auto d = &tr.t[n];
   d->key = key;
   d->f = f;
   d->g = g;
   d->prev = prev;
-  c.o2.link(left, n, pos);
+  tr.link(left, n, pos);
   return true;
 }
 
-// AStar::find_path(int, int) (AStar.cpp:100-113) + a_star_search (AStar.cpp:118-186)
-__device__ float holonomic(SearchCtx& c, int si, int sj) {
-  const PlannerDev& P = c.P;
+// The body of AStar::a_star_search (AStar.cpp:118-186).  G = false: LDS mode, returns
+// false (without popping) when the next pop could overflow LDS.  Returns true when the
+// search finished; *result = cost-to-goal or FLT_MAX.
+template <bool G>
+__device__ __forceinline__ bool astar_loop(SearchCtx& c, AStarLds& L, int adx, int ady, float acost, float* result) {
+  const PlannerDev& P = *c.P;
   const int lane = c.lane;
-  const size_t s_cell = (size_t)si * P.N + sj;
-  if (P.visited[s_cell]) return P.nm_f[s_cell];
-  const float h0 = euclid_h(P, si, sj);
-  P.nm_f[s_cell] = h0;  // Grid2D::set_start_node_grid -> Node2D::soft_reset
-  c.asearch++;
-  c.gen2++;
-  c.n_closed2 = 0;
-  c.o2.clear();
-  c.ps2.next = 1;
-  c.ps2.free = NIL;
-  if (!insert2(c, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL)) {
-    c.status = -75;
-    return FLT_MAX;
-  }
   const int nact = P.diag ? 8 : 4;
-  // this lane's action (AStar actions, Grid2D.cpp:22-40)
-  int adx = 0, ady = 0;
-  float acost = 0.0f;
-  if (P.diag) {
-    const int tx[8] = {0, 1, 1, 1, 0, -1, -1, -1}, ty[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
-    if (lane < 8) {
-      adx = tx[lane];
-      ady = ty[lane];
-      acost = (adx != 0 && ady != 0) ? P.act_cost_diag : P.act_cost_axis;
-    }
-  } else {
-    const int tx[4] = {0, 1, 0, -1}, ty[4] = {-1, 0, 1, 0};
-    if (lane < 4) {
-      adx = tx[lane];
-      ady = ty[lane];
-      acost = P.act_cost_axis;
-    }
-  }
-  while (!c.o2.empty()) {
-    const int b = c.o2.begin();
-    const Node2 top = P.open2[b];
+  typedef typename std::conditional<G, GAS Node2*, Node2*>::type NP;
+  typedef typename std::conditional<G, GAS Closed2*, Closed2*>::type CP;
+  RBTree<Node2, NP> tr{G ? (NP)gp(P.open2) : (NP)L.open};
+  CP cl = G ? (CP)gp(P.closed2) : (CP)L.closed;
+  const int cap = G ? P.open2_cap : A_CAP;
+  while (!tr.empty()) {
+    if (!G && (c.ps2.next + 8 > A_CAP || c.n_closed2 + 1 > A_CCAP)) return false;
+    const int b = tr.begin();
+    const Node2 top = gload(&tr.t[b]);
     const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
-    const size_t tcell = (size_t)tx * P.N + ty;
-    int ci;
-    if (P.cgen2[tcell] == c.gen2) {
-      ci = P.cidx2[tcell];  // duplicate pop: the old closed element is expanded
-    } else {
-      if (c.n_closed2 >= P.closed2_cap) {
-        c.status = -75;
-        return FLT_MAX;
-      }
+    const uint32_t tcell = (uint32_t)tx * (uint32_t)P.N + (uint32_t)ty;
+    int ci = G ? ((gp(P.cgen2)[tcell] == c.gen2) ? gp(P.cidx2)[tcell] : NIL) : lds_closed_find(L, tcell);
+    if (ci == NIL) {  // new closed element (duplicates expand the old one, AStar.cpp:130)
+      if (c.n_closed2 >= (G ? P.closed2_cap : A_CCAP)) { c.status = -75; *result = FLT_MAX; return true; }
       ci = c.n_closed2++;
-      Closed2* r = &P.closed2[ci];
+      auto r = &cl[ci];
       r->key = top.key;
       r->g = top.g;
       r->f = top.f;
       r->prev = top.prev;
-      P.cgen2[tcell] = c.gen2;
-      P.cidx2[tcell] = ci;
+      if (G) {
+        gp(P.cgen2)[tcell] = c.gen2;
+        gp(P.cidx2)[tcell] = ci;
+      } else {
+        if (lane == 0) lds_closed_put(L, tcell, ci);
+        __syncthreads();
+      }
     }
-    c.o2.unlink(b);
-    pool_free(P.open2, c.ps2, b);
+    tr.unlink(b);
+    pool_free(tr.t, c.ps2, b);
     c.apops++;
-    const Closed2 cur = P.closed2[ci];
+    if (G) c.apops_g++;
+    const Closed2 cur = gload(&cl[ci]);
     const int cx = (int)(cur.key >> 16), cy = (int)(cur.key & 0xffffu);
     if (cx == P.goal_cx && cy == P.goal_cy) {
-      memoise(c, cur.f, ci);
-      return cur.f;
+      memoise<G>(c, cl, cur.f, ci);
+      *result = cur.f;
+      return true;
     }
     const float g0 = cur.g;
-    // neighbour probes in parallel: lane k evaluates action k (Grid2D::get_neighbors)
+    // neighbour probes, one lane per action (Grid2D::get_neighbors, Grid2D.cpp:72-96): bounds,
+    // occupancy, memo flag, node-map f and closed membership are loop-invariant here.
     const int ni = cx + adx, nj = cy + ady;
-    bool valid = false, vis = false;
+    bool valid = false, vis = false, closed = false;
     float nf = 0.0f;
     if (lane < nact && ni > -1 && ni < P.N && nj > -1 && nj < P.N) {
-      const size_t cell = (size_t)ni * P.N + nj;
-      if (P.occ[cell] < P.thr) {
-        valid = true;
-        vis = P.visited[cell] != 0;
-        nf = P.nm_f[cell];
-      }
+      // all probe loads in flight together (one HBM round trip)
+      const uint32_t cell = (uint32_t)ni * (uint32_t)P.N + (uint32_t)nj;
+      const float occv = gp(P.occ)[cell];
+      const uint8_t visv = gp(P.visited)[cell];
+      nf = gp(P.nm_f)[cell];
+      const bool clv = G ? (gp(P.cgen2)[cell] == c.gen2) : (lds_closed_find(L, cell) != NIL);
+      valid = occv < P.thr;
+      vis = valid && visv != 0;
+      closed = valid && clv;
     }
-    const uint64_t vmask = __ballot(valid);
+    const uint64_t vmask = __ballot(valid), vismask = __ballot(vis), cmask = __ballot(closed);
     for (int k = 0; k < nact; ++k) {
       if (!((vmask >> k) & 1ull)) continue;
-      const int ki = shfl_i(ni, k), kj = shfl_i(nj, k);
-      const bool kvis = shfl_i((int)vis, k) != 0;
       const float kcost = shfl_f(acost, k);
-      const size_t cell = (size_t)ki * P.N + kj;
-      if (kvis) {
+      if ((vismask >> k) & 1ull) {
         const float tot = shfl_f(nf, k) + g0 + kcost;
-        memoise(c, tot, ci);
-        return tot;
+        memoise<G>(c, cl, tot, ci);
+        *result = tot;
+        return true;
       }
-      if (P.cgen2[cell] == c.gen2) continue;        // in the closed set
+      if ((cmask >> k) & 1ull) continue;
+      const int ki = shfl_i(ni, k), kj = shfl_i(nj, k);
       const uint32_t key = ((uint32_t)ki << 16) | (uint32_t)kj;
-      const float fprobe = P.nm_f[cell];           // stale _node_map f, as the reference
-      const int hit = c.o2.find(key, fprobe);
+      const float fprobe = shfl_f(nf, k);  // stale _node_map f, as the reference reads it
+      const int hit = tr.find(key, fprobe);
       const float gn = g0 + kcost;
       if (hit == 0) {
         const float fn = gn + euclid_h(P, ki, kj);
-        P.nm_f[cell] = fn;                         // Node2D::set_accumulated_cost
-        if (!insert2(c, key, fn, gn, ci)) { c.status = -75; return FLT_MAX; }
-      } else if (gn < P.open2[hit].g) {
-        c.o2.unlink(hit);
-        pool_free(P.open2, c.ps2, hit);
+        gp(P.nm_f)[(size_t)ki * P.N + kj] = fn;  // Node2D::set_accumulated_cost
+        if (!insert2(c, tr, cap, key, fn, gn, ci)) { c.status = -75; *result = FLT_MAX; return true; }
+      } else if (gn < tr.t[hit].g) {
+        tr.unlink(hit);
+        pool_free(tr.t, c.ps2, hit);
         const float fn = gn + euclid_h(P, ki, kj);
-        P.nm_f[cell] = fn;
-        if (!insert2(c, key, fn, gn, ci)) { c.status = -75; return FLT_MAX; }
+        gp(P.nm_f)[(size_t)ki * P.N + kj] = fn;
+        if (!insert2(c, tr, cap, key, fn, gn, ci)) { c.status = -75; *result = FLT_MAX; return true; }
       }
     }
+    if (!G) __syncthreads();
   }
-  return FLT_MAX;
+  *result = FLT_MAX;
+  return true;
+}
+
+// AStar::find_path(int, int) (AStar.cpp:100-113)
+__device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, int sj) {
+  const PlannerDev& P = *c.P;
+  const int lane = c.lane;
+  const size_t s_cell = (size_t)si * P.N + sj;
+  if (gp(P.visited)[s_cell]) return gp(P.nm_f)[s_cell];
+  const float h0 = euclid_h(P, si, sj);
+  gp(P.nm_f)[s_cell] = h0;  // Grid2D::set_start_node_grid -> Node2D::soft_reset
+  c.asearch++;
+  c.gen2++;
+  c.n_closed2 = 0;
+  c.ps2.next = 1;
+  c.ps2.free = NIL;
+  for (int q = lane; q < A_HS; q += 64) L.hkey[q] = 0;
+  __syncthreads();
+  RBTree<Node2, Node2*> tr{L.open};
+  tr.clear();
+  insert2(c, tr, A_CAP, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL);
+  __syncthreads();
+  const int nact = P.diag ? 8 : 4;
+  // this lane's action (Grid2D.cpp:22-40): nibble-packed (dx + 1, dy + 1) tables
+  int adx = 0, ady = 0;
+  float acost = 0.0f;
+  if (lane < nact) {
+    const uint32_t px = P.diag ? 0x00012221u : 0x0121u, py = P.diag ? 0x01222100u : 0x1210u;
+    adx = (int)((px >> (4 * lane)) & 0xfu) - 1;
+    ady = (int)((py >> (4 * lane)) & 0xfu) - 1;
+    acost = (adx != 0 && ady != 0) ? P.act_cost_diag : P.act_cost_axis;
+  }
+  float result = FLT_MAX;
+  if (astar_loop<false>(c, L, adx, ady, acost, &result)) return result;
+  // migrate the LDS state to HBM (identical indices) and continue there
+  c.amigr++;
+  for (int i = lane; i < c.ps2.next; i += 64) gstore(&gp(P.open2)[i], L.open[i]);
+  for (int i = lane; i < c.n_closed2; i += 64) {
+    const Closed2 r = L.closed[i];
+    gstore(&gp(P.closed2)[i], r);
+    const size_t cell = (size_t)(r.key >> 16) * P.N + (r.key & 0xffffu);
+    gp(P.cgen2)[cell] = c.gen2;
+    gp(P.cidx2)[cell] = i;
+  }
+  __syncthreads();
+  STAMP_T tg = STAMP_NOW();
+  astar_loop<true>(c, L, adx, ady, acost, &result);
+  STAMP_ADD(7, tg);
+  return result;
 }
 
 __device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, int prev) {
@@ -234,9 +320,9 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, in
   const uint32_t key = key3(s.cx, s.cy, s.bin);
   const int pos = c.o3.insert_pos(key, f, &left);
   if (pos == -2) return true;
-  const int n = pool_alloc(c.P.open3, c.ps3, c.P.open3_cap);
+  const int n = pool_alloc(gp(c.P->open3), c.ps3, c.P->open3_cap);
   if (n == NIL) return false;
-  Node3* d = &c.P.open3[n];
+  auto d = &gp(c.P->open3)[n];
   d->key = key;
   d->f = f;
   d->g = s.g;
@@ -255,25 +341,28 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
                                                            int max_pops) {
   if ((int)blockIdx.x >= n_planners) return;
   __shared__ Succ sl[MAXS];
+  __shared__ AStarLds alds;
   SearchCtx c;
-  c.P = descs[blockIdx.x];
-  const PlannerDev& P = c.P;
+  c.P = descs + blockIdx.x;
+  const PlannerDev& P = *c.P;
+#ifdef HASTAR_STAMPS
+  for (int q = 0; q < 8; ++q) c.cyc[q] = 0;
+#endif
   const int lane = threadIdx.x;
   c.lane = lane;
-  c.o3.t = P.open3;
-  c.o2.t = P.open2;
-  c.gen3 = P.gens[0] + 1;
-  c.gen2 = P.gens[1];
+  c.o3.t = gp(P.open3);
+  c.gen3 = gp(P.gens)[0] + 1;
+  c.gen2 = gp(P.gens)[1];
   c.n_closed3 = 0;
   c.n_closed2 = 0;
-  c.pops = c.succ = c.apops = c.asearch = c.shots = 0;
+  c.pops = c.succ = c.apops = c.asearch = c.shots = c.amigr = c.apops_g = 0;
   c.status = 0;
   c.o3.clear();
   c.ps3.next = 1;
   c.ps3.free = NIL;
 
   // Grid3D::set_start_node soft-resets the start cell's node (Grid3D.cpp:145-148 / 153-154)
-  P.nm_f[(size_t)P.start_cx * P.N + P.start_cy] = euclid_h(P, P.start_cx, P.start_cy);
+  gp(P.nm_f)[(size_t)P.start_cx * P.N + P.start_cy] = euclid_h(P, P.start_cx, P.start_cy);
   {
     Succ s0;
     s0.x = P.start_x;
@@ -295,19 +384,22 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
   int ok = 0, via_shot = 0, terminal = NIL, dub_n = 0;
   float cost = FLT_MAX;
   const int span = 2 * P.na + 1;
+  STAMP_T tloop = STAMP_NOW();
 
   while (!c.o3.empty()) {
     if (c.pops >= max_pops) { c.status = -75; break; }
+    STAMP_T tp = STAMP_NOW();
     const int b = c.o3.begin();
-    const Node3 top = P.open3[b];
+    const Node3 top = gload(&gp(P.open3)[b]);
     const int ci = closed3_insert(c, top);
     if (ci == NIL) { c.status = -75; break; }
     c.o3.unlink(b);
-    pool_free(P.open3, c.ps3, b);
+    pool_free(gp(P.open3), c.ps3, b);
     c.pops++;
-    const Closed3 cur = P.closed3[ci];
+    const Closed3 cur = gload(&gp(P.closed3)[ci]);
     const int cx = key3_x(cur.key), cy = key3_y(cur.key), cbin = key3_bin(cur.key);
     dig = mix64(dig ^ digest_key(cur.key)) + (uint64_t)fbits(cur.g);
+    STAMP_ADD(0, tp);
     // goal test: Node3D::operator== compares the cell only (Node3D.h:42)
     if (cx == P.goal_cx && cy == P.goal_cy) {
       terminal = ci;
@@ -317,17 +409,18 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
     }
     if (shot_allowed) {
       if (++counter == interval) {
+        STAMP_T tsh = STAMP_NOW();
         c.shots++;
         int word = 0;
         float prm[4];
         // Dubins::get_shortest_path (Dubins.cpp:125-153)
         const float L = dubins_shortest(r, cur.x, cur.y, cur.h, P.goal_x, P.goal_y, P.goal_h, &word, prm);
         const Centres C = dubins_centres(r, cur.x, cur.y, cur.h, P.goal_x, P.goal_y, P.goal_h);
-        const int n = dubins_sample(P, C, word, prm, P.dub_xyh, P.dub_curv, P.dub_cap, lane);
+        const int n = dubins_sample(P, C, word, prm, gp(P.dub_xyh), gp(P.dub_curv), P.dub_cap, lane);
         if (n < 0) { c.status = -75; break; }
         __syncthreads();
         const bool first_arc_long = fabsf(prm[1]) > (float)M_PI_2;
-        if (!first_arc_long && path_is_free(P, P.dub_xyh, n, lane)) {
+        if (!first_arc_long && path_is_free(P, gp(P.dub_xyh), n, lane)) {
           terminal = cur.prev;
           cost = cur.g + L;
           ok = 1;
@@ -337,9 +430,11 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
         }
         counter = 0;
         interval = max(interval - P.shot_decay, 50);
+        STAMP_ADD(4, tsh);
       }
     }
     // ---- successors: VehicleModel::get_neighbors (VehicleModel.cpp:63-105) + Grid3D filter
+    STAMP_T tx = STAMP_NOW();
     shot_allowed = cur.vmin < 1.0f;
     int lo = cur.ci - P.na;
     lo = lo < 0 ? 0 : lo;
@@ -347,24 +442,24 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
     for (int i = lo; i < lo + span && i < P.nsteer; ++i) {
       float vm = 0.0f;
       if (!shot_allowed) {
-        const float lat = cur.vmin * P.curv_abs[i];
+        const float lat = cur.vmin * gp(P.curv_abs)[i];
         if (lat > P.a_lat) continue;
         const float al = (float)sqrt(1.0 - (double)((lat * lat) / P.a_lat2));
         vm = cur.vmin - 2.0f * al * P.ts;
       }
-      const float* o = &P.off[2 * ((size_t)i * (P.bins + 1) + cbin)];
+      const GAS float* o = &gp(P.off)[2 * ((size_t)i * (P.bins + 1) + cbin)];
       Succ s;
       s.x = cur.x + o[0];
       s.y = cur.y + o[1];
-      s.h = wrap_pi_f(cur.h + P.dth[i]);
-      s.g = cur.g + P.act_cost[i];
+      s.h = wrap_pi_f(cur.h + gp(P.dth)[i]);
+      s.g = cur.g + gp(P.act_cost)[i];
       s.vmin = vm;
       s.ci = i;
       s.bin = heading_bin(s.h, P.prec);
       s.cx = trunc_f(s.x / P.res);
       s.cy = trunc_f(s.y / P.res);
       if (!(s.cx > -1 && s.cx < P.N && s.cy > -1 && s.cy < P.N)) continue;
-      if (!(P.occ[(size_t)s.cx * P.N + s.cy] < P.thr)) continue;
+      if (!(gp(P.occ)[(size_t)s.cx * P.N + s.cy] < P.thr)) continue;
       s.dub = 0.0f;
       if (lane == 0) sl[ns] = s;
       ++ns;
@@ -397,7 +492,9 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
       }
     }
     __syncthreads();
+    STAMP_ADD(1, tx);
     // ---- HybridAStar.cpp:159-193
+    STAMP_T tb = STAMP_NOW();
     bool fail = false;
     for (int q = 0; q < ns; ++q) {
       const Succ s = sl[q];
@@ -405,31 +502,38 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
       if (closed3_contains(c, key)) continue;
       const int hit = c.o3.find(key, s.g);  // f == g before the heuristic is added
       if (hit == 0) {
-        const float h1 = holonomic(c, s.cx, s.cy);
+        STAMP_T ta = STAMP_NOW();
+        const float h1 = holonomic(c, alds, s.cx, s.cy);
+        STAMP_ADD(3, ta);
         const float f = s.g + stl_max(h1, s.dub);
         if (!insert3(c, s, f, ci)) { fail = true; break; }
-      } else if (s.g < P.open3[hit].g) {
+      } else if (s.g < gp(P.open3)[hit].g) {
         c.o3.unlink(hit);
-        pool_free(P.open3, c.ps3, hit);
-        const float h1 = holonomic(c, s.cx, s.cy);
+        pool_free(gp(P.open3), c.ps3, hit);
+        STAMP_T ta = STAMP_NOW();
+        const float h1 = holonomic(c, alds, s.cx, s.cy);
+        STAMP_ADD(3, ta);
         const float f = s.g + stl_max(h1, s.dub);
         if (!insert3(c, s, f, ci)) { fail = true; break; }
       }
       if (c.status != 0) break;
     }
     __syncthreads();
+    STAMP_ADD(2, tb);
     if (fail) c.status = -75;
     if (c.status != 0) break;
   }
+  STAMP_ADD(6, tloop);
   if (c.status != 0) ok = 0;
 
   // ---- reconstruct_path (HybridAStar.cpp:208-262) into out_xyh / out_curv
+  STAMP_T trc = STAMP_NOW();
   int path_len = 0;
   if (ok) {
     int L = 0;
-    for (int i = terminal; i != NIL; i = P.closed3[i].prev) {
+    for (int i = terminal; i != NIL; i = gp(P.closed3)[i].prev) {
       if (dub_n + L >= P.out_cap) { c.status = -28; break; }
-      if (lane == 0) P.out_chain[L] = i;
+      if (lane == 0) gp(P.out_chain)[L] = i;
       ++L;
     }
     __syncthreads();
@@ -441,17 +545,17 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
         bool has_curv = true;
         if (k < dub_n) {
           const int q = dub_n - 1 - k;
-          px = P.dub_xyh[3 * q];
-          py = P.dub_xyh[3 * q + 1];
-          ph = P.dub_xyh[3 * q + 2];
-          kc = P.dub_curv[q];
+          px = gp(P.dub_xyh)[3 * q];
+          py = gp(P.dub_xyh)[3 * q + 1];
+          ph = gp(P.dub_xyh)[3 * q + 2];
+          kc = gp(P.dub_curv)[q];
         } else {
           const int m = k - dub_n;
-          const Closed3 nd = P.closed3[P.out_chain[m]];
+          const Closed3 nd = gload(&gp(P.closed3)[gp(P.out_chain)[m]]);
           px = nd.x;
           py = nd.y;
           ph = nd.h;
-          kc = P.curv_abs[nd.ci];
+          kc = gp(P.curv_abs)[nd.ci];
           has_curv = (m < L - 1);
         }
         const float x0 = px - P.goal_x, y0 = py - P.goal_y;
@@ -460,12 +564,12 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
         const float hr = wrap_pi_f(ph - ang);
         xr += P.world_goal_x;
         yr += P.world_goal_y;
-        P.out_xyh[3 * k] = xr;
-        P.out_xyh[3 * k + 1] = yr;
-        P.out_xyh[3 * k + 2] = hr;
-        if (has_curv) P.out_curv[k + 1] = kc;
+        gp(P.out_xyh)[3 * k] = xr;
+        gp(P.out_xyh)[3 * k + 1] = yr;
+        gp(P.out_xyh)[3 * k + 2] = hr;
+        if (has_curv) gp(P.out_curv)[k + 1] = kc;
       }
-      if (lane == 0) P.out_curv[0] = 0.0f;
+      if (lane == 0) gp(P.out_curv)[0] = 0.0f;
     } else {
       ok = 0;
     }
@@ -473,11 +577,12 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
 
   // ---- statistics: closed-set digest (order independent) and counters
   uint64_t cd = 0;
-  for (int i = lane; i < c.n_closed3; i += 64) cd += mix64(digest_key(P.closed3[i].key));
+  for (int i = lane; i < c.n_closed3; i += 64) cd += mix64(digest_key(gp(P.closed3)[i].key));
   cd = wave_sum_u64(cd);
   __syncthreads();
+  STAMP_ADD(5, trc);
   if (lane == 0) {
-    SearchResult* R = P.result;
+    auto R = gp(P.result);
     R->pops = c.pops;
     R->successors = c.succ;
     R->astar_pops = c.apops;
@@ -493,8 +598,15 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
     R->cost = ok ? cost : FLT_MAX;
     R->terminal = terminal;
     R->dubins_len = dub_n;
-    P.gens[0] = c.gen3;
-    P.gens[1] = c.gen2;
+    R->astar_migrations = c.amigr;
+    R->astar_pops_hbm = c.apops_g;
+#ifdef HASTAR_STAMPS
+    for (int q = 0; q < 8; ++q) R->cycles[q] = c.cyc[q];
+#else
+    for (int q = 0; q < 8; ++q) R->cycles[q] = 0;
+#endif
+    gp(P.gens)[0] = c.gen3;
+    gp(P.gens)[1] = c.gen2;
   }
 }
 
@@ -504,7 +616,7 @@ __global__ void k_init_nodemap(PlannerDev P) {
   const size_t NN = (size_t)P.N * P.N;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x) {
     const int i = (int)(t / P.N), j = (int)(t % P.N);
-    P.nm_f[t] = euclid_h(P, i, j);
+    gp(P.nm_f)[t] = euclid_h(P, i, j);
   }
 }
 
@@ -675,7 +787,7 @@ __global__ __launch_bounds__(64) void k_test_dubins_path(PlannerDev P, float sx,
   float prm[4];
   const float len = dubins_shortest(P.r_min, sx, sy, sh, P.goal_x, P.goal_y, P.goal_h, &word, prm);
   const Centres C = dubins_centres(P.r_min, sx, sy, sh, P.goal_x, P.goal_y, P.goal_h);
-  const int n = dubins_sample(P, C, word, prm, xyh, curv, cap, threadIdx.x);
+  const int n = dubins_sample(P, C, word, prm, gp(xyh), gp(curv), cap, threadIdx.x);
   if (threadIdx.x == 0) {
     *n_out = n;
     *len_out = len;

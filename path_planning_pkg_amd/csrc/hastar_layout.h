@@ -18,15 +18,16 @@ constexpr int RB_BLACK = 1;
 // is the libstdc++ header: p = root, l = leftmost, r = rightmost, color = red.
 // key = cell x << 20 | cell y << 8 | angle bin  (Node3D::operator!=, Node3D.h:44-47).
 struct alignas(16) Node3 {
-  int l, r, p, color;     // tree links (pool indices, NIL = null)
   uint32_t key;           // (x, y, bin)
   float f;                // _cost_f: the comparator's order key
+  int l, r;               // tree links (pool indices, NIL = null): {key, f, l, r} = one 16-B load per walk step
+  int p, color;
   float g;                // _cost_g
   float vmin;             // _vmin_sqr
   float x, y, h;          // _pose2D (grid frame)
   int ci;                 // _curvature_index
   int prev;               // closed-record index of the predecessor (NIL for the start)
-  int pad0, pad1, pad2;
+  int pad0, pad1;
 };
 
 // Closed-set record (unordered_set<Node3D>, HybridAStar.h:73-74): a copy of the popped
@@ -44,9 +45,10 @@ struct alignas(16) Closed3 {
 // Holonomic A* open-set node (std::set<Node2D<float>>, AStar.h:70).
 // key = x << 16 | y (Node2D::operator!=, Node2D.h:35-38).
 struct alignas(16) Node2 {
-  int l, r, p, color;
   uint32_t key;
   float f;
+  int l, r;               // {key, f, l, r}: one 16-B load per walk step
+  int p, color;
   float g;
   int prev;               // index into the A* closed records of the current search
 };
@@ -68,13 +70,14 @@ struct Slot3 {
 
 // Per-search result block (written by the search kernel, read by the host).
 struct SearchResult {
-  long long pops, successors, astar_pops, astar_searches, shots, closed_size;
+  long long pops, successors, astar_pops, astar_searches, shots, closed_size, astar_pops_hbm;
   unsigned long long pop_digest, closed_digest;
   int ok, via_shot, status, path_len;
   float cost;
   int terminal;           // closed record index the path is rebuilt from
   int dubins_len;         // samples of the successful shot
-  int pad;
+  int astar_migrations;   // inner A* searches that outgrew LDS
+  unsigned long long cycles[8];  // diagnostic build (-DHASTAR_STAMPS): s_memtime per phase
 };
 
 // Descriptor of one planner: constants + device pointers.  Lives in HBM; the kernel

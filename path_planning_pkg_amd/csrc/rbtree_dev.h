@@ -14,6 +14,7 @@
 // l = leftmost, r = rightmost, color red), NIL (-1) is the null link.
 // Tested against std::set on random operation streams: tests/test_rbtree_host.py.
 #pragma once
+#include <type_traits>
 #include "hastar_layout.h"
 
 #if defined(__HIPCC__)
@@ -27,9 +28,36 @@ namespace hastar {
 // comparator of the reference: (ka != kb) && (fa < fb)
 RB_HD bool rb_less(uint32_t ka, float fa, uint32_t kb, float fb) { return (ka != kb) && (fa < fb); }
 
-template <class NodeT>
+// {key, f, l, r} of one node in one 16-byte load (the first 16 bytes of every node type)
+struct Quad {
+  uint32_t key;
+  float f;
+  int l, r;
+};
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef int rb_v4i __attribute__((ext_vector_type(4)));
+template <class PtrT>
+__device__ __forceinline__ Quad rb_quad(PtrT t, int x) {
+  typedef typename std::remove_reference<decltype(t[0].key)>::type K;  // keeps the address space
+  (void)sizeof(K);
+  const rb_v4i v = *reinterpret_cast<decltype(&reinterpret_cast<const rb_v4i&>(t[x]))>(&t[x]);
+  Quad q;
+  q.key = (uint32_t)v.x;
+  q.f = __int_as_float(v.y);
+  q.l = v.z;
+  q.r = v.w;
+  return q;
+}
+#else
+template <class PtrT>
+inline Quad rb_quad(PtrT t, int x) {
+  return Quad{t[x].key, t[x].f, t[x].l, t[x].r};
+}
+#endif
+
+template <class NodeT, class PtrT = NodeT*>
 struct RBTree {
-  NodeT* t;
+  PtrT t;
 
   RB_HD int root() const { return t[0].p; }
   RB_HD int begin() const { return t[0].l; }          // == 0 (header) when empty
@@ -85,15 +113,20 @@ struct RBTree {
   // when not "found".
   RB_HD int find(uint32_t k, float f) const {
     int y = 0, x = t[0].p;
+    uint32_t yk = 0;
+    float yf = 0.0f;
     while (x != NIL) {
-      if (!rb_less(t[x].key, t[x].f, k, f)) {
+      const Quad q = rb_quad(t, x);
+      if (!rb_less(q.key, q.f, k, f)) {
         y = x;
-        x = t[x].l;
+        yk = q.key;
+        yf = q.f;
+        x = q.l;
       } else {
-        x = t[x].r;
+        x = q.r;
       }
     }
-    if (y == 0 || rb_less(k, f, t[y].key, t[y].f)) return 0;
+    if (y == 0 || rb_less(k, f, yk, yf)) return 0;
     return y;
   }
 
@@ -103,9 +136,10 @@ struct RBTree {
     int x = t[0].p, y = 0;
     bool comp = true;
     while (x != NIL) {
+      const Quad q = rb_quad(t, x);
       y = x;
-      comp = rb_less(k, f, t[x].key, t[x].f);
-      x = comp ? t[x].l : t[x].r;
+      comp = rb_less(k, f, q.key, q.f);
+      x = comp ? q.l : q.r;
     }
     int j = y;
     if (comp) {
@@ -295,8 +329,8 @@ struct PoolState {
   int free;   // head of the free list (NIL if empty)
 };
 
-template <class NodeT>
-RB_HD int pool_alloc(NodeT* t, PoolState& ps, int cap) {
+template <class PtrT>
+RB_HD int pool_alloc(PtrT t, PoolState& ps, int cap) {
   if (ps.free != NIL) {
     const int i = ps.free;
     ps.free = t[i].l;
@@ -306,8 +340,8 @@ RB_HD int pool_alloc(NodeT* t, PoolState& ps, int cap) {
   return ps.next++;
 }
 
-template <class NodeT>
-RB_HD void pool_free(NodeT* t, PoolState& ps, int i) {
+template <class PtrT>
+RB_HD void pool_free(PtrT t, PoolState& ps, int i) {
   t[i].l = ps.free;
   ps.free = i;
 }

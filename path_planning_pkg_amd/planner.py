@@ -15,7 +15,9 @@ import numpy as np
 
 from .capi import HastarStats, PlannerConfig, fptr, iptr
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libhastar_amd.so"
+import os
+
+LIB_PATH = Path(os.environ.get("HASTAR_LIB", Path(__file__).resolve().parent / "lib" / "libhastar_amd.so"))
 _lib = None
 
 HASTAR_ENOSPC = -28
@@ -60,6 +62,8 @@ def load_library():
     L.hastar_debug_apf.argtypes = [vp, fp, C.c_int]
     L.hastar_debug_motion.argtypes = [vp, fp, fp, fp, fp, fp, fp]
     L.hastar_debug_closed_keys.argtypes = [vp, ip, C.c_int]
+    L.hastar_debug_cycles.argtypes = [vp, C.POINTER(C.c_ulonglong)]
+    L.hastar_debug_astar_modes.argtypes = [vp, C.POINTER(C.c_longlong)]
     _lib = L
     return L
 
@@ -178,6 +182,16 @@ class HybridAStar:
         n = _check(load_library().hastar_debug_closed_keys(self.h, iptr(out), cap))
         return out[:min(n, cap)].copy()
 
+    def cycles(self):
+        out = (C.c_ulonglong * 8)()
+        _check(load_library().hastar_debug_cycles(self.h, out))
+        return list(out)
+
+    def astar_modes(self):
+        out = (C.c_longlong * 2)()
+        _check(load_library().hastar_debug_astar_modes(self.h, out))
+        return {"migrations": out[0], "astar_pops_hbm": out[1]}
+
     def field(self, poses):
         p = _f32(poses, (-1, 3))
         out = np.empty(len(p), np.float32)
@@ -210,7 +224,8 @@ def find_path_batch(planners, vels, starts, cap=4096):
     stats = (HastarStats * n)()
     rc = L.hastar_find_path_batch(hs, n, fptr(v), fptr(s), fptr(xyh), fptr(curv), cap, iptr(ln), fptr(cost),
                                   iptr(ok), stats)
-    _check(rc)
+    if rc != HASTAR_EOVERFLOW:  # per-planner arena overflows are reported in stats[i]["status"]
+        _check(rc)
     out = []
     for i in range(n):
         k = int(ln[i])

@@ -1,0 +1,47 @@
+"""Throughput vs batch size of the search kernel (cfg3 planners, one wavefront each).
+
+  python tools/batch_scaling.py --batches 64 256 1024 2048
+Builds max(batches) planners once (seeds 1..B), then for each B runs one batched search
+(after reset) and prints kernel ms, pops, A* pops, overflow count and pops/s.
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from path_planning_pkg_amd import planner as gpu  # noqa: E402
+from tests.scenarios import drive, synthetic  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batches", type=int, nargs="+", default=[64, 256, 1024])
+ap.add_argument("--grid", type=int, default=1024)
+ap.add_argument("--obstacles", type=int, default=200)
+ap.add_argument("--max-pops", type=int, default=65536)
+ap.add_argument("--max-astar-nodes", type=int, default=262144)
+args = ap.parse_args()
+Bmax = max(args.batches)
+t = time.time()
+ps, cf = [], []
+for q in range(Bmax):
+    cfg, proto = synthetic(args.grid, 72, args.obstacles, q + 1)
+    cfg.values["max_pops"] = args.max_pops
+    cfg.values["max_astar_nodes"] = args.max_astar_nodes
+    p = gpu.HybridAStar(cfg)
+    drive(p, proto)
+    ps.append(p)
+    cf.append(proto)
+print(json.dumps({"setup_s": time.time() - t, "planners": Bmax}), flush=True)
+for B in args.batches:
+    for p in ps[:B]:
+        p.reset()
+    t0 = time.time()
+    res, kms = gpu.find_path_batch(ps[:B], [c["vel"] for c in cf[:B]], [c["start"] for c in cf[:B]], cap=8192)
+    wall = time.time() - t0
+    pops = sum(r["stats"]["pops"] for r in res)
+    apops = sum(r["stats"]["astar_pops"] for r in res)
+    bad = [i + 1 for i, r in enumerate(res) if r["stats"]["status"] != 0]
+    print(json.dumps({"batch": B, "kernel_ms": kms, "wall_ms": wall * 1e3, "pops": pops, "astar_pops": apops,
+                      "pops_per_s": pops / (kms * 1e-3), "overflow_seeds": bad[:20], "n_overflow": len(bad)}),
+          flush=True)

@@ -1,0 +1,41 @@
+"""Single-query phase breakdown of the search kernel (diagnostic build with -DHASTAR_STAMPS).
+
+  HASTAR_LIB=path_planning_pkg_amd/lib_stamps/libhastar_amd.so python tools/profile_search.py --grid 1024 --seeds 1 3
+Prints pops, A* pops, kernel ms, and the share of s_memtime cycles per phase
+(0 pop+closed insert, 1 successors+APF+Dubins, 2 open/closed bookkeeping excl. A*,
+3 holonomic A*, 4 Dubins shot, 5 reconstruct+stats, 6 whole loop).
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from path_planning_pkg_amd import planner as gpu  # noqa: E402
+from tests.scenarios import drive, synthetic  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--grid", type=int, default=1024)
+ap.add_argument("--bins", type=int, default=72)
+ap.add_argument("--obstacles", type=int, default=200)
+ap.add_argument("--seeds", type=int, nargs="+", default=[1])
+args = ap.parse_args()
+names = ["pop", "expand", "open_bookkeeping", "astar", "shot", "reconstruct", "loop", "astar_hbm_mode"]
+for s in args.seeds:
+    cfg, proto = synthetic(args.grid, args.bins, args.obstacles, s)
+    p = gpu.HybridAStar(cfg)
+    drive(p, proto)
+    res, ms = gpu.find_path_batch([p], [proto["vel"]], [proto["start"]])
+    cyc = p.cycles()
+    st = res[0]["stats"]
+    loop = max(cyc[6], 1)
+    share = {names[i]: round(cyc[i] / loop, 4) for i in range(6)}
+    share["open_bookkeeping"] = round((cyc[2] - cyc[3]) / loop, 4)
+    share["astar_hbm_mode"] = round(cyc[7] / loop, 4)
+    modes = p.astar_modes()
+    print(json.dumps(dict(seed=s, kernel_ms=ms, pops=st["pops"], astar_pops=st["astar_pops"],
+                          astar_searches=st["astar_searches"], successors=st["successors"],
+                          loop_cycles=cyc[6], cycles_per_pop=cyc[6] / max(st["pops"], 1), share=share, **modes,
+                          cyc_per_apop_lds=(cyc[3] - cyc[7]) / max(st["astar_pops"] - modes["astar_pops_hbm"], 1),
+                          cyc_per_apop_hbm=cyc[7] / max(modes["astar_pops_hbm"], 1))))
