@@ -53,8 +53,8 @@ def main():
     ap.add_argument("--grid", type=int, default=1024)
     ap.add_argument("--bins", type=int, default=72)
     ap.add_argument("--obstacles", type=int, default=200)
-    ap.add_argument("--max-pops", type=int, default=65536)
-    ap.add_argument("--max-astar-nodes", type=int, default=262144)
+    ap.add_argument("--max-pops", type=int, default=131072)
+    ap.add_argument("--max-astar-nodes", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-queries", type=int, default=3)

@@ -1,20 +1,30 @@
 // hastar_capi.cpp — host runtime behind include/hastar.h (the drop-in C ABI).
 //
-// Each hastar_handle owns one planner's device state (maps, memo, search arenas) and a
-// HIP stream.  Per-call scalar preparation (rotations of the call's inputs into the
-// goal-centred grid frame, per-box/per-line raster parameters, the start node) is done
-// here with the same float arithmetic as the reference and the bit-faithful libm ports;
-// every per-cell and per-expansion operation runs in the HIP kernels.  There is no CPU
-// fallback: without a usable gfx950 device every call returns HASTAR_EDEVICE.
+// Ownership model (HBM layout):
+//   * a planner (hastar_handle) owns its persistent state: log-odds map, node-map f
+//     (A* memo + stale values), memo flags, APF list, motion tables, output buffers;
+//   * the transient search state (open/closed sets of both searches, Dubins scratch)
+//     lives in per-slot arenas owned by the device context: one arena per resident
+//     wavefront of the persistent search kernel, reused across planners and calls;
+//   * all work of a device goes to one HIP stream, so map updates are asynchronous and
+//     stream-ordered (the reference API is synchronous only where it returns data:
+//     find_path, get_obstacles).
+// Per-call scalar preparation (rotations of the call's inputs into the goal-centred grid
+// frame, per-box/per-line raster parameters, the start node) is done here with the
+// reference's float arithmetic and the bit-faithful libm ports; every per-cell and
+// per-expansion operation runs in the HIP kernels.  There is no CPU fallback: without a
+// usable gfx950 device every call returns HASTAR_EDEVICE.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
-#include <string>
 #include <mutex>
+#include <numeric>
+#include <string>
 #include <vector>
 
 #include "../../include/hastar.h"
@@ -62,42 +72,167 @@ V2 rot2(float x, float y, float ang) {
   const float c = g_cosf(ang), s = g_sinf(ang);
   return {x * c + y * s, -x * s + y * c};
 }
-float stl_max(float a, float b) { return (a < b) ? b : a; }
 
 template <class T>
 hipError_t dalloc(T** p, size_t n) {
   return hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(n, 1) * sizeof(T));
 }
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// Map-update scratch shared by every planner of a device (relocation target + claim
-// table, raster hit counters): N*N floats/ints each, grown to the largest grid seen.
-// Map updates of different handles on one device are serialised by its mutex.
-struct DeviceScratch {
-  std::mutex mu;
-  size_t cap = 0;
-  float* tmp = nullptr;
-  int* winner = nullptr;  // kept at -1 between uses
-  int* cnt = nullptr;     // kept at 0 between uses
-};
-DeviceScratch g_scratch[64];
-
-int scratch_acquire(int dev, size_t NN, hipStream_t st, DeviceScratch** out) {
-  DeviceScratch& S = g_scratch[dev & 63];
-  if (S.cap < NN) {
-    if (S.tmp) hipFree(S.tmp);
-    if (S.winner) hipFree(S.winner);
-    if (S.cnt) hipFree(S.cnt);
-    S.tmp = nullptr;
-    S.winner = S.cnt = nullptr;
-    S.cap = 0;
-    if (dalloc(&S.tmp, NN) != hipSuccess || dalloc(&S.winner, NN) != hipSuccess || dalloc(&S.cnt, NN) != hipSuccess)
-      return fail(HASTAR_ENOMEM, "map scratch allocation failed");
-    if (hipMemsetAsync(S.winner, 0xff, NN * sizeof(int), st) != hipSuccess ||
-        hipMemsetAsync(S.cnt, 0, NN * sizeof(int), st) != hipSuccess)
-      return fail(HASTAR_EDEVICE, "map scratch init failed");
-    S.cap = NN;
+// Arena requirements of one planner (the pool is sized for the maximum over a batch).
+struct ArenaReq {
+  int open3 = 0, closed3 = 0, open2 = 0, closed2 = 0, dub = 0, chain = 0;
+  uint32_t slots = 1;
+  size_t cells = 0;
+  bool covers(const ArenaReq& o) const {
+    return open3 >= o.open3 && closed3 >= o.closed3 && open2 >= o.open2 && closed2 >= o.closed2 && dub >= o.dub &&
+           chain >= o.chain && slots >= o.slots && cells >= o.cells;
   }
-  *out = &S;
+  void merge(const ArenaReq& o) {
+    open3 = std::max(open3, o.open3);
+    closed3 = std::max(closed3, o.closed3);
+    open2 = std::max(open2, o.open2);
+    closed2 = std::max(closed2, o.closed2);
+    dub = std::max(dub, o.dub);
+    chain = std::max(chain, o.chain);
+    slots = std::max(slots, o.slots);
+    cells = std::max(cells, o.cells);
+  }
+};
+
+// Everything a device shares among its planners.
+struct DeviceCtx {
+  std::mutex mu;
+  bool init = false;
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int resident_slots = 0;       // W: resident wavefronts of the search kernel
+  // map-update scratch (relocation target + claim table, raster hit counters)
+  size_t scratch_cap = 0;
+  float* tmp = nullptr;
+  int* winner = nullptr;        // kept at -1 between uses
+  int* cnt = nullptr;           // kept at 0 between uses
+  // slot arenas (one HBM slab)
+  ArenaReq areq;
+  int n_arenas = 0;
+  int fit_arenas = 1 << 30;     // pool size the memory budget allowed at the last build
+  void* slab = nullptr;
+  SlotArena* d_arenas = nullptr;
+  // batch buffers
+  PlannerDev* d_descs = nullptr;
+  int* d_order = nullptr;
+  int* d_next = nullptr;
+  int batch_cap = 0;
+};
+DeviceCtx g_dev[64];
+
+int device_ctx(int dev, DeviceCtx** out) {
+  DeviceCtx& D = g_dev[dev & 63];
+  if (!D.init) {
+    D.device = dev;
+    HIPCHK(hipSetDevice(dev));
+    HIPCHK(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&D.ev0));
+    HIPCHK(hipEventCreate(&D.ev1));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, dev));
+    D.resident_slots = search_slots_per_cu() * prop.multiProcessorCount;
+    HIPCHK(dalloc(&D.d_next, 1));
+    D.init = true;
+  }
+  *out = &D;
+  return 0;
+}
+
+int scratch_acquire(DeviceCtx& D, size_t NN) {
+  if (D.scratch_cap >= NN) return 0;
+  if (D.tmp) hipFree(D.tmp);
+  if (D.winner) hipFree(D.winner);
+  if (D.cnt) hipFree(D.cnt);
+  D.tmp = nullptr;
+  D.winner = D.cnt = nullptr;
+  D.scratch_cap = 0;
+  HIPCHK(dalloc(&D.tmp, NN));
+  HIPCHK(dalloc(&D.winner, NN));
+  HIPCHK(dalloc(&D.cnt, NN));
+  HIPCHK(hipMemsetAsync(D.winner, 0xff, NN * sizeof(int), D.stream));
+  HIPCHK(hipMemsetAsync(D.cnt, 0, NN * sizeof(int), D.stream));
+  D.scratch_cap = NN;
+  return 0;
+}
+
+// (Re)build the arena pool so that n arenas each cover `need`.
+// The pool may come out smaller than n when n arenas do not fit the memory budget.
+int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
+  if (D.n_arenas >= n && D.areq.covers(need)) return 0;
+  if (D.n_arenas > 0 && D.areq.covers(need) && D.n_arenas >= D.fit_arenas) return 0;
+  ArenaReq r = D.areq;
+  r.merge(need);
+  n = std::max(n, D.n_arenas);
+  HIPCHK(hipStreamSynchronize(D.stream));
+  if (D.slab) hipFree(D.slab);
+  if (D.d_arenas) hipFree(D.d_arenas);
+  D.slab = nullptr;
+  D.d_arenas = nullptr;
+  D.n_arenas = 0;
+  const size_t b_open3 = align256((size_t)r.open3 * sizeof(Node3)), b_closed3 = align256((size_t)r.closed3 * sizeof(Closed3));
+  const size_t b_slots = align256((size_t)r.slots * sizeof(Slot3)), b_open2 = align256((size_t)r.open2 * sizeof(Node2));
+  const size_t b_closed2 = align256((size_t)r.closed2 * sizeof(Closed2)), b_cgen = align256(r.cells * sizeof(uint32_t));
+  const size_t b_cidx = align256(r.cells * sizeof(int)), b_gens = 256, b_dub = align256((size_t)r.dub * 3 * sizeof(float));
+  const size_t b_dubc = align256((size_t)r.dub * sizeof(float)), b_chain = align256((size_t)r.chain * sizeof(int));
+  const size_t per = b_open3 + b_closed3 + b_slots + b_open2 + b_closed2 + b_cgen + b_cidx + b_gens + b_dub + b_dubc + b_chain;
+  // memory budget of the pool: HASTAR_ARENA_MB, else 80% of the free HBM
+  size_t budget = 0;
+  if (const char* e = std::getenv("HASTAR_ARENA_MB")) budget = (size_t)std::strtoull(e, nullptr, 10) << 20;
+  if (budget == 0) {
+    size_t fr = 0, tot = 0;
+    HIPCHK(hipMemGetInfo(&fr, &tot));
+    budget = fr / 10 * 8;
+  }
+  const int n_want = n;
+  n = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, budget / per));
+  hipError_t e = hipMalloc(&D.slab, per * (size_t)n);
+  if (e != hipSuccess) {
+    D.slab = nullptr;
+    return fail(HASTAR_ENOMEM, "search arenas: hipMalloc of " + std::to_string(per * (size_t)n >> 20) + " MiB failed");
+  }
+  std::vector<SlotArena> host(n);
+  char* base = static_cast<char*>(D.slab);
+  for (int i = 0; i < n; ++i) {
+    char* q = base + per * (size_t)i;
+    SlotArena& A = host[i];
+    std::memset(&A, 0, sizeof(A));
+    A.open3 = reinterpret_cast<Node3*>(q); q += b_open3;
+    A.closed3 = reinterpret_cast<Closed3*>(q); q += b_closed3;
+    A.slots3 = reinterpret_cast<Slot3*>(q); q += b_slots;
+    A.open2 = reinterpret_cast<Node2*>(q); q += b_open2;
+    A.closed2 = reinterpret_cast<Closed2*>(q); q += b_closed2;
+    A.cgen2 = reinterpret_cast<uint32_t*>(q); q += b_cgen;
+    A.cidx2 = reinterpret_cast<int*>(q); q += b_cidx;
+    A.gens = reinterpret_cast<uint32_t*>(q); q += b_gens;
+    A.dub_xyh = reinterpret_cast<float*>(q); q += b_dub;
+    A.dub_curv = reinterpret_cast<float*>(q); q += b_dubc;
+    A.out_chain = reinterpret_cast<int*>(q); q += b_chain;
+    A.open3_cap = r.open3;
+    A.closed3_cap = r.closed3;
+    A.slots3_mask = r.slots - 1;
+    A.open2_cap = r.open2;
+    A.closed2_cap = r.closed2;
+    A.cells = r.cells;
+    A.dub_cap = r.dub;
+    A.chain_cap = r.chain;
+    // generation-stamped tables start at generation 0 (all stale)
+    HIPCHK(hipMemsetAsync(A.slots3, 0, b_slots, D.stream));
+    HIPCHK(hipMemsetAsync(A.cgen2, 0, b_cgen, D.stream));
+    HIPCHK(hipMemsetAsync(A.gens, 0, b_gens, D.stream));
+  }
+  HIPCHK(dalloc(&D.d_arenas, (size_t)n));
+  HIPCHK(hipMemcpyAsync(D.d_arenas, host.data(), (size_t)n * sizeof(SlotArena), hipMemcpyHostToDevice, D.stream));
+  HIPCHK(hipStreamSynchronize(D.stream));
+  D.areq = r;
+  D.n_arenas = n;
+  D.fit_arenas = n < n_want ? n : (1 << 30);
   return 0;
 }
 
@@ -105,17 +240,16 @@ int scratch_acquire(int dev, size_t NN, hipStream_t st, DeviceScratch** out) {
 
 struct hastar_handle_s {
   int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  PlannerDev desc{};            // host copy of the descriptor
-  PlannerDev* d_desc = nullptr; // device copy
+  DeviceCtx* dc = nullptr;
+  PlannerDev desc{};            // host copy of the descriptor (device copies are batch-local)
   float lp_min = 0, lp_max = 0, lp_free = 0;
   int max_pops = 0;
+  ArenaReq areq;
   std::vector<float> curv_abs;
   // grid-frame state (Grid2D::_grid_heading/_goal_location, Grid3D::_goal_location3D)
   float grid_heading = 0, goal2x = 0, goal2y = 0, goal3x = 0, goal3y = 0, goal3h = 0;
   bool goal_set = false;
-  // device buffers not referenced by the descriptor
+  // per-call upload buffers
   int apf_cap = 0;
   int* d_rp = nullptr;
   float* d_dl = nullptr;
@@ -123,39 +257,25 @@ struct hastar_handle_s {
   float* d_lp = nullptr;
   float* d_seq = nullptr;
   float* d_wid = nullptr;
-  int lp_cap = 0, seq_cap = 0, wid_cap = 0;
+  int lp_cap = 0, wid_cap = 0;
+  void* slab = nullptr;         // the planner's persistent state, one allocation
   SearchResult last{};
   bool have_last = false;
-  std::vector<void*> owned;
+  long long last_pops = 0;      // work estimate for longest-first scheduling
 };
 
 static void free_handle(hastar_handle h) {
   if (!h) return;
-  if (h->device >= 0) hipSetDevice(h->device);
-  for (void* p : h->owned) hipFree(p);
+  hipSetDevice(h->device);
+  if (h->dc) hipStreamSynchronize(h->dc->stream);
+  if (h->slab) hipFree(h->slab);
   if (h->d_rp) hipFree(h->d_rp);
   if (h->d_dl) hipFree(h->d_dl);
   if (h->d_lp) hipFree(h->d_lp);
   if (h->d_seq) hipFree(h->d_seq);
   if (h->d_wid) hipFree(h->d_wid);
   if (h->desc.apf) hipFree(h->desc.apf);
-  if (h->ev0) hipEventDestroy(h->ev0);
-  if (h->ev1) hipEventDestroy(h->ev1);
-  if (h->stream) hipStreamDestroy(h->stream);
   delete h;
-}
-
-template <class T>
-static int own_alloc(hastar_handle h, T** p, size_t n) {
-  hipError_t e = dalloc(p, n);
-  if (e != hipSuccess) return fail(HASTAR_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
-  h->owned.push_back(*p);
-  return 0;
-}
-
-static int push_desc(hastar_handle h) {
-  HIPCHK(hipMemcpyAsync(h->d_desc, &h->desc, sizeof(PlannerDev), hipMemcpyHostToDevice, h->stream));
-  return 0;
 }
 
 extern "C" {
@@ -178,11 +298,17 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(HASTAR_EDEVICE, "no HIP device available (this library has no CPU path)");
-  if (device < 0 || device >= ndev) return fail(HASTAR_EINVAL, "device ordinal out of range");
-  if (hipSetDevice(device) != hipSuccess) return fail(HASTAR_EDEVICE, "hipSetDevice failed");
+  if (device < 0 || device >= ndev || device >= 64) return fail(HASTAR_EINVAL, "device ordinal out of range");
+  DeviceCtx* dc = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_dev[device].mu);
+    if (int rc = device_ctx(device, &dc)) return rc;
+  }
+  HIPCHK(hipSetDevice(device));
 
   hastar_handle h = new hastar_handle_s();
   h->device = device;
+  h->dc = dc;
   PlannerDev& D = h->desc;
   const int N = p->grid_size;
   D.N = N;
@@ -242,73 +368,61 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   D.step = p->step_size;
   D.ang_step = p->step_size / D.r_min;
 
-  // arena sizes
-  h->max_pops = p->max_pops > 0 ? p->max_pops : 262144;
+  // arena requirements of this planner
   const size_t NN = (size_t)N * N;
-  const int open3_cap = 3 * h->max_pops + 64;
-  uint32_t slots = 1;
-  while (slots < 2u * (uint32_t)h->max_pops + 64) slots <<= 1;
+  h->max_pops = p->max_pops > 0 ? p->max_pops : 262144;
+  ArenaReq& R = h->areq;
+  R.open3 = 3 * h->max_pops + 64;
+  R.closed3 = h->max_pops + 1;
+  R.slots = 1;
+  while (R.slots < 2u * (uint32_t)h->max_pops + 64) R.slots <<= 1;
   const int astar_cap = p->max_astar_nodes > 0 ? p->max_astar_nodes : (int)std::min<size_t>(NN + 16, 1u << 30);
+  R.open2 = astar_cap + 1;
+  R.closed2 = (int)std::min<size_t>(NN, (size_t)astar_cap);
+  R.cells = NN;
   int dub_cap = p->max_dubins_samples;
   if (dub_cap <= 0) {
     const double span = 2.0 * N * D.res;
     dub_cap = (int)(span / D.step) + 2 * (int)(2 * M_PI / D.ang_step + 2) + 64;
   }
-  D.open3_cap = open3_cap;
-  D.closed3_cap = h->max_pops + 1;
-  D.slots3_mask = slots - 1;
-  D.open2_cap = astar_cap + 1;
-  D.closed2_cap = (int)std::min<size_t>(NN, (size_t)astar_cap);
-  D.dub_cap = dub_cap;
+  R.dub = dub_cap;
+  R.chain = h->max_pops + 2;
   D.out_cap = dub_cap + h->max_pops + 2;
 
-  int rc = 0;
-  hipError_t he = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-  if (he == hipSuccess) he = hipEventCreate(&h->ev0);
-  if (he == hipSuccess) he = hipEventCreate(&h->ev1);
-  if (he != hipSuccess) {
+  // the planner's persistent state: one allocation
+  const size_t b_occ = align256(NN * sizeof(float)), b_nm = align256(NN * sizeof(float)), b_vis = align256(NN);
+  const size_t b_off = align256(off.size() * sizeof(float)), b_s = align256((size_t)ns * sizeof(float));
+  const size_t b_ox = align256((size_t)D.out_cap * 3 * sizeof(float)), b_oc = align256((size_t)D.out_cap * sizeof(float));
+  const size_t b_res = align256(sizeof(SearchResult));
+  const size_t total = b_occ + b_nm + b_vis + b_off + 3 * b_s + b_ox + b_oc + b_res;
+  if (hipMalloc(&h->slab, total) != hipSuccess) {
+    h->slab = nullptr;
     free_handle(h);
-    return fail(HASTAR_EDEVICE, std::string("stream/event: ") + hipGetErrorString(he));
+    return fail(HASTAR_ENOMEM, "planner state allocation failed");
   }
-#define OWN(ptr, n) do { if ((rc = own_alloc(h, &(ptr), (n))) != 0) { free_handle(h); return rc; } } while (0)
-  OWN(D.occ, NN);
-  OWN(D.nm_f, NN);
-  OWN(D.visited, NN);
-  OWN(D.off, off.size());
-  OWN(D.dth, (size_t)ns);
-  OWN(D.act_cost, (size_t)ns);
-  OWN(D.curv_abs, (size_t)ns);
-  OWN(D.open3, (size_t)open3_cap);
-  OWN(D.closed3, (size_t)D.closed3_cap);
-  OWN(D.slots3, (size_t)slots);
-  OWN(D.open2, (size_t)D.open2_cap);
-  OWN(D.closed2, (size_t)D.closed2_cap);
-  OWN(D.cgen2, NN);
-  OWN(D.cidx2, NN);
-  OWN(D.gens, (size_t)4);
-  OWN(D.dub_xyh, (size_t)dub_cap * 3);
-  OWN(D.dub_curv, (size_t)dub_cap);
-  OWN(D.out_xyh, (size_t)D.out_cap * 3);
-  OWN(D.out_curv, (size_t)D.out_cap);
-  OWN(D.out_chain, (size_t)D.out_cap);
-  OWN(D.result, (size_t)1);
-  OWN(h->d_desc, (size_t)1);
-#undef OWN
+  char* q = static_cast<char*>(h->slab);
+  D.occ = reinterpret_cast<float*>(q); q += b_occ;
+  D.nm_f = reinterpret_cast<float*>(q); q += b_nm;
+  D.visited = reinterpret_cast<uint8_t*>(q); q += b_vis;
+  D.off = reinterpret_cast<float*>(q); q += b_off;
+  D.dth = reinterpret_cast<float*>(q); q += b_s;
+  D.act_cost = reinterpret_cast<float*>(q); q += b_s;
+  D.curv_abs = reinterpret_cast<float*>(q); q += b_s;
+  D.out_xyh = reinterpret_cast<float*>(q); q += b_ox;
+  D.out_curv = reinterpret_cast<float*>(q); q += b_oc;
+  D.result = reinterpret_cast<SearchResult*>(q); q += b_res;
   D.apf = nullptr;
   D.n_apf = 0;
-  hipStream_t st = h->stream;
-  he = hipMemsetAsync(D.occ, 0, NN * sizeof(float), st);
+  hipStream_t st = dc->stream;
+  hipError_t he = hipMemsetAsync(D.occ, 0, NN * sizeof(float), st);
   if (he == hipSuccess) he = hipMemsetAsync(D.visited, 0, NN, st);
-  if (he == hipSuccess) he = hipMemsetAsync(D.slots3, 0, (size_t)slots * sizeof(Slot3), st);
-  if (he == hipSuccess) he = hipMemsetAsync(D.cgen2, 0, NN * sizeof(uint32_t), st);
-  if (he == hipSuccess) he = hipMemsetAsync(D.gens, 0, 4 * sizeof(uint32_t), st);
   if (he == hipSuccess) he = hipMemcpyAsync(D.off, off.data(), off.size() * sizeof(float), hipMemcpyHostToDevice, st);
   if (he == hipSuccess) he = hipMemcpyAsync(D.dth, dth.data(), ns * sizeof(float), hipMemcpyHostToDevice, st);
   if (he == hipSuccess) he = hipMemcpyAsync(D.act_cost, cost.data(), ns * sizeof(float), hipMemcpyHostToDevice, st);
   if (he == hipSuccess)
     he = hipMemcpyAsync(D.curv_abs, h->curv_abs.data(), ns * sizeof(float), hipMemcpyHostToDevice, st);
   if (he == hipSuccess) he = launch_init_nodemap(D, st);
-  if (he == hipSuccess) he = hipStreamSynchronize(st);
+  if (he == hipSuccess) he = hipStreamSynchronize(st);  // the host vectors above go out of scope
   if (he != hipSuccess) {
     free_handle(h);
     return fail(HASTAR_EDEVICE, std::string("init: ") + hipGetErrorString(he));
@@ -328,6 +442,7 @@ int hastar_destroy(hastar_handle h) {
 int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3]) {
   if (!h || !goal || !start) return fail(HASTAR_EINVAL, "null argument");
   HIPCHK(hipSetDevice(h->device));
+  DeviceCtx& DC = *h->dc;
   PlannerDev& D = h->desc;
   const float gh_prev = h->grid_heading;
   const float g3px = h->goal3x, g3py = h->goal3y;
@@ -344,13 +459,11 @@ int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3
   V2 org{(float)D.n45 + gno.x / D.res, (float)D.n2 + gno.y / D.res};
   org = {org.x - gp.x, org.y - gp.y};
   {
-    std::lock_guard<std::mutex> lk(g_scratch[h->device & 63].mu);
-    DeviceScratch* S = nullptr;
+    std::lock_guard<std::mutex> lk(DC.mu);
     const size_t NN = (size_t)D.N * D.N;
-    if (int rc = scratch_acquire(h->device, NN, h->stream, &S)) return rc;
-    HIPCHK(launch_relocate(D.N, g_cosf(dh), g_sinf(dh), org.x, org.y, D.occ, S->tmp, S->winner, h->stream));
-    HIPCHK(hipMemcpyAsync(D.occ, S->tmp, NN * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    if (int rc = scratch_acquire(DC, NN)) return rc;
+    HIPCHK(launch_relocate(D.N, g_cosf(dh), g_sinf(dh), org.x, org.y, D.occ, DC.tmp, DC.winner, DC.stream));
+    HIPCHK(hipMemcpyAsync(D.occ, DC.tmp, NN * sizeof(float), hipMemcpyDeviceToDevice, DC.stream));
   }
   // the goal node (Grid3D.cpp:115-123)
   D.goal_x = D.n45 * D.res;
@@ -365,7 +478,6 @@ int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3
   D.rot_c = g_cosf(-gh);
   D.rot_s = g_sinf(-gh);
   h->goal_set = true;
-  HIPCHK(hipStreamSynchronize(h->stream));
   return HASTAR_OK;
 }
 
@@ -373,8 +485,7 @@ int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3
 int hastar_reset(hastar_handle h) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipMemsetAsync(h->desc.visited, 0, (size_t)h->desc.N * h->desc.N, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemsetAsync(h->desc.visited, 0, (size_t)h->desc.N * h->desc.N, h->dc->stream));
   return HASTAR_OK;
 }
 
@@ -382,8 +493,7 @@ int hastar_reset(hastar_handle h) {
 int hastar_decay(hastar_handle h) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(launch_decay(h->desc.occ, (size_t)h->desc.N * h->desc.N, h->lp_free, h->lp_min, h->lp_max, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(launch_decay(h->desc.occ, (size_t)h->desc.N * h->desc.N, h->lp_free, h->lp_min, h->lp_max, h->dc->stream));
   return HASTAR_OK;
 }
 
@@ -391,6 +501,7 @@ int hastar_decay(hastar_handle h) {
 int hastar_update_boxes(hastar_handle h, const float* boxes, const float* conf, int n, float apf_added_radius) {
   if (!h || n < 0 || (n > 0 && (!boxes || !conf))) return fail(HASTAR_EINVAL, "bad argument");
   HIPCHK(hipSetDevice(h->device));
+  DeviceCtx& DC = *h->dc;
   PlannerDev& D = h->desc;
   const float gh = h->grid_heading;
   std::vector<float> apf((size_t)std::max(n, 1) * 3);
@@ -407,43 +518,42 @@ int hastar_update_boxes(hastar_handle h, const float* boxes, const float* conf, 
     const V2 bl = rot2((ox - dx / 2) - h->goal2x, (oy - dy / 2) - h->goal2y, gh);
     rp[4 * k] = gmath::x86_trunc_int(std::round(bl.x / D.res) + (float)D.n45);
     rp[4 * k + 1] = gmath::x86_trunc_int(std::round(bl.y / D.res) + (float)D.n2);
-    rp[4 * k + 2] = 2 * gmath::x86_trunc_int(std::ceil(dx / D.res));
-    rp[4 * k + 3] = 2 * gmath::x86_trunc_int(std::ceil(dy / D.res));
-    if (rp[4 * k + 2] < 0) rp[4 * k + 2] = 0;
-    if (rp[4 * k + 3] < 0) rp[4 * k + 3] = 0;
+    rp[4 * k + 2] = std::max(0, 2 * gmath::x86_trunc_int(std::ceil(dx / D.res)));
+    rp[4 * k + 3] = std::max(0, 2 * gmath::x86_trunc_int(std::ceil(dy / D.res)));
     const float lc = (float)std::log((double)conf[k] / (1.0 - (double)conf[k]));
     dl[k] = lc - h->lp_free;
   }
-  if (n > h->apf_cap) {
-    if (D.apf) hipFree(D.apf);
-    D.apf = nullptr;
-    h->apf_cap = 0;
-    HIPCHK(dalloc(&D.apf, (size_t)n * 3));
-    h->apf_cap = n;
-  }
-  if (n > h->rp_cap) {
-    if (h->d_rp) hipFree(h->d_rp);
-    if (h->d_dl) hipFree(h->d_dl);
-    h->d_rp = nullptr;
-    h->d_dl = nullptr;
-    h->rp_cap = 0;
-    HIPCHK(dalloc(&h->d_rp, (size_t)n * 4));
-    HIPCHK(dalloc(&h->d_dl, (size_t)n));
-    h->rp_cap = n;
+  if (n > h->apf_cap || n > h->rp_cap) {
+    HIPCHK(hipStreamSynchronize(DC.stream));  // buffers may still be read by queued work
+    if (n > h->apf_cap) {
+      if (D.apf) hipFree(D.apf);
+      D.apf = nullptr;
+      h->apf_cap = 0;
+      HIPCHK(dalloc(&D.apf, (size_t)n * 3));
+      h->apf_cap = n;
+    }
+    if (n > h->rp_cap) {
+      if (h->d_rp) hipFree(h->d_rp);
+      if (h->d_dl) hipFree(h->d_dl);
+      h->d_rp = nullptr;
+      h->d_dl = nullptr;
+      h->rp_cap = 0;
+      HIPCHK(dalloc(&h->d_rp, (size_t)n * 4));
+      HIPCHK(dalloc(&h->d_dl, (size_t)n));
+      h->rp_cap = n;
+    }
   }
   D.n_apf = n;
   if (n > 0) {
-    HIPCHK(hipMemcpyAsync(D.apf, apf.data(), (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, h->stream));
-    HIPCHK(hipMemcpyAsync(h->d_rp, rp.data(), (size_t)n * 4 * sizeof(int), hipMemcpyHostToDevice, h->stream));
-    HIPCHK(hipMemcpyAsync(h->d_dl, dl.data(), (size_t)n * sizeof(float), hipMemcpyHostToDevice, h->stream));
-    std::lock_guard<std::mutex> lk(g_scratch[h->device & 63].mu);
-    DeviceScratch* S = nullptr;
-    if (int rc = scratch_acquire(h->device, (size_t)D.N * D.N, h->stream, &S)) return rc;
-    HIPCHK(launch_raster_boxes(D.occ, S->cnt, D.N, h->d_rp, h->d_dl, n, g_cosf(gh), g_sinf(gh), h->lp_min,
-                               h->lp_max, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    // pageable sources: hipMemcpyAsync returns after staging, so the vectors may go
+    HIPCHK(hipMemcpyAsync(D.apf, apf.data(), (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, DC.stream));
+    HIPCHK(hipMemcpyAsync(h->d_rp, rp.data(), (size_t)n * 4 * sizeof(int), hipMemcpyHostToDevice, DC.stream));
+    HIPCHK(hipMemcpyAsync(h->d_dl, dl.data(), (size_t)n * sizeof(float), hipMemcpyHostToDevice, DC.stream));
+    std::lock_guard<std::mutex> lk(DC.mu);
+    if (int rc = scratch_acquire(DC, (size_t)D.N * D.N)) return rc;
+    HIPCHK(launch_raster_boxes(D.occ, DC.cnt, D.N, h->d_rp, h->d_dl, n, g_cosf(gh), g_sinf(gh), h->lp_min,
+                               h->lp_max, DC.stream));
   }
-  HIPCHK(hipStreamSynchronize(h->stream));
   return HASTAR_OK;
 }
 
@@ -451,6 +561,7 @@ int hastar_update_boxes(hastar_handle h, const float* boxes, const float* conf, 
 int hastar_update_lines(hastar_handle h, const float* lines, const float* conf, int n, float width) {
   if (!h || n < 0 || (n > 0 && (!lines || !conf))) return fail(HASTAR_EINVAL, "bad argument");
   HIPCHK(hipSetDevice(h->device));
+  DeviceCtx& DC = *h->dc;
   PlannerDev& D = h->desc;
   if (n == 0) return HASTAR_OK;
   const float gh = h->grid_heading;
@@ -484,36 +595,34 @@ int hastar_update_lines(hastar_handle h, const float* lines, const float* conf, 
     L[7] = (float)cntl;
     L[8] = (float)wid.size();
   }
-  if (n > h->lp_cap) {
-    if (h->d_lp) hipFree(h->d_lp);
-    if (h->d_seq) hipFree(h->d_seq);
-    h->d_lp = nullptr;
-    h->d_seq = nullptr;
-    h->lp_cap = 0;
-    HIPCHK(dalloc(&h->d_lp, (size_t)n * 9));
-    HIPCHK(dalloc(&h->d_seq, (size_t)n * stride));
-    h->lp_cap = n;
+  if (wid.empty()) return HASTAR_OK;
+  if (n > h->lp_cap || (int)wid.size() > h->wid_cap) {
+    HIPCHK(hipStreamSynchronize(DC.stream));
+    if (n > h->lp_cap) {
+      if (h->d_lp) hipFree(h->d_lp);
+      if (h->d_seq) hipFree(h->d_seq);
+      h->d_lp = nullptr;
+      h->d_seq = nullptr;
+      h->lp_cap = 0;
+      HIPCHK(dalloc(&h->d_lp, (size_t)n * 9));
+      HIPCHK(dalloc(&h->d_seq, (size_t)n * stride));
+      h->lp_cap = n;
+    }
+    if ((int)wid.size() > h->wid_cap) {
+      if (h->d_wid) hipFree(h->d_wid);
+      h->d_wid = nullptr;
+      h->wid_cap = 0;
+      HIPCHK(dalloc(&h->d_wid, wid.size()));
+      h->wid_cap = (int)wid.size();
+    }
   }
-  if ((int)wid.size() > h->wid_cap) {
-    if (h->d_wid) hipFree(h->d_wid);
-    h->d_wid = nullptr;
-    h->wid_cap = 0;
-    HIPCHK(dalloc(&h->d_wid, wid.size()));
-    h->wid_cap = (int)wid.size();
-  }
-  HIPCHK(hipMemcpyAsync(h->d_lp, lp.data(), lp.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->d_seq, seq.data(), seq.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
-  if (!wid.empty())
-    HIPCHK(hipMemcpyAsync(h->d_wid, wid.data(), wid.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
-  if (!wid.empty()) {
-    std::lock_guard<std::mutex> lk(g_scratch[h->device & 63].mu);
-    DeviceScratch* S = nullptr;
-    if (int rc = scratch_acquire(h->device, (size_t)D.N * D.N, h->stream, &S)) return rc;
-    HIPCHK(launch_raster_lines(D.occ, S->cnt, D.N, D.n45, D.n2, D.res, h->d_lp, h->d_seq, h->d_wid, stride, n,
-                               h->lp_min, h->lp_max, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-  }
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpyAsync(h->d_lp, lp.data(), lp.size() * sizeof(float), hipMemcpyHostToDevice, DC.stream));
+  HIPCHK(hipMemcpyAsync(h->d_seq, seq.data(), seq.size() * sizeof(float), hipMemcpyHostToDevice, DC.stream));
+  HIPCHK(hipMemcpyAsync(h->d_wid, wid.data(), wid.size() * sizeof(float), hipMemcpyHostToDevice, DC.stream));
+  std::lock_guard<std::mutex> lk(DC.mu);
+  if (int rc = scratch_acquire(DC, (size_t)D.N * D.N)) return rc;
+  HIPCHK(launch_raster_lines(D.occ, DC.cnt, D.N, D.n45, D.n2, D.res, h->d_lp, h->d_seq, h->d_wid, stride, n, h->lp_min,
+                             h->lp_max, DC.stream));
   return HASTAR_OK;
 }
 
@@ -521,8 +630,8 @@ int hastar_get_obstacles(hastar_handle h, float* out) {
   if (!h || !out) return fail(HASTAR_EINVAL, "null argument");
   HIPCHK(hipSetDevice(h->device));
   const size_t NN = (size_t)h->desc.N * h->desc.N;
-  HIPCHK(hipMemcpyAsync(out, h->desc.occ, NN * sizeof(float), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpyAsync(out, h->desc.occ, NN * sizeof(float), hipMemcpyDeviceToHost, h->dc->stream));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
   return HASTAR_OK;
 }
 
@@ -591,52 +700,64 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     return fail(HASTAR_EINVAL, "bad argument");
   const int dev = hs[0] ? hs[0]->device : -1;
   int max_pops = 0;
+  ArenaReq need;
   for (int i = 0; i < n; ++i) {
     if (!hs[i] || hs[i]->device != dev) return fail(HASTAR_EINVAL, "null handle or handles on different devices");
     if (!hs[i]->goal_set) return fail(HASTAR_EINVAL, "update_goal must be called before find_path");
     max_pops = std::max(max_pops, hs[i]->max_pops);
+    need.merge(hs[i]->areq);
   }
   HIPCHK(hipSetDevice(dev));
-  hastar_handle h0 = hs[0];
-  hipStream_t st = h0->stream;
-  // descriptors of all planners, contiguous on the device
-  static thread_local PlannerDev* d_batch = nullptr;
-  static thread_local int d_batch_cap = 0;
-  static thread_local int d_batch_dev = -1;
+  DeviceCtx& DC = *hs[0]->dc;
+  std::lock_guard<std::mutex> lk(DC.mu);
+  hipStream_t st = DC.stream;
+  const int W = std::max(1, std::min(n, DC.resident_slots));
+  if (int rc = arenas_acquire(DC, need, W)) return rc;
+  const int slots = std::min(W, DC.n_arenas);
+  if (n > DC.batch_cap) {
+    HIPCHK(hipStreamSynchronize(st));
+    if (DC.d_descs) hipFree(DC.d_descs);
+    if (DC.d_order) hipFree(DC.d_order);
+    DC.d_descs = nullptr;
+    DC.d_order = nullptr;
+    DC.batch_cap = 0;
+    HIPCHK(dalloc(&DC.d_descs, (size_t)n));
+    HIPCHK(dalloc(&DC.d_order, (size_t)n));
+    DC.batch_cap = n;
+  }
   std::vector<PlannerDev> descs(n);
   for (int i = 0; i < n; ++i) {
     prepare_start(hs[i], vel[i], starts + 3 * i);
     descs[i] = hs[i]->desc;
   }
-  if (n > d_batch_cap || d_batch_dev != dev) {
-    if (d_batch) hipFree(d_batch);
-    d_batch = nullptr;
-    d_batch_cap = 0;
-    HIPCHK(dalloc(&d_batch, (size_t)n));
-    d_batch_cap = n;
-    d_batch_dev = dev;
-  }
-  HIPCHK(hipMemcpyAsync(d_batch, descs.data(), (size_t)n * sizeof(PlannerDev), hipMemcpyHostToDevice, st));
-  HIPCHK(hipEventRecord(h0->ev0, st));
-  HIPCHK(launch_search(d_batch, n, max_pops, st));
-  HIPCHK(hipEventRecord(h0->ev1, st));
+  // longest-expected-first: planners ordered by the pops of their previous search
+  std::vector<int> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return hs[a]->last_pops > hs[b]->last_pops; });
+  HIPCHK(hipMemcpyAsync(DC.d_descs, descs.data(), (size_t)n * sizeof(PlannerDev), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(DC.d_order, order.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
+  HIPCHK(hipEventRecord(DC.ev0, st));
+  HIPCHK(launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, DC.d_next, max_pops, st));
+  HIPCHK(hipEventRecord(DC.ev1, st));
   std::vector<SearchResult> res(n);
   for (int i = 0; i < n; ++i)
     HIPCHK(hipMemcpyAsync(&res[i], hs[i]->desc.result, sizeof(SearchResult), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   float ms = 0.0f;
-  hipEventElapsedTime(&ms, h0->ev0, h0->ev1);
+  hipEventElapsedTime(&ms, DC.ev0, DC.ev1);
   g_last_ms = ms;
   int rc = HASTAR_OK;
   for (int i = 0; i < n; ++i) {
     hs[i]->last = res[i];
     hs[i]->have_last = true;
+    hs[i]->last_pops = res[i].pops + res[i].astar_pops;
     ok[i] = res[i].ok;
     cost[i] = res[i].ok ? res[i].cost : FLT_MAX;
     fill_stats(res[i], stats ? &stats[i] : nullptr);
     if (res[i].status != 0 && rc == HASTAR_OK) {
-      rc = res[i].status == -75 ? HASTAR_EOVERFLOW : HASTAR_EDEVICE;
-      g_err = "search arena overflow (raise max_pops / max_astar_nodes)";
+      rc = res[i].status == -75 ? HASTAR_EOVERFLOW : HASTAR_ENOSPC;
+      g_err = res[i].status == -75 ? "search arena overflow (raise max_pops / max_astar_nodes)"
+                                   : "path longer than the planner's output buffer";
     }
     int r = copy_path_out(hs[i], xyh ? xyh + (size_t)i * cap * 3 : nullptr, curv ? curv + (size_t)i * cap : nullptr,
                           cap, &len[i], st);
@@ -649,8 +770,8 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
 int hastar_copy_path(hastar_handle h, float* xyh, float* curv, int cap, int* len) {
   if (!h || !h->have_last) return fail(HASTAR_EINVAL, "no search result");
   HIPCHK(hipSetDevice(h->device));
-  int r = copy_path_out(h, xyh, curv, cap, len, h->stream);
-  HIPCHK(hipStreamSynchronize(h->stream));
+  int r = copy_path_out(h, xyh, curv, cap, len, h->dc->stream);
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
   return r;
 }
 
@@ -677,6 +798,7 @@ int hastar_test_field(hastar_handle h, const float* poses, int n, float* out) {
   if (!h || n < 0) return fail(HASTAR_EINVAL, "bad argument");
   if (n == 0) return HASTAR_OK;
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
   float *dp = nullptr, *dout = nullptr;
   HIPCHK(dalloc(&dp, (size_t)n * 3));
   HIPCHK(dalloc(&dout, (size_t)n));
@@ -709,6 +831,7 @@ int hastar_test_dubins_path(hastar_handle h, const float start[3], float* xyh, f
                             float* length, int* first_arc_gt_90) {
   if (!h || !h->goal_set) return fail(HASTAR_EINVAL, "bad handle / no goal");
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
   float *dx = nullptr, *dc = nullptr, *dl = nullptr;
   int *dn = nullptr, *df = nullptr;
   HIPCHK(dalloc(&dx, (size_t)cap * 3));
@@ -735,6 +858,7 @@ int hastar_test_dubins_path(hastar_handle h, const float start[3], float* xyh, f
 int hastar_debug_memo(hastar_handle h, float* f_out, unsigned char* visited_out) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
   const size_t NN = (size_t)h->desc.N * h->desc.N;
   HIPCHK(hipMemcpy(f_out, h->desc.nm_f, NN * sizeof(float), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(visited_out, h->desc.visited, NN, hipMemcpyDeviceToHost));
@@ -746,6 +870,7 @@ int hastar_debug_apf(hastar_handle h, float* out, int cap) {
   const int n = h->desc.n_apf;
   if (n > cap) return n;
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
   if (n) HIPCHK(hipMemcpy(out, h->desc.apf, (size_t)n * 3 * sizeof(float), hipMemcpyDeviceToHost));
   return n;
 }
@@ -754,6 +879,7 @@ int hastar_debug_motion(hastar_handle h, float* off, float* dth, float* cost, fl
                         float* r_min) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
   const PlannerDev& D = h->desc;
   const int ns = D.nsteer;
   HIPCHK(hipMemcpy(off, D.off, (size_t)ns * (D.bins + 1) * 2 * sizeof(float), hipMemcpyDeviceToHost));
@@ -778,12 +904,20 @@ int hastar_debug_astar_modes(hastar_handle h, long long* out2) {
   return HASTAR_OK;
 }
 
+// Closed-set keys of the last search.  The closed records live in the slot arena that
+// ran it, so this hook is only meaningful right after a single-planner find_path.
 int hastar_debug_closed_keys(hastar_handle h, int* out, int cap) {
   if (!h || !h->have_last) return fail(HASTAR_EINVAL, "no search result");
   HIPCHK(hipSetDevice(h->device));
+  DeviceCtx& DC = *h->dc;
+  std::lock_guard<std::mutex> lk(DC.mu);
+  HIPCHK(hipStreamSynchronize(DC.stream));
+  if (DC.n_arenas < 1) return fail(HASTAR_EINVAL, "no arena");
+  SlotArena A0;
+  HIPCHK(hipMemcpy(&A0, DC.d_arenas, sizeof(SlotArena), hipMemcpyDeviceToHost));
   const int n = (int)h->last.closed_size;
   std::vector<Closed3> rec(n);
-  if (n) HIPCHK(hipMemcpy(rec.data(), h->desc.closed3, (size_t)n * sizeof(Closed3), hipMemcpyDeviceToHost));
+  if (n) HIPCHK(hipMemcpy(rec.data(), A0.closed3, (size_t)n * sizeof(Closed3), hipMemcpyDeviceToHost));
   std::vector<long long> k(n);
   for (int i = 0; i < n; ++i) {
     const uint32_t kk = rec[i].key;

@@ -40,7 +40,8 @@ struct Succ {
 };
 
 struct SearchCtx {
-  const PlannerDev* __restrict__ P;   // descriptor in HBM (uniform, read-only: scalar loads)
+  const PlannerDev* __restrict__ P;   // planner descriptor in HBM (uniform, read-only: scalar loads)
+  const SlotArena* __restrict__ A;    // this wave's search arena
   int lane;
   RBTree<Node3, GAS Node3*> o3;
   PoolState ps3, ps2;
@@ -67,13 +68,14 @@ __device__ __forceinline__ uint32_t slot_hash(uint32_t k) {
 // copy of the popped open node.
 __device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n) {
   const PlannerDev& P = *c.P;
-  uint32_t h = slot_hash(n.key) & P.slots3_mask;
+  const SlotArena& A = *c.A;
+  uint32_t h = slot_hash(n.key) & A.slots3_mask;
   for (;;) {
-    auto s = &gp(P.slots3)[h];
+    auto s = &gp(A.slots3)[h];
     if (s->gen != c.gen3) {
-      if (c.n_closed3 >= P.closed3_cap) return NIL;
+      if (c.n_closed3 >= A.closed3_cap) return NIL;
       const int idx = c.n_closed3++;
-      auto r = &gp(P.closed3)[idx];
+      auto r = &gp(A.closed3)[idx];
       r->key = n.key;
       r->g = n.g;
       r->f = n.f;
@@ -89,18 +91,19 @@ __device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n) {
       return idx;
     }
     if (s->key == n.key) return s->idx;
-    h = (h + 1) & P.slots3_mask;
+    h = (h + 1) & A.slots3_mask;
   }
 }
 
 __device__ __forceinline__ bool closed3_contains(const SearchCtx& c, uint32_t key) {
   const PlannerDev& P = *c.P;
-  uint32_t h = slot_hash(key) & P.slots3_mask;
+  const SlotArena& A = *c.A;
+  uint32_t h = slot_hash(key) & A.slots3_mask;
   for (;;) {
-    const Slot3 s = gload(&gp(P.slots3)[h]);
+    const Slot3 s = gload(&gp(A.slots3)[h]);
     if (s.gen != c.gen3) return false;
     if (s.key == key) return true;
-    h = (h + 1) & P.slots3_mask;
+    h = (h + 1) & A.slots3_mask;
   }
 }
 
@@ -144,6 +147,7 @@ __device__ __forceinline__ void lds_closed_put(AStarLds& L, uint32_t cell, int i
 template <bool G, class CP>
 __device__ __forceinline__ void memoise(SearchCtx& c, CP cl, float total, int from) {
   const PlannerDev& P = *c.P;
+  const SlotArena& A = *c.A;
   for (int i = from; i != NIL; i = cl[i].prev) {
     const Closed2 r = gload(&cl[i]);
     const size_t cell = (size_t)(r.key >> 16) * P.N + (r.key & 0xffffu);
@@ -175,22 +179,23 @@ __device__ __forceinline__ bool insert2(SearchCtx& c, RBTree<Node2, NP>& tr, int
 template <bool G>
 __device__ __forceinline__ bool astar_loop(SearchCtx& c, AStarLds& L, int adx, int ady, float acost, float* result) {
   const PlannerDev& P = *c.P;
+  const SlotArena& A = *c.A;
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
   typedef typename std::conditional<G, GAS Node2*, Node2*>::type NP;
   typedef typename std::conditional<G, GAS Closed2*, Closed2*>::type CP;
-  RBTree<Node2, NP> tr{G ? (NP)gp(P.open2) : (NP)L.open};
-  CP cl = G ? (CP)gp(P.closed2) : (CP)L.closed;
-  const int cap = G ? P.open2_cap : A_CAP;
+  RBTree<Node2, NP> tr{G ? (NP)gp(A.open2) : (NP)L.open};
+  CP cl = G ? (CP)gp(A.closed2) : (CP)L.closed;
+  const int cap = G ? A.open2_cap : A_CAP;
   while (!tr.empty()) {
     if (!G && (c.ps2.next + 8 > A_CAP || c.n_closed2 + 1 > A_CCAP)) return false;
     const int b = tr.begin();
     const Node2 top = gload(&tr.t[b]);
     const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
     const uint32_t tcell = (uint32_t)tx * (uint32_t)P.N + (uint32_t)ty;
-    int ci = G ? ((gp(P.cgen2)[tcell] == c.gen2) ? gp(P.cidx2)[tcell] : NIL) : lds_closed_find(L, tcell);
+    int ci = G ? ((gp(A.cgen2)[tcell] == c.gen2) ? gp(A.cidx2)[tcell] : NIL) : lds_closed_find(L, tcell);
     if (ci == NIL) {  // new closed element (duplicates expand the old one, AStar.cpp:130)
-      if (c.n_closed2 >= (G ? P.closed2_cap : A_CCAP)) { c.status = -75; *result = FLT_MAX; return true; }
+      if (c.n_closed2 >= (G ? A.closed2_cap : A_CCAP)) { c.status = -75; *result = FLT_MAX; return true; }
       ci = c.n_closed2++;
       auto r = &cl[ci];
       r->key = top.key;
@@ -198,8 +203,8 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, AStarLds& L, int adx, i
       r->f = top.f;
       r->prev = top.prev;
       if (G) {
-        gp(P.cgen2)[tcell] = c.gen2;
-        gp(P.cidx2)[tcell] = ci;
+        gp(A.cgen2)[tcell] = c.gen2;
+        gp(A.cidx2)[tcell] = ci;
       } else {
         if (lane == 0) lds_closed_put(L, tcell, ci);
         __syncthreads();
@@ -228,7 +233,7 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, AStarLds& L, int adx, i
       const float occv = gp(P.occ)[cell];
       const uint8_t visv = gp(P.visited)[cell];
       nf = gp(P.nm_f)[cell];
-      const bool clv = G ? (gp(P.cgen2)[cell] == c.gen2) : (lds_closed_find(L, cell) != NIL);
+      const bool clv = G ? (gp(A.cgen2)[cell] == c.gen2) : (lds_closed_find(L, cell) != NIL);
       valid = occv < P.thr;
       vis = valid && visv != 0;
       closed = valid && clv;
@@ -270,6 +275,7 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, AStarLds& L, int adx, i
 // AStar::find_path(int, int) (AStar.cpp:100-113)
 __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, int sj) {
   const PlannerDev& P = *c.P;
+  const SlotArena& A = *c.A;
   const int lane = c.lane;
   const size_t s_cell = (size_t)si * P.N + sj;
   if (gp(P.visited)[s_cell]) return gp(P.nm_f)[s_cell];
@@ -300,13 +306,13 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   if (astar_loop<false>(c, L, adx, ady, acost, &result)) return result;
   // migrate the LDS state to HBM (identical indices) and continue there
   c.amigr++;
-  for (int i = lane; i < c.ps2.next; i += 64) gstore(&gp(P.open2)[i], L.open[i]);
+  for (int i = lane; i < c.ps2.next; i += 64) gstore(&gp(A.open2)[i], L.open[i]);
   for (int i = lane; i < c.n_closed2; i += 64) {
     const Closed2 r = L.closed[i];
-    gstore(&gp(P.closed2)[i], r);
+    gstore(&gp(A.closed2)[i], r);
     const size_t cell = (size_t)(r.key >> 16) * P.N + (r.key & 0xffffu);
-    gp(P.cgen2)[cell] = c.gen2;
-    gp(P.cidx2)[cell] = i;
+    gp(A.cgen2)[cell] = c.gen2;
+    gp(A.cidx2)[cell] = i;
   }
   __syncthreads();
   STAMP_T tg = STAMP_NOW();
@@ -320,9 +326,9 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, in
   const uint32_t key = key3(s.cx, s.cy, s.bin);
   const int pos = c.o3.insert_pos(key, f, &left);
   if (pos == -2) return true;
-  const int n = pool_alloc(gp(c.P->open3), c.ps3, c.P->open3_cap);
+  const int n = pool_alloc(gp(c.A->open3), c.ps3, c.A->open3_cap);
   if (n == NIL) return false;
-  auto d = &gp(c.P->open3)[n];
+  auto d = &gp(c.A->open3)[n];
   d->key = key;
   d->f = f;
   d->g = s.g;
@@ -337,22 +343,17 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, in
 }
 
 // ------------------------------------------------------------------- the search -------
-__global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners,
-                                                           int max_pops) {
-  if ((int)blockIdx.x >= n_planners) return;
-  __shared__ Succ sl[MAXS];
-  __shared__ AStarLds alds;
-  SearchCtx c;
-  c.P = descs + blockIdx.x;
+// One find_path (HybridAStar.cpp:68-88 incl. hybrid_a_star_search 93-199 and
+// reconstruct_path 208-262) of planner *c.P in arena *c.A, run by one wavefront.
+__device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& alds, int max_pops) {
   const PlannerDev& P = *c.P;
+  const SlotArena& A = *c.A;
+  const int lane = c.lane;
 #ifdef HASTAR_STAMPS
   for (int q = 0; q < 8; ++q) c.cyc[q] = 0;
 #endif
-  const int lane = threadIdx.x;
-  c.lane = lane;
-  c.o3.t = gp(P.open3);
-  c.gen3 = gp(P.gens)[0] + 1;
-  c.gen2 = gp(P.gens)[1];
+  c.o3.t = gp(A.open3);
+  c.gen3 += 1;
   c.n_closed3 = 0;
   c.n_closed2 = 0;
   c.pops = c.succ = c.apops = c.asearch = c.shots = c.amigr = c.apops_g = 0;
@@ -390,13 +391,13 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
     if (c.pops >= max_pops) { c.status = -75; break; }
     STAMP_T tp = STAMP_NOW();
     const int b = c.o3.begin();
-    const Node3 top = gload(&gp(P.open3)[b]);
+    const Node3 top = gload(&gp(A.open3)[b]);
     const int ci = closed3_insert(c, top);
     if (ci == NIL) { c.status = -75; break; }
     c.o3.unlink(b);
-    pool_free(gp(P.open3), c.ps3, b);
+    pool_free(gp(A.open3), c.ps3, b);
     c.pops++;
-    const Closed3 cur = gload(&gp(P.closed3)[ci]);
+    const Closed3 cur = gload(&gp(A.closed3)[ci]);
     const int cx = key3_x(cur.key), cy = key3_y(cur.key), cbin = key3_bin(cur.key);
     dig = mix64(dig ^ digest_key(cur.key)) + (uint64_t)fbits(cur.g);
     STAMP_ADD(0, tp);
@@ -416,11 +417,11 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
         // Dubins::get_shortest_path (Dubins.cpp:125-153)
         const float L = dubins_shortest(r, cur.x, cur.y, cur.h, P.goal_x, P.goal_y, P.goal_h, &word, prm);
         const Centres C = dubins_centres(r, cur.x, cur.y, cur.h, P.goal_x, P.goal_y, P.goal_h);
-        const int n = dubins_sample(P, C, word, prm, gp(P.dub_xyh), gp(P.dub_curv), P.dub_cap, lane);
+        const int n = dubins_sample(P, C, word, prm, gp(A.dub_xyh), gp(A.dub_curv), A.dub_cap, lane);
         if (n < 0) { c.status = -75; break; }
         __syncthreads();
         const bool first_arc_long = fabsf(prm[1]) > (float)M_PI_2;
-        if (!first_arc_long && path_is_free(P, gp(P.dub_xyh), n, lane)) {
+        if (!first_arc_long && path_is_free(P, gp(A.dub_xyh), n, lane)) {
           terminal = cur.prev;
           cost = cur.g + L;
           ok = 1;
@@ -507,9 +508,9 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
         STAMP_ADD(3, ta);
         const float f = s.g + stl_max(h1, s.dub);
         if (!insert3(c, s, f, ci)) { fail = true; break; }
-      } else if (s.g < gp(P.open3)[hit].g) {
+      } else if (s.g < gp(A.open3)[hit].g) {
         c.o3.unlink(hit);
-        pool_free(gp(P.open3), c.ps3, hit);
+        pool_free(gp(A.open3), c.ps3, hit);
         STAMP_T ta = STAMP_NOW();
         const float h1 = holonomic(c, alds, s.cx, s.cy);
         STAMP_ADD(3, ta);
@@ -531,9 +532,9 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
   int path_len = 0;
   if (ok) {
     int L = 0;
-    for (int i = terminal; i != NIL; i = gp(P.closed3)[i].prev) {
-      if (dub_n + L >= P.out_cap) { c.status = -28; break; }
-      if (lane == 0) gp(P.out_chain)[L] = i;
+    for (int i = terminal; i != NIL; i = gp(A.closed3)[i].prev) {
+      if (dub_n + L >= P.out_cap || L >= A.chain_cap) { c.status = -28; break; }
+      if (lane == 0) gp(A.out_chain)[L] = i;
       ++L;
     }
     __syncthreads();
@@ -545,13 +546,13 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
         bool has_curv = true;
         if (k < dub_n) {
           const int q = dub_n - 1 - k;
-          px = gp(P.dub_xyh)[3 * q];
-          py = gp(P.dub_xyh)[3 * q + 1];
-          ph = gp(P.dub_xyh)[3 * q + 2];
-          kc = gp(P.dub_curv)[q];
+          px = gp(A.dub_xyh)[3 * q];
+          py = gp(A.dub_xyh)[3 * q + 1];
+          ph = gp(A.dub_xyh)[3 * q + 2];
+          kc = gp(A.dub_curv)[q];
         } else {
           const int m = k - dub_n;
-          const Closed3 nd = gload(&gp(P.closed3)[gp(P.out_chain)[m]]);
+          const Closed3 nd = gload(&gp(A.closed3)[gp(A.out_chain)[m]]);
           px = nd.x;
           py = nd.y;
           ph = nd.h;
@@ -577,7 +578,7 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
 
   // ---- statistics: closed-set digest (order independent) and counters
   uint64_t cd = 0;
-  for (int i = lane; i < c.n_closed3; i += 64) cd += mix64(digest_key(gp(P.closed3)[i].key));
+  for (int i = lane; i < c.n_closed3; i += 64) cd += mix64(digest_key(gp(A.closed3)[i].key));
   cd = wave_sum_u64(cd);
   __syncthreads();
   STAMP_ADD(5, trc);
@@ -605,8 +606,36 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
 #else
     for (int q = 0; q < 8; ++q) R->cycles[q] = 0;
 #endif
-    gp(P.gens)[0] = c.gen3;
-    gp(P.gens)[1] = c.gen2;
+  }
+  __syncthreads();
+}
+
+// Persistent work-queue kernel: grid = W resident slots (one wavefront each).  Each slot
+// pulls planner indices (in `order`, longest-expected-first when the host knows) from a
+// device counter until the queue is drained, so early finishers take the next planner.
+__global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners,
+                                                           const SlotArena* __restrict__ arenas,
+                                                           const int* __restrict__ order, int* __restrict__ next,
+                                                           int max_pops) {
+  __shared__ Succ sl[MAXS];
+  __shared__ AStarLds alds;
+  SearchCtx c;
+  c.A = arenas + blockIdx.x;
+  const SlotArena& A = *c.A;
+  c.lane = threadIdx.x;
+  c.gen3 = gp(A.gens)[0];
+  c.gen2 = gp(A.gens)[1];
+  for (;;) {
+    int q = 0;
+    if (c.lane == 0) q = atomicAdd(next, 1);
+    q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
+    if (q >= n_planners) break;
+    c.P = descs + order[q];
+    search_one(c, sl, alds, max_pops);
+  }
+  if (c.lane == 0) {
+    gp(A.gens)[0] = c.gen3;
+    gp(A.gens)[1] = c.gen2;
   }
 }
 
@@ -796,9 +825,18 @@ __global__ __launch_bounds__(64) void k_test_dubins_path(PlannerDev P, float sx,
 }
 
 // ------------------------------------------------------------- launch wrappers -------
-hipError_t launch_search(const PlannerDev* d_descs, int n, int max_pops, hipStream_t st) {
-  hipLaunchKernelGGL(hastar_search_kernel, dim3(n), dim3(64), 0, st, d_descs, n, max_pops);
+hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots, const int* d_order,
+                         int* d_next, int max_pops, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(d_next, 0, sizeof(int), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(hastar_search_kernel, dim3(n_slots), dim3(64), 0, st, d_descs, n, d_arenas, d_order, d_next,
+                     max_pops);
   return hipGetLastError();
+}
+int search_slots_per_cu() {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, hastar_search_kernel, 64, 0) != hipSuccess) return 1;
+  return nb > 0 ? nb : 1;
 }
 hipError_t launch_init_nodemap(const PlannerDev& P, hipStream_t st) {
   hipLaunchKernelGGL(k_init_nodemap, dim3(1024), dim3(256), 0, st, P);

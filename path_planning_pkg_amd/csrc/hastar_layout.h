@@ -108,17 +108,29 @@ struct PlannerDev {
   float* dth;            // nsteer  _offset_heading
   float* act_cost;       // nsteer  _actions_cost
   float* curv_abs;       // nsteer  _abs_curvatures
-  // --- arenas
-  Node3* open3;   int open3_cap;  int pad_a0;
-  Closed3* closed3; int closed3_cap; int pad_a1;
-  Slot3* slots3;  uint32_t slots3_mask; int pad_a7;
-  Node2* open2;   int open2_cap;  int pad_a2;
-  Closed2* closed2; int closed2_cap; int pad_a3;
-  uint32_t* cgen2; int* cidx2;
-  uint32_t* gens;        // [0] closed-set generation, [1] A* closed generation (kernel-owned)
-  float* dub_xyh; float* dub_curv; int dub_cap; int pad_a5;
-  float* out_xyh; float* out_curv; int* out_chain; int out_cap; int pad_a6;
+  float* out_xyh;        // reconstructed path (out_cap x 3) and curvature (out_cap)
+  float* out_curv;
+  int out_cap;
+  int pad_o0;
   SearchResult* result;
+};
+
+// Search arena of one resident wavefront ("slot").  Every search is transient state
+// (HybridAStar's open/closed sets, AStar's open/closed sets, the Dubins scratch), so it
+// belongs to the wave that runs the search, not to the planner: a persistent kernel with
+// W slots serves any number of planners, and the planners keep only their maps.
+struct SlotArena {
+  Node3* open3;     int open3_cap;   int pad0;
+  Closed3* closed3; int closed3_cap; int pad1;
+  Slot3* slots3;    uint32_t slots3_mask; int pad2;
+  Node2* open2;     int open2_cap;   int pad3;
+  Closed2* closed2; int closed2_cap; int pad4;
+  uint32_t* cgen2;  // N*N generation stamps (cell -> closed record of the current A* search)
+  int* cidx2;
+  size_t cells;     // capacity of cgen2/cidx2 (max N*N served)
+  uint32_t* gens;   // [0] closed-set generation, [1] A* closed generation
+  float* dub_xyh; float* dub_curv; int dub_cap; int pad5;
+  int* out_chain;   int chain_cap;   int pad6;
 };
 
 }  // namespace hastar

@@ -18,8 +18,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batches", type=int, nargs="+", default=[64, 256, 1024])
 ap.add_argument("--grid", type=int, default=1024)
 ap.add_argument("--obstacles", type=int, default=200)
-ap.add_argument("--max-pops", type=int, default=65536)
-ap.add_argument("--max-astar-nodes", type=int, default=262144)
+ap.add_argument("--max-pops", type=int, default=131072)
+ap.add_argument("--max-astar-nodes", type=int, default=0)
 args = ap.parse_args()
 Bmax = max(args.batches)
 t = time.time()
