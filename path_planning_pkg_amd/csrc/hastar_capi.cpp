@@ -123,7 +123,18 @@ struct DeviceCtx {
   PlannerDev* d_descs = nullptr;
   int* d_order = nullptr;
   int* d_next = nullptr;
+  SearchResult* d_results = nullptr;
+  SearchResult* h_results = nullptr;   // pinned
+  long long* d_off = nullptr;          // path point offsets of the packed hand-back
+  int* d_len = nullptr;
+  long long* h_offlen = nullptr;       // pinned: n offsets then n lengths (as int)
   int batch_cap = 0;
+  // packed paths of a batch (device staging + pinned host copy)
+  float* d_pxyh = nullptr;
+  float* d_pcurv = nullptr;
+  float* h_pxyh = nullptr;
+  float* h_pcurv = nullptr;
+  size_t pts_cap = 0;
 };
 DeviceCtx g_dev[64];
 
@@ -393,8 +404,7 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   const size_t b_occ = align256(NN * sizeof(float)), b_nm = align256(NN * sizeof(float)), b_vis = align256(NN);
   const size_t b_off = align256(off.size() * sizeof(float)), b_s = align256((size_t)ns * sizeof(float));
   const size_t b_ox = align256((size_t)D.out_cap * 3 * sizeof(float)), b_oc = align256((size_t)D.out_cap * sizeof(float));
-  const size_t b_res = align256(sizeof(SearchResult));
-  const size_t total = b_occ + b_nm + b_vis + b_off + 3 * b_s + b_ox + b_oc + b_res;
+  const size_t total = b_occ + b_nm + b_vis + b_off + 3 * b_s + b_ox + b_oc;
   if (hipMalloc(&h->slab, total) != hipSuccess) {
     h->slab = nullptr;
     free_handle(h);
@@ -410,7 +420,7 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   D.curv_abs = reinterpret_cast<float*>(q); q += b_s;
   D.out_xyh = reinterpret_cast<float*>(q); q += b_ox;
   D.out_curv = reinterpret_cast<float*>(q); q += b_oc;
-  D.result = reinterpret_cast<SearchResult*>(q); q += b_res;
+  D.result = nullptr;  // set per batch to the device context's result array
   D.apf = nullptr;
   D.n_apf = 0;
   hipStream_t st = dc->stream;
@@ -718,19 +728,35 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     HIPCHK(hipStreamSynchronize(st));
     if (DC.d_descs) hipFree(DC.d_descs);
     if (DC.d_order) hipFree(DC.d_order);
+    if (DC.d_results) hipFree(DC.d_results);
+    if (DC.d_off) hipFree(DC.d_off);
+    if (DC.d_len) hipFree(DC.d_len);
+    if (DC.h_results) hipHostFree(DC.h_results);
+    if (DC.h_offlen) hipHostFree(DC.h_offlen);
     DC.d_descs = nullptr;
     DC.d_order = nullptr;
+    DC.d_results = nullptr;
+    DC.d_off = nullptr;
+    DC.d_len = nullptr;
+    DC.h_results = nullptr;
+    DC.h_offlen = nullptr;
     DC.batch_cap = 0;
     HIPCHK(dalloc(&DC.d_descs, (size_t)n));
     HIPCHK(dalloc(&DC.d_order, (size_t)n));
+    HIPCHK(dalloc(&DC.d_results, (size_t)n));
+    HIPCHK(dalloc(&DC.d_off, (size_t)n));
+    HIPCHK(dalloc(&DC.d_len, (size_t)n));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_results), (size_t)n * sizeof(SearchResult)));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_offlen), (size_t)n * 2 * sizeof(long long)));
     DC.batch_cap = n;
   }
   std::vector<PlannerDev> descs(n);
   for (int i = 0; i < n; ++i) {
     prepare_start(hs[i], vel[i], starts + 3 * i);
     descs[i] = hs[i]->desc;
+    descs[i].result = DC.d_results + i;
   }
-  // longest-expected-first: planners ordered by the pops of their previous search
+  // longest-expected-first: planners ordered by the work of their previous search
   std::vector<int> order(n);
   std::iota(order.begin(), order.end(), 0);
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return hs[a]->last_pops > hs[b]->last_pops; });
@@ -739,31 +765,67 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   HIPCHK(hipEventRecord(DC.ev0, st));
   HIPCHK(launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, DC.d_next, max_pops, st));
   HIPCHK(hipEventRecord(DC.ev1, st));
-  std::vector<SearchResult> res(n);
-  for (int i = 0; i < n; ++i)
-    HIPCHK(hipMemcpyAsync(&res[i], hs[i]->desc.result, sizeof(SearchResult), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(DC.h_results, DC.d_results, (size_t)n * sizeof(SearchResult), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   float ms = 0.0f;
   hipEventElapsedTime(&ms, DC.ev0, DC.ev1);
   g_last_ms = ms;
   int rc = HASTAR_OK;
+  // pack the paths that fit the caller's buffers: offsets, one gather kernel, one copy
+  long long* h_off = DC.h_offlen;
+  int* h_len = reinterpret_cast<int*>(DC.h_offlen + n);
+  long long total = 0;
   for (int i = 0; i < n; ++i) {
-    hs[i]->last = res[i];
-    hs[i]->have_last = true;
-    hs[i]->last_pops = res[i].pops + res[i].astar_pops;
-    ok[i] = res[i].ok;
-    cost[i] = res[i].ok ? res[i].cost : FLT_MAX;
-    fill_stats(res[i], stats ? &stats[i] : nullptr);
-    if (res[i].status != 0 && rc == HASTAR_OK) {
-      rc = res[i].status == -75 ? HASTAR_EOVERFLOW : HASTAR_ENOSPC;
-      g_err = res[i].status == -75 ? "search arena overflow (raise max_pops / max_astar_nodes)"
-                                   : "path longer than the planner's output buffer";
+    const SearchResult& R = DC.h_results[i];
+    hastar_handle h = hs[i];
+    h->last = R;
+    h->have_last = true;
+    h->last_pops = (long long)R.pops + R.astar_pops;
+    ok[i] = R.ok;
+    cost[i] = R.ok ? R.cost : FLT_MAX;
+    fill_stats(R, stats ? &stats[i] : nullptr);
+    len[i] = R.path_len;
+    if (R.status != 0 && rc == HASTAR_OK) {
+      rc = R.status == -75 ? HASTAR_EOVERFLOW : HASTAR_ENOSPC;
+      g_err = R.status == -75 ? "search arena overflow (raise max_pops / max_astar_nodes)"
+                              : "path longer than the planner's output buffer";
     }
-    int r = copy_path_out(hs[i], xyh ? xyh + (size_t)i * cap * 3 : nullptr, curv ? curv + (size_t)i * cap : nullptr,
-                          cap, &len[i], st);
-    if (r != 0 && rc == HASTAR_OK) rc = r;
+    int take = R.path_len;
+    if (take > cap) {
+      take = 0;  // the caller fetches it with hastar_copy_path
+      if (rc == HASTAR_OK) rc = fail(HASTAR_ENOSPC, "path buffer too small");
+    }
+    h_off[i] = total;
+    h_len[i] = take;
+    total += take;
   }
-  HIPCHK(hipStreamSynchronize(st));
+  if (total > 0) {
+    if ((size_t)total > DC.pts_cap) {
+      if (DC.d_pxyh) hipFree(DC.d_pxyh);
+      if (DC.d_pcurv) hipFree(DC.d_pcurv);
+      if (DC.h_pxyh) hipHostFree(DC.h_pxyh);
+      if (DC.h_pcurv) hipHostFree(DC.h_pcurv);
+      DC.d_pxyh = DC.d_pcurv = DC.h_pxyh = DC.h_pcurv = nullptr;
+      DC.pts_cap = 0;
+      const size_t c2 = (size_t)total + (size_t)total / 2 + 1024;
+      HIPCHK(dalloc(&DC.d_pxyh, c2 * 3));
+      HIPCHK(dalloc(&DC.d_pcurv, c2));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_pxyh), c2 * 3 * sizeof(float)));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_pcurv), c2 * sizeof(float)));
+      DC.pts_cap = c2;
+    }
+    HIPCHK(hipMemcpyAsync(DC.d_off, h_off, (size_t)n * sizeof(long long), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(DC.d_len, h_len, (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(launch_gather_paths(DC.d_descs, DC.d_off, DC.d_len, n, DC.d_pxyh, DC.d_pcurv, st));
+    HIPCHK(hipMemcpyAsync(DC.h_pxyh, DC.d_pxyh, (size_t)total * 3 * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(DC.h_pcurv, DC.d_pcurv, (size_t)total * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (int i = 0; i < n; ++i) {
+      if (h_len[i] == 0) continue;
+      std::memcpy(xyh + (size_t)i * cap * 3, DC.h_pxyh + 3 * h_off[i], (size_t)h_len[i] * 3 * sizeof(float));
+      std::memcpy(curv + (size_t)i * cap, DC.h_pcurv + h_off[i], (size_t)h_len[i] * sizeof(float));
+    }
+  }
   return rc;
 }
 

@@ -67,7 +67,6 @@ __device__ __forceinline__ uint32_t slot_hash(uint32_t k) {
 // unordered_set<Node3D>::insert(*it).first (HybridAStar.cpp:110): existing record or a new
 // copy of the popped open node.
 __device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n) {
-  const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   uint32_t h = slot_hash(n.key) & A.slots3_mask;
   for (;;) {
@@ -96,7 +95,6 @@ __device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n) {
 }
 
 __device__ __forceinline__ bool closed3_contains(const SearchCtx& c, uint32_t key) {
-  const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   uint32_t h = slot_hash(key) & A.slots3_mask;
   for (;;) {
@@ -147,7 +145,6 @@ __device__ __forceinline__ void lds_closed_put(AStarLds& L, uint32_t cell, int i
 template <bool G, class CP>
 __device__ __forceinline__ void memoise(SearchCtx& c, CP cl, float total, int from) {
   const PlannerDev& P = *c.P;
-  const SlotArena& A = *c.A;
   for (int i = from; i != NIL; i = cl[i].prev) {
     const Closed2 r = gload(&cl[i]);
     const size_t cell = (size_t)(r.key >> 16) * P.N + (r.key & 0xffffu);
@@ -641,6 +638,20 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
 
 // ------------------------------------------------------------------ map kernels -------
 // Grid2D ctor + compute_heuristic (Grid2D.cpp:7-62, 303-316): _node_map f = h.
+// Batched result hand-back: planner i's path (len_i points, when it fits the caller's
+// buffer) is packed at point offset off[i] of one staging buffer, so a batch returns
+// with a single device-to-host copy.
+__global__ __launch_bounds__(256) void k_gather_paths(const PlannerDev* __restrict__ descs,
+    const long long* __restrict__ off, const int* __restrict__ len, float* __restrict__ xyh, float* __restrict__ curv) {
+  const int i = blockIdx.x;
+  const int n = len[i];
+  const long long o = off[i];
+  const GAS float* sx = gp(descs[i].out_xyh);
+  const GAS float* sc = gp(descs[i].out_curv);
+  for (int t = threadIdx.x; t < 3 * n; t += blockDim.x) xyh[3 * o + t] = sx[t];
+  for (int t = threadIdx.x; t < n; t += blockDim.x) curv[o + t] = sc[t];
+}
+
 __global__ void k_init_nodemap(PlannerDev P) {
   const size_t NN = (size_t)P.N * P.N;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x) {
@@ -837,6 +848,12 @@ int search_slots_per_cu() {
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, hastar_search_kernel, 64, 0) != hipSuccess) return 1;
   return nb > 0 ? nb : 1;
+}
+hipError_t launch_gather_paths(const PlannerDev* d_descs, const long long* d_off, const int* d_len, int n, float* xyh,
+                               float* curv, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_paths, dim3(n), dim3(256), 0, st, d_descs, d_off, d_len, xyh, curv);
+  return hipGetLastError();
 }
 hipError_t launch_init_nodemap(const PlannerDev& P, hipStream_t st) {
   hipLaunchKernelGGL(k_init_nodemap, dim3(1024), dim3(256), 0, st, P);
