@@ -33,6 +33,24 @@ def algorithmic_bytes(st, K):
     return 40 * st["pops"] + 44 * st["successors"] + 208 * st["astar_pops"] + 12 * K
 
 
+def shard_query_ids(rank, world, batch):
+    """Queries of one rank: weak scaling, B per GPU, disjoint across ranks, no exchange."""
+    assert 0 <= rank < world
+    return [rank * batch + i for i in range(batch)]
+
+
+def reduce_over_ranks(dist, elapsed, pops, device):
+    """(max elapsed, total pops) over ranks; identity without a process group."""
+    if dist is None:
+        return elapsed, float(pops)
+    import torch
+    t = torch.tensor([elapsed, float(pops)], dtype=torch.float64, device=device)
+    tmax, tsum = t[:1].clone(), t[1:].clone()
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+    return float(tmax[0]), float(tsum[0])
+
+
 def build_planners(gpu, cfgs, device):
     from tests.scenarios import drive
     planners = []
@@ -83,7 +101,7 @@ def main():
         cfg.values["max_astar_nodes"] = args.max_astar_nodes
         return cfg, proto
 
-    qids = [rank * B + i for i in range(B)]
+    qids = shard_query_ids(rank, world, B)
     cfgs = [cfg_for(q) for q in qids]
     t_setup = time.perf_counter()
     planners = build_planners(gpu, cfgs, device)
@@ -119,14 +137,7 @@ def main():
         last = res
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed, float(pops), float(sum(kernel_ms))], dtype=torch.float64, device=f"cuda:{device}")
-        tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
-        elapsed, pops_all = float(tmax[0]), float(t[1])
-    else:
-        pops_all = float(pops)
+    elapsed, pops_all = reduce_over_ranks(dist, elapsed, pops, f"cuda:{device}")
 
     out = None
     if rank == 0:
