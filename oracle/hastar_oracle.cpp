@@ -40,6 +40,9 @@
 #include "../include/hastar.h"
 
 namespace orc {
+#ifdef ORC_SHAPE_STATS
+long long g_shape[8];
+#endif
 
 template <class T> struct P2 { T x, y; };
 template <class T> struct P3 { T x, y, h; };
@@ -484,6 +487,32 @@ template <class T> struct Planner {
   }
   void reset() { std::fill(visited.begin(), visited.end(), 0); }
 
+#ifdef ORC_SHAPE_STATS
+  // Analysis build only (tools/astar_shape_stats.py): how often the open tree's shape can
+  // matter for find/insert (a node of the same cell on the "wrong" side of the probe f).
+  template <class S> void shape_probe(const S& op, int i, int j, T fprobe, T fn) {
+    bool same = false, unsafe_find = false, unsafe_ins = false;
+    T prev = -std::numeric_limits<T>::infinity();
+    for (const auto& n : op) {
+      if (!(n.f > prev)) g_shape[7]++;  // strict f order violated
+      prev = n.f;
+      if (n.x == i && n.y == j) {
+        same = true;
+        if (n.f < fprobe) unsafe_find = true;
+        if (n.f > fn) unsafe_ins = true;
+      }
+    }
+    g_shape[0]++;
+    g_shape[1] += same;
+    g_shape[2] += unsafe_find;
+    g_shape[3] += unsafe_ins;
+  }
+  void shape_size(size_t n) {
+    if ((long long)n > g_shape[4]) g_shape[4] = (long long)n;
+    g_shape[5] += n > 256;
+    g_shape[6] += n > 1024;
+  }
+#endif
   // ----------------------------------------------------- holonomic heuristic (AStar)
   // AStar::update_visted + Grid2D::update_costs (AStar.cpp:209-218, Grid2D.cpp:219-227)
   void memoise(T total, const N2<T>* last) {
@@ -499,6 +528,9 @@ template <class T> struct Planner {
     op2.clear();
     op2.insert(N2<T>{si, sj, 0, nm_f[(size_t)si * N + sj], nullptr});
     while (!op2.empty()) {
+#ifdef ORC_SHAPE_STATS
+      shape_size(op2.size());
+#endif
       auto it = op2.begin();
       const N2<T>* cur = &*cl2.insert(*it).first;
       op2.erase(it);
@@ -520,6 +552,9 @@ template <class T> struct Planner {
         }
         N2<T> probe{i, j, 0, nm_f[c], nullptr};
         if (cl2.find(probe) != cl2.end()) continue;
+#ifdef ORC_SHAPE_STATS
+        shape_probe(op2, i, j, nm_f[c], g0 + act_cost[k] + nm_h[c]);
+#endif
         auto hit = op2.find(probe);
         const T gn = g0 + act_cost[k];
         if (hit == op2.end()) {
@@ -915,3 +950,9 @@ extern "C" void orc_libm(int fn, const float* a, const float* b, float* out, int
     out[i] = v;
   }
 }
+
+#ifdef ORC_SHAPE_STATS
+extern "C" void orc_shape_stats(long long* out) {
+  for (int q = 0; q < 8; ++q) out[q] = orc::g_shape[q], orc::g_shape[q] = 0;
+}
+#endif

@@ -192,7 +192,9 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
   const size_t b_closed2 = align256((size_t)r.closed2 * sizeof(Closed2)), b_cgen = align256(r.cells * sizeof(uint32_t));
   const size_t b_cidx = align256(r.cells * sizeof(int)), b_gens = 256, b_dub = align256((size_t)r.dub * 3 * sizeof(float));
   const size_t b_dubc = align256((size_t)r.dub * sizeof(float)), b_chain = align256((size_t)r.chain * sizeof(int));
-  const size_t per = b_open3 + b_closed3 + b_slots + b_open2 + b_closed2 + b_cgen + b_cidx + b_gens + b_dub + b_dubc + b_chain;
+  const size_t b_prevl = align256((size_t)ASTAR_LDS_CAP * sizeof(int));
+  const size_t per =
+      b_open3 + b_closed3 + b_slots + b_open2 + b_closed2 + b_cgen + b_cidx + b_gens + b_dub + b_dubc + b_chain + b_prevl;
   // memory budget of the pool: HASTAR_ARENA_MB, else 80% of the free HBM
   size_t budget = 0;
   if (const char* e = std::getenv("HASTAR_ARENA_MB")) budget = (size_t)std::strtoull(e, nullptr, 10) << 20;
@@ -225,6 +227,7 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
     A.dub_xyh = reinterpret_cast<float*>(q); q += b_dub;
     A.dub_curv = reinterpret_cast<float*>(q); q += b_dubc;
     A.out_chain = reinterpret_cast<int*>(q); q += b_chain;
+    A.prevl = reinterpret_cast<int*>(q); q += b_prevl;
     A.open3_cap = r.open3;
     A.closed3_cap = r.closed3;
     A.slots3_mask = r.slots - 1;
@@ -955,7 +958,7 @@ int hastar_debug_motion(hastar_handle h, float* off, float* dth, float* cost, fl
 
 int hastar_debug_cycles(hastar_handle h, unsigned long long* out8) {
   if (!h || !h->have_last) return fail(HASTAR_EINVAL, "no search result");
-  for (int q = 0; q < 8; ++q) out8[q] = h->last.cycles[q];
+  for (int q = 0; q < 16; ++q) out8[q] = h->last.cycles[q];
   return HASTAR_OK;
 }
 

@@ -21,6 +21,16 @@ template <class T>
 __device__ __forceinline__ GAS T* gp(T* p) {
   return (GAS T*)p;
 }
+
+// Cross-lane hand-off through LDS/HBM inside ONE wavefront: the wave's memory operations
+// stay in order in hardware (LLVM AMDGPU memory model: wavefront scope needs no cache or
+// counter action), so this is only a compiler barrier — unlike __syncthreads, which also
+// drains every outstanding global load and store (s_waitcnt vmcnt(0)).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 // whole-record copies to/from HBM in 16-byte pieces (records are 16-byte aligned)
 typedef int v4i __attribute__((ext_vector_type(4)));
 template <class T>

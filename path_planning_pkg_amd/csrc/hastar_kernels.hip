@@ -50,7 +50,7 @@ struct SearchCtx {
   long long pops, succ, apops, asearch, shots, amigr, apops_g;
   int status;
 #ifdef HASTAR_STAMPS
-  unsigned long long cyc[8];
+  unsigned long long cyc[16];
 #endif
 };
 
@@ -106,142 +106,188 @@ __device__ __forceinline__ bool closed3_contains(const SearchCtx& c, uint32_t ke
 }
 
 // -------------------------------------------------------- holonomic A* (AStar.cpp) -----
-// Each lazy A* search (AStar::find_path(int, int), AStar.cpp:100-113) starts with its open
-// tree, closed records and a cell -> closed-record hash in LDS (16 KiB per wavefront).
-// Most searches stop after a few dozen pops at the first memoised neighbour; a search
-// that outgrows LDS is migrated once (same pool indices, plain copies) to the HBM arena
-// and continues there.  Both modes run the same templated loop.
-constexpr int A_CAP = 256;   // LDS open-tree nodes (index 0 = header)
-constexpr int A_CCAP = 256;  // LDS closed records
-constexpr int A_HS = 512;    // LDS hash slots (power of two, load factor <= 1/2)
+// Each lazy A* search (AStar::find_path(int, int), AStar.cpp:100-113) keeps its open
+// tree in LDS as compact nodes (16-bit links, 20 B per node, A_CAP nodes per wavefront);
+// the closed records, the cell -> closed-record map and the nodes' prev links live in
+// the HBM slot arena, so every pop needs exactly one HBM round trip (the popped cell's
+// closed state, its prev link and the 8 neighbour probes, all in flight together).  A
+// search whose tree outgrows LDS is migrated once (same pool indices) to HBM nodes and
+// continues there.  Both modes run the same templated loop.
+constexpr int A_CAP = ASTAR_LDS_CAP;  // LDS open-tree nodes (index 0 = header)
 
+struct NodeA2 {
+  uint32_t key;
+  float f;
+  float g;
+  int16_t l, r;
+};
+struct NodeB2 {
+  int16_t p, color;
+};
 struct AStarLds {
-  Node2 open[A_CAP];
-  Closed2 closed[A_CCAP];
-  uint32_t hkey[A_HS];  // cell + 1, 0 = empty
-  int hidx[A_HS];
+  NodeA2 a[A_CAP];
+  NodeB2 b[A_CAP];
 };
 
-__device__ __forceinline__ uint32_t cell_hash(uint32_t cell) { return (cell * 0x9E3779B1u) >> 23; }  // 9 bits
+#define LAS __attribute__((address_space(3)))
+template <class T>
+__device__ __forceinline__ LAS T* lp(T* p) {
+  return (LAS T*)p;
+}
 
-// returns the closed index of cell or NIL (LDS mode)
-__device__ __forceinline__ int lds_closed_find(const AStarLds& L, uint32_t cell) {
-  uint32_t h = cell_hash(cell) & (A_HS - 1);
-  for (;;) {
-    const uint32_t k = L.hkey[h];
-    if (k == 0) return NIL;
-    if (k == cell + 1) return L.hidx[h];
-    h = (h + 1) & (A_HS - 1);
+// compact LDS layout for RBT<>: {key, f, g, l|r} (16 B) + {p, color} (4 B), prev in HBM
+struct LdsAcc {
+  LAS NodeA2* a;
+  LAS NodeB2* b;
+  GAS int* pv;
+  __device__ __forceinline__ int L(int x) const { return a[x].l; }
+  __device__ __forceinline__ int R(int x) const { return a[x].r; }
+  __device__ __forceinline__ int P(int x) const { return b[x].p; }
+  __device__ __forceinline__ int C(int x) const { return b[x].color; }
+  __device__ __forceinline__ void sL(int x, int v) { a[x].l = (int16_t)v; }
+  __device__ __forceinline__ void sR(int x, int v) { a[x].r = (int16_t)v; }
+  __device__ __forceinline__ void sP(int x, int v) { b[x].p = (int16_t)v; }
+  __device__ __forceinline__ void sC(int x, int v) { b[x].color = (int16_t)v; }
+  __device__ __forceinline__ uint32_t K(int x) const { return a[x].key; }
+  __device__ __forceinline__ float F(int x) const { return a[x].f; }
+  __device__ __forceinline__ float G(int x) const { return a[x].g; }
+  __device__ __forceinline__ int PV(int x) const { return pv[x]; }
+  __device__ __forceinline__ Quad quad(int x) const {
+    typedef int v4 __attribute__((ext_vector_type(4)));
+    const v4 v = *(const LAS v4*)&a[x];
+    Quad q;
+    q.key = (uint32_t)v.x;
+    q.f = __int_as_float(v.y);
+    q.l = (v.w << 16) >> 16;
+    q.r = v.w >> 16;
+    return q;
   }
-}
-__device__ __forceinline__ void lds_closed_put(AStarLds& L, uint32_t cell, int idx) {
-  uint32_t h = cell_hash(cell) & (A_HS - 1);
-  while (L.hkey[h] != 0) h = (h + 1) & (A_HS - 1);
-  L.hkey[h] = cell + 1;
-  L.hidx[h] = idx;
-}
+  __device__ __forceinline__ void leaf(int x, int p) {
+    *(LAS int*)&a[x].l = -1;  // l = r = NIL
+    *(LAS int*)&b[x] = (RB_RED << 16) | (p & 0xffff);
+  }
+  __device__ __forceinline__ void payload(int x, uint32_t key, float f, float g, int prev) {
+    a[x].key = key;
+    a[x].f = f;
+    a[x].g = g;
+    pv[x] = prev;
+  }
+};
+// HBM layout (Node2, 32-bit links, prev in the node)
+struct HbmAcc : AosAcc<Node2, GAS Node2*> {
+  __device__ __forceinline__ float G(int x) const { return t[x].g; }
+  __device__ __forceinline__ int PV(int x) const { return t[x].prev; }
+  __device__ __forceinline__ void payload(int x, uint32_t key, float f, float g, int prev) {
+    t[x].key = key;
+    t[x].f = f;
+    t[x].g = g;
+    t[x].prev = prev;
+  }
+};
 
 // AStar::update_visted + Grid2D::update_costs (AStar.cpp:209-218, Grid2D.cpp:219-227)
-template <bool G, class CP>
-__device__ __forceinline__ void memoise(SearchCtx& c, CP cl, float total, int from) {
+__device__ __forceinline__ void memoise(SearchCtx& c, float total, int from) {
   const PlannerDev& P = *c.P;
-  for (int i = from; i != NIL; i = cl[i].prev) {
+  const GAS Closed2* cl = gp(c.A->closed2);
+  for (int i = from; i != NIL;) {
     const Closed2 r = gload(&cl[i]);
     const size_t cell = (size_t)(r.key >> 16) * P.N + (r.key & 0xffffu);
     gp(P.visited)[cell] = 1;
     gp(P.nm_f)[cell] = total - r.g;
+    i = r.prev;
   }
 }
 
-template <class NP>
-__device__ __forceinline__ bool insert2(SearchCtx& c, RBTree<Node2, NP>& tr, int cap, uint32_t key, float f, float g,
-                                        int prev) {
+template <class Tree>
+__device__ __forceinline__ bool insert2(SearchCtx& c, Tree& tr, int cap, uint32_t key, float f, float g, int prev) {
   bool left;
   const int pos = tr.insert_pos(key, f, &left);
   if (pos == -2) return true;  // equal-f "duplicate": dropped like std::set::insert
-  const int n = pool_alloc(tr.t, c.ps2, cap);
+  const int n = tpool_alloc(tr, c.ps2, cap);
   if (n == NIL) return false;
-  auto d = &tr.t[n];
-  d->key = key;
-  d->f = f;
-  d->g = g;
-  d->prev = prev;
+  tr.payload(n, key, f, g, prev);
   tr.link(left, n, pos);
   return true;
 }
 
-// The body of AStar::a_star_search (AStar.cpp:118-186).  G = false: LDS mode, returns
-// false (without popping) when the next pop could overflow LDS.  Returns true when the
-// search finished; *result = cost-to-goal or FLT_MAX.
-template <bool G>
-__device__ __forceinline__ bool astar_loop(SearchCtx& c, AStarLds& L, int adx, int ady, float acost, float* result) {
+// The body of AStar::a_star_search (AStar.cpp:118-186).  G = false: LDS tree, returns
+// false (without popping) when the next pop could overflow the LDS pool.  Returns true
+// when the search finished; *result = cost-to-goal or FLT_MAX.
+template <bool G, class Tree>
+__device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int ady, float acost, float* result) {
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
-  typedef typename std::conditional<G, GAS Node2*, Node2*>::type NP;
-  typedef typename std::conditional<G, GAS Closed2*, Closed2*>::type CP;
-  RBTree<Node2, NP> tr{G ? (NP)gp(A.open2) : (NP)L.open};
-  CP cl = G ? (CP)gp(A.closed2) : (CP)L.closed;
+  GAS Closed2* cl = gp(A.closed2);
+  GAS uint32_t* cgen = gp(A.cgen2);
+  GAS int* cidx = gp(A.cidx2);
   const int cap = G ? A.open2_cap : A_CAP;
   while (!tr.empty()) {
-    if (!G && (c.ps2.next + 8 > A_CAP || c.n_closed2 + 1 > A_CCAP)) return false;
+    if (!G && c.ps2.next + 8 > A_CAP) return false;
+    STAMP_T t_pop = STAMP_NOW();
     const int b = tr.begin();
-    const Node2 top = gload(&tr.t[b]);
+    const Quad top = tr.quad(b);
+    const float top_g = tr.G(b);
     const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
     const uint32_t tcell = (uint32_t)tx * (uint32_t)P.N + (uint32_t)ty;
-    int ci = G ? ((gp(A.cgen2)[tcell] == c.gen2) ? gp(A.cidx2)[tcell] : NIL) : lds_closed_find(L, tcell);
-    if (ci == NIL) {  // new closed element (duplicates expand the old one, AStar.cpp:130)
-      if (c.n_closed2 >= (G ? A.closed2_cap : A_CCAP)) { c.status = -75; *result = FLT_MAX; return true; }
-      ci = c.n_closed2++;
-      auto r = &cl[ci];
-      r->key = top.key;
-      r->g = top.g;
-      r->f = top.f;
-      r->prev = top.prev;
-      if (G) {
-        gp(A.cgen2)[tcell] = c.gen2;
-        gp(A.cidx2)[tcell] = ci;
-      } else {
-        if (lane == 0) lds_closed_put(L, tcell, ci);
-        __syncthreads();
-      }
-    }
-    tr.unlink(b);
-    pool_free(tr.t, c.ps2, b);
-    c.apops++;
-    if (G) c.apops_g++;
-    const Closed2 cur = gload(&cl[ci]);
-    const int cx = (int)(cur.key >> 16), cy = (int)(cur.key & 0xffffu);
-    if (cx == P.goal_cx && cy == P.goal_cy) {
-      memoise<G>(c, cl, cur.f, ci);
-      *result = cur.f;
-      return true;
-    }
-    const float g0 = cur.g;
-    // neighbour probes, one lane per action (Grid2D::get_neighbors, Grid2D.cpp:72-96): bounds,
-    // occupancy, memo flag, node-map f and closed membership are loop-invariant here.
-    const int ni = cx + adx, nj = cy + ady;
+    // one HBM round trip: the popped cell's closed state and prev link, and the
+    // neighbour probes (bounds, occupancy, memo flag, node-map f, closed membership —
+    // loop-invariant during this expansion; Grid2D::get_neighbors, Grid2D.cpp:72-96)
+    const uint32_t tgen = cgen[tcell];
+    const int tcidx = cidx[tcell];
+    const int tprev = tr.PV(b);
+    const int ni = tx + adx, nj = ty + ady;
     bool valid = false, vis = false, closed = false;
     float nf = 0.0f;
     if (lane < nact && ni > -1 && ni < P.N && nj > -1 && nj < P.N) {
-      // all probe loads in flight together (one HBM round trip)
       const uint32_t cell = (uint32_t)ni * (uint32_t)P.N + (uint32_t)nj;
       const float occv = gp(P.occ)[cell];
       const uint8_t visv = gp(P.visited)[cell];
       nf = gp(P.nm_f)[cell];
-      const bool clv = G ? (gp(A.cgen2)[cell] == c.gen2) : (lds_closed_find(L, cell) != NIL);
+      const uint32_t cg = cgen[cell];
       valid = occv < P.thr;
       vis = valid && visv != 0;
-      closed = valid && clv;
+      closed = valid && cg == c.gen2;
     }
+    tr.unlink(b);
+    tpool_free(tr, c.ps2, b);
+    // unordered_set::insert(*it).first (AStar.cpp:130): a duplicate expands the OLD record
+    int ci;
+    Closed2 cur;
+    if (tgen == c.gen2) {
+      ci = tcidx;
+      cur = gload(&cl[ci]);
+    } else {
+      if (c.n_closed2 >= A.closed2_cap) { c.status = -75; *result = FLT_MAX; return true; }
+      ci = c.n_closed2++;
+      cur.key = top.key;
+      cur.g = top_g;
+      cur.f = top.f;
+      cur.prev = tprev;
+      gstore(&cl[ci], cur);
+      cgen[tcell] = c.gen2;
+      cidx[tcell] = ci;
+    }
+    c.apops++;
+    if (G) c.apops_g++;
+    const int cx = (int)(cur.key >> 16), cy = (int)(cur.key & 0xffffu);
+    if (cx == P.goal_cx && cy == P.goal_cy) {
+      memoise(c, cur.f, ci);
+      *result = cur.f;
+      return true;
+    }
+    const float g0 = cur.g;
     const uint64_t vmask = __ballot(valid), vismask = __ballot(vis), cmask = __ballot(closed);
+    if (!G) STAMP_ADD(8, t_pop);
     for (int k = 0; k < nact; ++k) {
       if (!((vmask >> k) & 1ull)) continue;
       const float kcost = shfl_f(acost, k);
       if ((vismask >> k) & 1ull) {
         const float tot = shfl_f(nf, k) + g0 + kcost;
-        memoise<G>(c, cl, tot, ci);
+        STAMP_T t_m = STAMP_NOW();
+        memoise(c, tot, ci);
+        STAMP_ADD(12, t_m);
         *result = tot;
         return true;
       }
@@ -249,21 +295,27 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, AStarLds& L, int adx, i
       const int ki = shfl_i(ni, k), kj = shfl_i(nj, k);
       const uint32_t key = ((uint32_t)ki << 16) | (uint32_t)kj;
       const float fprobe = shfl_f(nf, k);  // stale _node_map f, as the reference reads it
+      STAMP_T t_f = STAMP_NOW();
       const int hit = tr.find(key, fprobe);
+      if (!G) STAMP_ADD(9, t_f);
       const float gn = g0 + kcost;
       if (hit == 0) {
         const float fn = gn + euclid_h(P, ki, kj);
         gp(P.nm_f)[(size_t)ki * P.N + kj] = fn;  // Node2D::set_accumulated_cost
+        STAMP_T t_i = STAMP_NOW();
         if (!insert2(c, tr, cap, key, fn, gn, ci)) { c.status = -75; *result = FLT_MAX; return true; }
-      } else if (gn < tr.t[hit].g) {
+        if (!G) STAMP_ADD(10, t_i);
+      } else if (gn < tr.G(hit)) {
+        STAMP_T t_u = STAMP_NOW();
         tr.unlink(hit);
-        pool_free(tr.t, c.ps2, hit);
+        tpool_free(tr, c.ps2, hit);
+        if (!G) STAMP_ADD(11, t_u);
         const float fn = gn + euclid_h(P, ki, kj);
         gp(P.nm_f)[(size_t)ki * P.N + kj] = fn;
         if (!insert2(c, tr, cap, key, fn, gn, ci)) { c.status = -75; *result = FLT_MAX; return true; }
       }
     }
-    if (!G) __syncthreads();
+    wave_lds_sync();
   }
   *result = FLT_MAX;
   return true;
@@ -283,12 +335,13 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   c.n_closed2 = 0;
   c.ps2.next = 1;
   c.ps2.free = NIL;
-  for (int q = lane; q < A_HS; q += 64) L.hkey[q] = 0;
-  __syncthreads();
-  RBTree<Node2, Node2*> tr{L.open};
-  tr.clear();
-  insert2(c, tr, A_CAP, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL);
-  __syncthreads();
+  RBT<LdsAcc> tl;
+  tl.a = lp(L.a);
+  tl.b = lp(L.b);
+  tl.pv = gp(A.prevl);
+  tl.clear();
+  insert2(c, tl, A_CAP, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL);
+  wave_lds_sync();
   const int nact = P.diag ? 8 : 4;
   // this lane's action (Grid2D.cpp:22-40): nibble-packed (dx + 1, dy + 1) tables
   int adx = 0, ady = 0;
@@ -300,20 +353,27 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
     acost = (adx != 0 && ady != 0) ? P.act_cost_diag : P.act_cost_axis;
   }
   float result = FLT_MAX;
-  if (astar_loop<false>(c, L, adx, ady, acost, &result)) return result;
-  // migrate the LDS state to HBM (identical indices) and continue there
+  if (astar_loop<false>(c, tl, adx, ady, acost, &result)) return result;
+  // migrate the LDS tree to HBM nodes (identical indices) and continue there
   c.amigr++;
-  for (int i = lane; i < c.ps2.next; i += 64) gstore(&gp(A.open2)[i], L.open[i]);
-  for (int i = lane; i < c.n_closed2; i += 64) {
-    const Closed2 r = L.closed[i];
-    gstore(&gp(A.closed2)[i], r);
-    const size_t cell = (size_t)(r.key >> 16) * P.N + (r.key & 0xffffu);
-    gp(A.cgen2)[cell] = c.gen2;
-    gp(A.cidx2)[cell] = i;
+  GAS Node2* o2 = gp(A.open2);
+  for (int i = lane; i < c.ps2.next; i += 64) {
+    Node2 n;
+    n.key = L.a[i].key;
+    n.f = L.a[i].f;
+    n.g = L.a[i].g;
+    n.l = L.a[i].l;
+    n.r = L.a[i].r;
+    n.p = L.b[i].p;
+    n.color = L.b[i].color;
+    n.prev = gp(A.prevl)[i];
+    gstore(&o2[i], n);
   }
-  __syncthreads();
+  wave_lds_sync();
+  RBT<HbmAcc> th;
+  th.t = o2;
   STAMP_T tg = STAMP_NOW();
-  astar_loop<true>(c, L, adx, ady, acost, &result);
+  astar_loop<true>(c, th, adx, ady, acost, &result);
   STAMP_ADD(7, tg);
   return result;
 }
@@ -347,7 +407,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
   const SlotArena& A = *c.A;
   const int lane = c.lane;
 #ifdef HASTAR_STAMPS
-  for (int q = 0; q < 8; ++q) c.cyc[q] = 0;
+  for (int q = 0; q < 16; ++q) c.cyc[q] = 0;
 #endif
   c.o3.t = gp(A.open3);
   c.gen3 += 1;
@@ -416,7 +476,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
         const Centres C = dubins_centres(r, cur.x, cur.y, cur.h, P.goal_x, P.goal_y, P.goal_h);
         const int n = dubins_sample(P, C, word, prm, gp(A.dub_xyh), gp(A.dub_curv), A.dub_cap, lane);
         if (n < 0) { c.status = -75; break; }
-        __syncthreads();
+        wave_lds_sync();
         const bool first_arc_long = fabsf(prm[1]) > (float)M_PI_2;
         if (!first_arc_long && path_is_free(P, gp(A.dub_xyh), n, lane)) {
           terminal = cur.prev;
@@ -462,14 +522,14 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
       if (lane == 0) sl[ns] = s;
       ++ns;
     }
-    __syncthreads();
+    wave_lds_sync();
     c.succ += ns;
     // APF field of every kept successor (lanes over obstacles)
     for (int q = 0; q < ns; ++q) {
       const float fc = apf_field(P, sl[q].x, sl[q].y, sl[q].h, lane);
-      __syncthreads();
+      wave_lds_sync();
       if (lane == 0) sl[q].g = sl[q].g + fc;
-      __syncthreads();
+      wave_lds_sync();
     }
     // Dubins lengths: lane = 4 * successor + word
     {
@@ -489,7 +549,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
         if (lane == 0) sl[s].dub = best;
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     STAMP_ADD(1, tx);
     // ---- HybridAStar.cpp:159-193
     STAMP_T tb = STAMP_NOW();
@@ -516,7 +576,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
       }
       if (c.status != 0) break;
     }
-    __syncthreads();
+    wave_lds_sync();
     STAMP_ADD(2, tb);
     if (fail) c.status = -75;
     if (c.status != 0) break;
@@ -534,7 +594,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
       if (lane == 0) gp(A.out_chain)[L] = i;
       ++L;
     }
-    __syncthreads();
+    wave_lds_sync();
     if (c.status == 0) {
       const float cs = P.rot_c, sn = P.rot_s, ang = -P.grid_heading;
       path_len = dub_n + L;
@@ -577,7 +637,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
   uint64_t cd = 0;
   for (int i = lane; i < c.n_closed3; i += 64) cd += mix64(digest_key(gp(A.closed3)[i].key));
   cd = wave_sum_u64(cd);
-  __syncthreads();
+  wave_lds_sync();
   STAMP_ADD(5, trc);
   if (lane == 0) {
     auto R = gp(P.result);
@@ -599,12 +659,12 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
     R->astar_migrations = c.amigr;
     R->astar_pops_hbm = c.apops_g;
 #ifdef HASTAR_STAMPS
-    for (int q = 0; q < 8; ++q) R->cycles[q] = c.cyc[q];
+    for (int q = 0; q < 16; ++q) R->cycles[q] = c.cyc[q];
 #else
-    for (int q = 0; q < 8; ++q) R->cycles[q] = 0;
+    for (int q = 0; q < 16; ++q) R->cycles[q] = 0;
 #endif
   }
-  __syncthreads();
+  wave_lds_sync();
 }
 
 // Persistent work-queue kernel: grid = W resident slots (one wavefront each).  Each slot

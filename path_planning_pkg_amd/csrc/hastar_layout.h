@@ -77,7 +77,7 @@ struct SearchResult {
   int terminal;           // closed record index the path is rebuilt from
   int dubins_len;         // samples of the successful shot
   int astar_migrations;   // inner A* searches that outgrew LDS
-  unsigned long long cycles[8];  // diagnostic build (-DHASTAR_STAMPS): s_memtime per phase
+  unsigned long long cycles[16]; // diagnostic build (-DHASTAR_STAMPS): s_memtime per phase
 };
 
 // Descriptor of one planner: constants + device pointers.  Lives in HBM; the kernel
@@ -115,6 +115,9 @@ struct PlannerDev {
   SearchResult* result;
 };
 
+// Open-tree capacity of an inner A* search while it stays in LDS (kernel and host agree).
+constexpr int ASTAR_LDS_CAP = 1024;
+
 // Search arena of one resident wavefront ("slot").  Every search is transient state
 // (HybridAStar's open/closed sets, AStar's open/closed sets, the Dubins scratch), so it
 // belongs to the wave that runs the search, not to the planner: a persistent kernel with
@@ -131,6 +134,7 @@ struct SlotArena {
   uint32_t* gens;   // [0] closed-set generation, [1] A* closed generation
   float* dub_xyh; float* dub_curv; int dub_cap; int pad5;
   int* out_chain;   int chain_cap;   int pad6;
+  int* prevl;       // prev links of the LDS-resident A* tree nodes (A_CAP)
 };
 
 }  // namespace hastar

@@ -55,56 +55,94 @@ inline Quad rb_quad(PtrT t, int x) {
 }
 #endif
 
+// Field access of a tree layout.  The algorithms below (RBT) only use these members,
+// so the same libstdc++ restatement runs on the array-of-structs HBM nodes (Node3,
+// Node2; 32-bit links) and on the compact LDS nodes of the inner A* (16-bit links).
 template <class NodeT, class PtrT = NodeT*>
-struct RBTree {
+struct AosAcc {
   PtrT t;
+  RB_HD int L(int x) const { return t[x].l; }
+  RB_HD int R(int x) const { return t[x].r; }
+  RB_HD int P(int x) const { return t[x].p; }
+  RB_HD int C(int x) const { return t[x].color; }
+  RB_HD void sL(int x, int v) { t[x].l = v; }
+  RB_HD void sR(int x, int v) { t[x].r = v; }
+  RB_HD void sP(int x, int v) { t[x].p = v; }
+  RB_HD void sC(int x, int v) { t[x].color = v; }
+  RB_HD uint32_t K(int x) const { return t[x].key; }
+  RB_HD float F(int x) const { return t[x].f; }
+  RB_HD Quad quad(int x) const { return rb_quad(t, x); }
+  RB_HD void leaf(int x, int p) {  // new node: parent p, no children, red
+    t[x].p = p;
+    t[x].l = NIL;
+    t[x].r = NIL;
+    t[x].color = RB_RED;
+  }
+};
 
-  RB_HD int root() const { return t[0].p; }
-  RB_HD int begin() const { return t[0].l; }          // == 0 (header) when empty
-  RB_HD bool empty() const { return t[0].p == NIL; }
+template <class Acc>
+struct RBT : Acc {
+  using Acc::L;
+  using Acc::R;
+  using Acc::P;
+  using Acc::C;
+  using Acc::sL;
+  using Acc::sR;
+  using Acc::sP;
+  using Acc::sC;
+  using Acc::K;
+  using Acc::F;
+
+  RB_HD int root() const { return P(0); }
+  RB_HD int begin() const { return L(0); }          // == 0 (header) when empty
+  RB_HD bool empty() const { return P(0) == NIL; }
 
   RB_HD void clear() {
-    t[0].p = NIL;
-    t[0].l = 0;
-    t[0].r = 0;
-    t[0].color = RB_RED;
+    sP(0, NIL);
+    sL(0, 0);
+    sR(0, 0);
+    sC(0, RB_RED);
   }
 
   RB_HD void rotate_left(int x) {
-    const int y = t[x].r;
-    t[x].r = t[y].l;
-    if (t[y].l != NIL) t[t[y].l].p = x;
-    t[y].p = t[x].p;
-    if (x == t[0].p) t[0].p = y;
-    else if (x == t[t[x].p].l) t[t[x].p].l = y;
-    else t[t[x].p].r = y;
-    t[y].l = x;
-    t[x].p = y;
+    const int y = R(x);
+    const int yl = L(y);
+    sR(x, yl);
+    if (yl != NIL) sP(yl, x);
+    const int xp = P(x);
+    sP(y, xp);
+    if (x == P(0)) sP(0, y);
+    else if (x == L(xp)) sL(xp, y);
+    else sR(xp, y);
+    sL(y, x);
+    sP(x, y);
   }
 
   RB_HD void rotate_right(int x) {
-    const int y = t[x].l;
-    t[x].l = t[y].r;
-    if (t[y].r != NIL) t[t[y].r].p = x;
-    t[y].p = t[x].p;
-    if (x == t[0].p) t[0].p = y;
-    else if (x == t[t[x].p].r) t[t[x].p].r = y;
-    else t[t[x].p].l = y;
-    t[y].r = x;
-    t[x].p = y;
+    const int y = L(x);
+    const int yr = R(y);
+    sL(x, yr);
+    if (yr != NIL) sP(yr, x);
+    const int xp = P(x);
+    sP(y, xp);
+    if (x == P(0)) sP(0, y);
+    else if (x == R(xp)) sR(xp, y);
+    else sL(xp, y);
+    sR(y, x);
+    sP(x, y);
   }
 
   RB_HD int decrement(int x) const {
-    if (t[x].color == RB_RED && t[x].p != NIL && t[t[x].p].p == x) return t[x].r;  // header
-    if (t[x].l != NIL) {
-      int y = t[x].l;
-      while (t[y].r != NIL) y = t[y].r;
+    if (C(x) == RB_RED && P(x) != NIL && P(P(x)) == x) return R(x);  // header
+    if (L(x) != NIL) {
+      int y = L(x);
+      while (R(y) != NIL) y = R(y);
       return y;
     }
-    int y = t[x].p;
-    while (x == t[y].l) {
+    int y = P(x);
+    while (x == L(y)) {
       x = y;
-      y = t[y].p;
+      y = P(y);
     }
     return y;
   }
@@ -112,11 +150,11 @@ struct RBTree {
   // std::set::find (stl_tree.h _M_lower_bound + key_compare check).  Returns 0 (= end)
   // when not "found".
   RB_HD int find(uint32_t k, float f) const {
-    int y = 0, x = t[0].p;
+    int y = 0, x = P(0);
     uint32_t yk = 0;
     float yf = 0.0f;
     while (x != NIL) {
-      const Quad q = rb_quad(t, x);
+      const Quad q = this->quad(x);
       if (!rb_less(q.key, q.f, k, f)) {
         y = x;
         yk = q.key;
@@ -133,24 +171,28 @@ struct RBTree {
   // _M_get_insert_unique_pos: returns the parent for the new node (>= 0) or -2 when an
   // "equivalent" element exists (insert dropped).  *left = insert_left of _M_insert_.
   RB_HD int insert_pos(uint32_t k, float f, bool* left) const {
-    int x = t[0].p, y = 0;
+    int x = P(0), y = 0;
     bool comp = true;
+    uint32_t yk = 0;
+    float yf = 0.0f;
     while (x != NIL) {
-      const Quad q = rb_quad(t, x);
+      const Quad q = this->quad(x);
       y = x;
+      yk = q.key;
+      yf = q.f;
       comp = rb_less(k, f, q.key, q.f);
       x = comp ? q.l : q.r;
     }
     int j = y;
     if (comp) {
-      if (j == t[0].l) {
+      if (j == L(0)) {
         *left = true;  // _M_insert_: x != 0 is false; p == end() or comp(v, p) holds
         return y;
       }
       j = decrement(j);
     }
-    if (rb_less(t[j].key, t[j].f, k, f)) {
-      *left = (y == 0) || rb_less(k, f, t[y].key, t[y].f);
+    if (rb_less(K(j), F(j), k, f)) {
+      *left = (y == 0) || rb_less(k, f, yk, yf);
       return y;
     }
     return -2;
@@ -158,176 +200,200 @@ struct RBTree {
 
   // _Rb_tree_insert_and_rebalance(insert_left, x, p, header)
   RB_HD void link(bool insert_left, int x, int p) {
-    t[x].p = p;
-    t[x].l = NIL;
-    t[x].r = NIL;
-    t[x].color = RB_RED;
+    this->leaf(x, p);
     if (insert_left) {
-      t[p].l = x;
+      sL(p, x);
       if (p == 0) {
-        t[0].p = x;
-        t[0].r = x;
-      } else if (p == t[0].l) {
-        t[0].l = x;
+        sP(0, x);
+        sR(0, x);
+      } else if (p == L(0)) {
+        sL(0, x);
       }
     } else {
-      t[p].r = x;
-      if (p == t[0].r) t[0].r = x;
+      sR(p, x);
+      if (p == R(0)) sR(0, x);
     }
-    while (x != t[0].p && t[t[x].p].color == RB_RED) {
-      const int xp = t[x].p;
-      const int xpp = t[xp].p;
-      if (xp == t[xpp].l) {
-        const int y = t[xpp].r;
-        if (y != NIL && t[y].color == RB_RED) {
-          t[xp].color = RB_BLACK;
-          t[y].color = RB_BLACK;
-          t[xpp].color = RB_RED;
+    int rootv = P(0);
+    while (x != rootv) {
+      const int xp = P(x);
+      if (C(xp) != RB_RED) break;
+      const int xpp = P(xp);
+      if (xp == L(xpp)) {
+        const int y = R(xpp);
+        if (y != NIL && C(y) == RB_RED) {
+          sC(xp, RB_BLACK);
+          sC(y, RB_BLACK);
+          sC(xpp, RB_RED);
           x = xpp;
         } else {
-          if (x == t[xp].r) {
+          if (x == R(xp)) {
             x = xp;
             rotate_left(x);
           }
-          t[t[x].p].color = RB_BLACK;
-          t[xpp].color = RB_RED;
+          sC(P(x), RB_BLACK);
+          sC(xpp, RB_RED);
           rotate_right(xpp);
+          rootv = P(0);
         }
       } else {
-        const int y = t[xpp].l;
-        if (y != NIL && t[y].color == RB_RED) {
-          t[xp].color = RB_BLACK;
-          t[y].color = RB_BLACK;
-          t[xpp].color = RB_RED;
+        const int y = L(xpp);
+        if (y != NIL && C(y) == RB_RED) {
+          sC(xp, RB_BLACK);
+          sC(y, RB_BLACK);
+          sC(xpp, RB_RED);
           x = xpp;
         } else {
-          if (x == t[xp].l) {
+          if (x == L(xp)) {
             x = xp;
             rotate_right(x);
           }
-          t[t[x].p].color = RB_BLACK;
-          t[xpp].color = RB_RED;
+          sC(P(x), RB_BLACK);
+          sC(xpp, RB_RED);
           rotate_left(xpp);
+          rootv = P(0);
         }
       }
     }
-    t[t[0].p].color = RB_BLACK;
+    sC(P(0), RB_BLACK);
   }
 
   RB_HD int minimum(int x) const {
-    while (t[x].l != NIL) x = t[x].l;
+    while (L(x) != NIL) x = L(x);
     return x;
   }
   RB_HD int maximum(int x) const {
-    while (t[x].r != NIL) x = t[x].r;
+    while (R(x) != NIL) x = R(x);
     return x;
   }
 
   // _Rb_tree_rebalance_for_erase(z, header); the caller frees z afterwards.
   RB_HD void unlink(int z) {
     int y = z, x = NIL, xp = NIL;
-    if (t[y].l == NIL) {
-      x = t[y].r;
-    } else if (t[y].r == NIL) {
-      x = t[y].l;
+    const int zl = L(z), zr = R(z), zp = P(z);
+    if (zl == NIL) {
+      x = zr;
+    } else if (zr == NIL) {
+      x = zl;
     } else {
-      y = t[y].r;
-      while (t[y].l != NIL) y = t[y].l;
-      x = t[y].r;
+      y = zr;
+      while (L(y) != NIL) y = L(y);
+      x = R(y);
     }
     if (y != z) {
-      t[t[z].l].p = y;
-      t[y].l = t[z].l;
-      if (y != t[z].r) {
-        xp = t[y].p;
-        if (x != NIL) t[x].p = t[y].p;
-        t[t[y].p].l = x;
-        t[y].r = t[z].r;
-        t[t[z].r].p = y;
+      sP(zl, y);
+      sL(y, zl);
+      if (y != zr) {
+        xp = P(y);
+        if (x != NIL) sP(x, xp);
+        sL(xp, x);
+        sR(y, zr);
+        sP(zr, y);
       } else {
         xp = y;
       }
-      if (t[0].p == z) t[0].p = y;
-      else if (t[t[z].p].l == z) t[t[z].p].l = y;
-      else t[t[z].p].r = y;
-      t[y].p = t[z].p;
-      const int c = t[y].color;
-      t[y].color = t[z].color;
-      t[z].color = c;
+      if (P(0) == z) sP(0, y);
+      else if (L(zp) == z) sL(zp, y);
+      else sR(zp, y);
+      sP(y, zp);
+      const int cy = C(y);
+      sC(y, C(z));
+      sC(z, cy);
       y = z;
     } else {
-      xp = t[y].p;
-      if (x != NIL) t[x].p = t[y].p;
-      if (t[0].p == z) t[0].p = x;
-      else if (t[t[z].p].l == z) t[t[z].p].l = x;
-      else t[t[z].p].r = x;
-      if (t[0].l == z) t[0].l = (t[z].r == NIL) ? t[z].p : minimum(x);
-      if (t[0].r == z) t[0].r = (t[z].l == NIL) ? t[z].p : maximum(x);
+      xp = zp;
+      if (x != NIL) sP(x, zp);
+      if (P(0) == z) sP(0, x);
+      else if (L(zp) == z) sL(zp, x);
+      else sR(zp, x);
+      if (L(0) == z) sL(0, (zr == NIL) ? zp : minimum(x));
+      if (R(0) == z) sR(0, (zl == NIL) ? zp : maximum(x));
     }
-    if (t[y].color != RB_RED) {
-      while (x != t[0].p && (x == NIL || t[x].color == RB_BLACK)) {
-        if (x == t[xp].l) {
-          int w = t[xp].r;
-          if (t[w].color == RB_RED) {
-            t[w].color = RB_BLACK;
-            t[xp].color = RB_RED;
+    if (C(y) != RB_RED) {
+      while (x != P(0) && (x == NIL || C(x) == RB_BLACK)) {
+        if (x == L(xp)) {
+          int w = R(xp);
+          if (C(w) == RB_RED) {
+            sC(w, RB_BLACK);
+            sC(xp, RB_RED);
             rotate_left(xp);
-            w = t[xp].r;
+            w = R(xp);
           }
-          if ((t[w].l == NIL || t[t[w].l].color == RB_BLACK) && (t[w].r == NIL || t[t[w].r].color == RB_BLACK)) {
-            t[w].color = RB_RED;
+          const int wl = L(w), wr = R(w);
+          if ((wl == NIL || C(wl) == RB_BLACK) && (wr == NIL || C(wr) == RB_BLACK)) {
+            sC(w, RB_RED);
             x = xp;
-            xp = t[xp].p;
+            xp = P(xp);
           } else {
-            if (t[w].r == NIL || t[t[w].r].color == RB_BLACK) {
-              t[t[w].l].color = RB_BLACK;
-              t[w].color = RB_RED;
+            if (wr == NIL || C(wr) == RB_BLACK) {
+              sC(wl, RB_BLACK);
+              sC(w, RB_RED);
               rotate_right(w);
-              w = t[xp].r;
+              w = R(xp);
             }
-            t[w].color = t[xp].color;
-            t[xp].color = RB_BLACK;
-            if (t[w].r != NIL) t[t[w].r].color = RB_BLACK;
+            sC(w, C(xp));
+            sC(xp, RB_BLACK);
+            if (R(w) != NIL) sC(R(w), RB_BLACK);
             rotate_left(xp);
             break;
           }
         } else {
-          int w = t[xp].l;
-          if (t[w].color == RB_RED) {
-            t[w].color = RB_BLACK;
-            t[xp].color = RB_RED;
+          int w = L(xp);
+          if (C(w) == RB_RED) {
+            sC(w, RB_BLACK);
+            sC(xp, RB_RED);
             rotate_right(xp);
-            w = t[xp].l;
+            w = L(xp);
           }
-          if ((t[w].r == NIL || t[t[w].r].color == RB_BLACK) && (t[w].l == NIL || t[t[w].l].color == RB_BLACK)) {
-            t[w].color = RB_RED;
+          const int wl = L(w), wr = R(w);
+          if ((wr == NIL || C(wr) == RB_BLACK) && (wl == NIL || C(wl) == RB_BLACK)) {
+            sC(w, RB_RED);
             x = xp;
-            xp = t[xp].p;
+            xp = P(xp);
           } else {
-            if (t[w].l == NIL || t[t[w].l].color == RB_BLACK) {
-              t[t[w].r].color = RB_BLACK;
-              t[w].color = RB_RED;
+            if (wl == NIL || C(wl) == RB_BLACK) {
+              sC(wr, RB_BLACK);
+              sC(w, RB_RED);
               rotate_left(w);
-              w = t[xp].l;
+              w = L(xp);
             }
-            t[w].color = t[xp].color;
-            t[xp].color = RB_BLACK;
-            if (t[w].l != NIL) t[t[w].l].color = RB_BLACK;
+            sC(w, C(xp));
+            sC(xp, RB_BLACK);
+            if (L(w) != NIL) sC(L(w), RB_BLACK);
             rotate_right(xp);
             break;
           }
         }
       }
-      if (x != NIL) t[x].color = RB_BLACK;
+      if (x != NIL) sC(x, RB_BLACK);
     }
   }
 };
+
+template <class NodeT, class PtrT = NodeT*>
+using RBTree = RBT<AosAcc<NodeT, PtrT>>;
 
 // Pool allocator for tree nodes: bump pointer + intrusive free list through .l.
 struct PoolState {
   int next;   // next never-used index (index 0 is the header)
   int free;   // head of the free list (NIL if empty)
 };
+
+// pool over any tree layout (free list through the left link)
+template <class Acc>
+RB_HD int tpool_alloc(Acc& a, PoolState& ps, int cap) {
+  if (ps.free != NIL) {
+    const int i = ps.free;
+    ps.free = a.L(i);
+    return i;
+  }
+  if (ps.next >= cap) return NIL;
+  return ps.next++;
+}
+template <class Acc>
+RB_HD void tpool_free(Acc& a, PoolState& ps, int i) {
+  a.sL(i, ps.free);
+  ps.free = i;
+}
 
 template <class PtrT>
 RB_HD int pool_alloc(PtrT t, PoolState& ps, int cap) {

@@ -42,6 +42,10 @@ for B in args.batches:
     pops = sum(r["stats"]["pops"] for r in res)
     apops = sum(r["stats"]["astar_pops"] for r in res)
     bad = [i + 1 for i, r in enumerate(res) if r["stats"]["status"] != 0]
+    modes = [p.astar_modes() for p in ps[:B]]
+    hbm = sum(m["astar_pops_hbm"] for m in modes)
+    migr = sum(m["migrations"] for m in modes)
     print(json.dumps({"batch": B, "kernel_ms": kms, "wall_ms": wall * 1e3, "pops": pops, "astar_pops": apops,
-                      "pops_per_s": pops / (kms * 1e-3), "overflow_seeds": bad[:20], "n_overflow": len(bad)}),
+                      "pops_per_s": pops / (kms * 1e-3), "astar_pops_hbm": hbm, "astar_migrations": migr,
+                      "astar_searches": sum(r["stats"]["astar_searches"] for r in res), "overflow_seeds": bad[:20], "n_overflow": len(bad)}),
           flush=True)

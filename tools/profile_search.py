@@ -38,4 +38,7 @@ for s in args.seeds:
                           astar_searches=st["astar_searches"], successors=st["successors"],
                           loop_cycles=cyc[6], cycles_per_pop=cyc[6] / max(st["pops"], 1), share=share, **modes,
                           cyc_per_apop_lds=(cyc[3] - cyc[7]) / max(st["astar_pops"] - modes["astar_pops_hbm"], 1),
-                          cyc_per_apop_hbm=cyc[7] / max(modes["astar_pops_hbm"], 1))))
+                          cyc_per_apop_hbm=cyc[7] / max(modes["astar_pops_hbm"], 1),
+                          lds_astar_per_apop={n: round(cyc[8 + i] / max(st["astar_pops"] - modes["astar_pops_hbm"], 1))
+                                              for i, n in enumerate(["pop_probe", "find", "insert", "unlink_hit",
+                                                                     "memoise"])})))

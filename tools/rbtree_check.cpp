@@ -26,7 +26,7 @@ int main(int argc, char** argv) {
     const int fspace = 2 + (int)(rng() % 40);
     std::set<E, Less> ref;
     std::vector<Node3> pool(ops + 2);
-    RBTree<Node3> tr{pool.data()};
+    RBTree<Node3> tr{{pool.data()}};
     tr.clear();
     PoolState ps{1, NIL};
     std::vector<int> id_of_node(ops + 2, -1);
