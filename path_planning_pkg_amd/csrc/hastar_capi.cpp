@@ -724,7 +724,8 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   DeviceCtx& DC = *hs[0]->dc;
   std::lock_guard<std::mutex> lk(DC.mu);
   hipStream_t st = DC.stream;
-  const int W = std::max(1, std::min(n, DC.resident_slots));
+  int W = std::max(1, std::min(n, DC.resident_slots));
+  if (const char* e = std::getenv("HASTAR_SLOTS")) W = std::max(1, std::min(W, std::atoi(e)));
   if (int rc = arenas_acquire(DC, need, W)) return rc;
   const int slots = std::min(W, DC.n_arenas);
   if (n > DC.batch_cap) {
@@ -766,7 +767,10 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   HIPCHK(hipMemcpyAsync(DC.d_descs, descs.data(), (size_t)n * sizeof(PlannerDev), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(DC.d_order, order.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
   HIPCHK(hipEventRecord(DC.ev0, st));
-  HIPCHK(launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, DC.d_next, max_pops, st));
+  // raised issue priority for the head of the longest-first queue (HASTAR_PRIO_N overrides)
+  int n_prio = std::max(1, slots / 8);
+  if (const char* e = std::getenv("HASTAR_PRIO_N")) n_prio = std::atoi(e);
+  HIPCHK(launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, max_pops, st));
   HIPCHK(hipEventRecord(DC.ev1, st));
   HIPCHK(hipMemcpyAsync(DC.h_results, DC.d_results, (size_t)n * sizeof(SearchResult), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));

@@ -22,6 +22,13 @@ __device__ __forceinline__ GAS T* gp(T* p) {
   return (GAS T*)p;
 }
 
+// Wave-uniform value into an SGPR (values every lane loaded from the same address).
+__device__ __forceinline__ int ufi(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t ufu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ float uff(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
 // Cross-lane hand-off through LDS/HBM inside ONE wavefront: the wave's memory operations
 // stay in order in hardware (LLVM AMDGPU memory model: wavefront scope needs no cache or
 // counter action), so this is only a compiler barrier — unlike __syncthreads, which also

@@ -127,6 +127,7 @@ struct NodeB2 {
 struct AStarLds {
   NodeA2 a[A_CAP];
   NodeB2 b[A_CAP];
+  int16_t ring[A_CAP];  // live node indices in f order (a ring: rank r at ring[(head + r) % A_CAP])
 };
 
 #define LAS __attribute__((address_space(3)))
@@ -140,26 +141,27 @@ struct LdsAcc {
   LAS NodeA2* a;
   LAS NodeB2* b;
   GAS int* pv;
-  __device__ __forceinline__ int L(int x) const { return a[x].l; }
-  __device__ __forceinline__ int R(int x) const { return a[x].r; }
-  __device__ __forceinline__ int P(int x) const { return b[x].p; }
-  __device__ __forceinline__ int C(int x) const { return b[x].color; }
+  __device__ __forceinline__ int L(int x) const { return ufi(a[x].l); }
+  __device__ __forceinline__ int R(int x) const { return ufi(a[x].r); }
+  __device__ __forceinline__ int P(int x) const { return ufi(b[x].p); }
+  __device__ __forceinline__ int C(int x) const { return ufi(b[x].color); }
   __device__ __forceinline__ void sL(int x, int v) { a[x].l = (int16_t)v; }
   __device__ __forceinline__ void sR(int x, int v) { a[x].r = (int16_t)v; }
   __device__ __forceinline__ void sP(int x, int v) { b[x].p = (int16_t)v; }
   __device__ __forceinline__ void sC(int x, int v) { b[x].color = (int16_t)v; }
-  __device__ __forceinline__ uint32_t K(int x) const { return a[x].key; }
-  __device__ __forceinline__ float F(int x) const { return a[x].f; }
-  __device__ __forceinline__ float G(int x) const { return a[x].g; }
+  __device__ __forceinline__ uint32_t K(int x) const { return ufu(a[x].key); }
+  __device__ __forceinline__ float F(int x) const { return uff(a[x].f); }
+  __device__ __forceinline__ float G(int x) const { return uff(a[x].g); }
   __device__ __forceinline__ int PV(int x) const { return pv[x]; }
   __device__ __forceinline__ Quad quad(int x) const {
     typedef int v4 __attribute__((ext_vector_type(4)));
     const v4 v = *(const LAS v4*)&a[x];
     Quad q;
-    q.key = (uint32_t)v.x;
-    q.f = __int_as_float(v.y);
-    q.l = (v.w << 16) >> 16;
-    q.r = v.w >> 16;
+    const int w = ufi(v.w);
+    q.key = ufu((uint32_t)v.x);
+    q.f = __int_as_float(ufi(v.y));
+    q.l = (w << 16) >> 16;
+    q.r = w >> 16;
     return q;
   }
   __device__ __forceinline__ void leaf(int x, int p) {
@@ -170,9 +172,176 @@ struct LdsAcc {
     a[x].key = key;
     a[x].f = f;
     a[x].g = g;
-    pv[x] = prev;
+    (void)prev;  // pv[x] is stored by the caller after the expansion (see astar_loop_lds)
   }
 };
+// ---- f-ordered index of the LDS tree -------------------------------------------------
+// The reference's open-set comparator keeps the tree's in-order sequence STRICTLY
+// increasing in f (an insert whose in-order predecessor has an equal f, or the same cell,
+// is dropped).  So while no node of the probed cell sits on the "wrong" side of the probe
+// value, std::set::find / insert are decided by f ranks alone, independent of the tree
+// shape: find(k, f) returns the first node with f' >= f when f' == f or it is the cell's
+// own node; insert(k, f) attaches the new node between its rank neighbours (as the right
+// child of the predecessor when that slot is free, else as the left child of the
+// successor) unless the predecessor has f' == f or the same cell.  The wavefront answers
+// those rank queries with a 2-level parallel search over a ring of node indices kept in f
+// order (64 samples, then 16), instead of a ~10-level dependent tree walk.  The tree
+// itself is still maintained exactly (link / rebalance / erase), and the rare shape-
+// dependent cases (a node of the same cell with f' < probe f for find, f' > new f for
+// insert, or several nodes of that cell) fall back to the tree walks.
+struct Ring {
+  int head, n;
+};
+struct RankOut {
+  int r;        // #(live f < v)
+  int at;       // node at rank r (first with f >= v), NIL if r == n
+  float at_f;
+  int pred;     // node at rank r - 1, NIL if r == 0
+};
+
+// Level 1 samples every SR-th rank (64 lanes cover A_CAP ranks); level 2 resolves the
+// SR ranks of one bucket per value (lanes [0, SR) for value A, [SR, 2 SR) for value B).
+constexpr int SR = A_CAP / 64;
+static_assert(SR >= 2 && SR <= 32 && (SR & (SR - 1)) == 0, "A_CAP must be 128..2048, a power of two");
+
+__device__ __forceinline__ void rank_out(RankOut& O, int b, int cnt, int off, int n, int i1, float f1, int i2,
+                                         float f2) {
+  auto rl_i = [](int v, int l) { return __builtin_amdgcn_readlane(v, l); };
+  auto rl_f = [](float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+  if (b == 0) {
+    O.r = 0;
+    O.pred = NIL;
+    O.at = n > 0 ? rl_i(i1, 0) : NIL;
+    O.at_f = n > 0 ? rl_f(f1, 0) : 0.0f;
+    return;
+  }
+  O.r = (b - 1) * SR + cnt;
+  O.pred = rl_i(i2, off + cnt - 1);
+  if (O.r >= n) {
+    O.at = NIL;
+    O.at_f = 0.0f;
+  } else if (cnt < SR) {
+    O.at = rl_i(i2, off + cnt);
+    O.at_f = rl_f(f2, off + cnt);
+  } else {
+    O.at = rl_i(i1, b);
+    O.at_f = rl_f(f1, b);
+  }
+}
+
+__device__ __forceinline__ void rank2(const AStarLds& L, const Ring& rg, float vA, float vB, int lane, RankOut& A,
+                                      RankOut& B) {
+  constexpr int M = A_CAP - 1;
+  constexpr uint64_t SMASK = (SR == 32) ? 0xffffffffull : ((1ull << SR) - 1);
+  const int n = rg.n;
+  const int s_r = lane * SR;
+  const bool h1 = s_r < n;
+  const int i1 = (int)L.ring[(rg.head + s_r) & M] & M;  // unconditional loads, masked use
+  const float f1 = L.a[i1].f;
+  const int bA = __popcll(__ballot(h1 && f1 < vA)), bB = __popcll(__ballot(h1 && f1 < vB));
+  const bool forA = lane < SR;
+  const int bb = forA ? bA : bB;
+  const int sub = lane & (SR - 1);
+  const int r2 = (bb - 1) * SR + sub;
+  const bool h2 = lane < 2 * SR && bb > 0 && r2 < n;
+  const int i2 = (int)L.ring[(rg.head + r2) & M] & M;
+  const float f2 = L.a[i2].f;
+  const uint64_t m2 = __ballot(h2 && f2 < (forA ? vA : vB));
+  const int cA = __popcll(m2 & SMASK), cB = __popcll((m2 >> SR) & SMASK);
+  // lanes of level 2 hold ranks base..base+SR-1; rank base+SR is level-1 sample lane b
+  rank_out(A, bA, cA, 0, n, i1, f1, i2, f2);
+  rank_out(B, bB, cB, SR, n, i1, f1, i2, f2);
+}
+
+// ring insert of node x at rank r (shifts the shorter side by one)
+__device__ __forceinline__ void ring_insert(AStarLds& L, Ring& rg, int r, int x, int lane) {
+  constexpr int M = A_CAP - 1;
+  if (r < rg.n - r) {  // ranks [0, r) move one slot down, head - 1
+    rg.head = (rg.head - 1) & M;
+    for (int c0 = 0; c0 < r; c0 += 64) {
+      const int i = c0 + lane;
+      int16_t v = 0;
+      if (i < r) v = L.ring[(rg.head + i + 1) & M];
+      wave_lds_sync();
+      if (i < r) L.ring[(rg.head + i) & M] = v;
+      wave_lds_sync();
+    }
+  } else {  // ranks [r, n) move one slot up, from the top
+    for (int c1 = rg.n; c1 > r; c1 -= 64) {
+      const int i = c1 - 1 - lane;
+      int16_t v = 0;
+      if (i >= r) v = L.ring[(rg.head + i) & M];
+      wave_lds_sync();
+      if (i >= r) L.ring[(rg.head + i + 1) & M] = v;
+      wave_lds_sync();
+    }
+  }
+  if (lane == 0) L.ring[(rg.head + r) & M] = (int16_t)x;
+  rg.n++;
+  wave_lds_sync();
+}
+
+// ring erase of the node at rank r
+__device__ __forceinline__ void ring_erase(AStarLds& L, Ring& rg, int r, int lane) {
+  constexpr int M = A_CAP - 1;
+  if (r < rg.n - 1 - r) {  // ranks [0, r) move one slot up, head + 1
+    for (int c1 = r; c1 > 0; c1 -= 64) {
+      const int i = c1 - 1 - lane;
+      int16_t v = 0;
+      if (i >= 0) v = L.ring[(rg.head + i) & M];
+      wave_lds_sync();
+      if (i >= 0) L.ring[(rg.head + i + 1) & M] = v;
+      wave_lds_sync();
+    }
+    rg.head = (rg.head + 1) & M;
+  } else {  // ranks (r, n) move one slot down
+    for (int c0 = r + 1; c0 < rg.n; c0 += 64) {
+      const int i = c0 + lane;
+      int16_t v = 0;
+      if (i < rg.n) v = L.ring[(rg.head + i) & M];
+      wave_lds_sync();
+      if (i < rg.n) L.ring[(rg.head + i - 1) & M] = v;
+      wave_lds_sync();
+    }
+  }
+  rg.n--;
+}
+
+// nodes of cell `key` among the pool's used slots: cnt 0, 1 (idx, f) or 2 (= several)
+struct SameCell {
+  int cnt, idx;
+  float f;
+};
+__device__ __forceinline__ SameCell same_cell(const AStarLds& L, int used, uint32_t key, int lane) {
+  // all loads unconditional (in-bounds by construction) so they issue back to back
+  uint32_t kk[A_CAP / 64];
+#pragma unroll
+  for (int q = 0; q < A_CAP / 64; ++q) kk[q] = L.a[lane + 64 * q].key;
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < A_CAP / 64; ++q) m |= (uint32_t)((lane + 64 * q < used) & (kk[q] == key)) << q;
+  const uint64_t any = __ballot(m != 0);
+  SameCell sc;
+  sc.cnt = 0;
+  sc.idx = NIL;
+  sc.f = 0.0f;
+  if (any == 0) return sc;
+  if (__popcll(any) > 1) {
+    sc.cnt = 2;
+    return sc;
+  }
+  const int ln = __ffsll((unsigned long long)any) - 1;
+  const uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)m, ln);
+  if (__popc(mm) > 1) {
+    sc.cnt = 2;
+    return sc;
+  }
+  sc.cnt = 1;
+  sc.idx = ln + 64 * (__ffs(mm) - 1);
+  sc.f = uff(L.a[sc.idx].f);
+  return sc;
+}
+
 // HBM layout (Node2, 32-bit links, prev in the node)
 struct HbmAcc : AosAcc<Node2, GAS Node2*> {
   __device__ __forceinline__ float G(int x) const { return t[x].g; }
@@ -228,15 +397,15 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     STAMP_T t_pop = STAMP_NOW();
     const int b = tr.begin();
     const Quad top = tr.quad(b);
-    const float top_g = tr.G(b);
+    const float top_g = uff(tr.G(b));
     const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
     const uint32_t tcell = (uint32_t)tx * (uint32_t)P.N + (uint32_t)ty;
     // one HBM round trip: the popped cell's closed state and prev link, and the
     // neighbour probes (bounds, occupancy, memo flag, node-map f, closed membership —
     // loop-invariant during this expansion; Grid2D::get_neighbors, Grid2D.cpp:72-96)
-    const uint32_t tgen = cgen[tcell];
-    const int tcidx = cidx[tcell];
-    const int tprev = tr.PV(b);
+    const uint32_t tgen = ufu(cgen[tcell]);
+    const int tcidx = ufi(cidx[tcell]);
+    const int tprev = ufi(tr.PV(b));
     const int ni = tx + adx, nj = ty + ady;
     bool valid = false, vis = false, closed = false;
     float nf = 0.0f;
@@ -258,6 +427,9 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     if (tgen == c.gen2) {
       ci = tcidx;
       cur = gload(&cl[ci]);
+      cur.key = ufu(cur.key);
+      cur.g = uff(cur.g);
+      cur.f = uff(cur.f);
     } else {
       if (c.n_closed2 >= A.closed2_cap) { c.status = -75; *result = FLT_MAX; return true; }
       ci = c.n_closed2++;
@@ -282,9 +454,9 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     if (!G) STAMP_ADD(8, t_pop);
     for (int k = 0; k < nact; ++k) {
       if (!((vmask >> k) & 1ull)) continue;
-      const float kcost = shfl_f(acost, k);
+      const float kcost = uff(shfl_f(acost, k));
       if ((vismask >> k) & 1ull) {
-        const float tot = shfl_f(nf, k) + g0 + kcost;
+        const float tot = uff(shfl_f(nf, k)) + g0 + kcost;
         STAMP_T t_m = STAMP_NOW();
         memoise(c, tot, ci);
         STAMP_ADD(12, t_m);
@@ -292,9 +464,9 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
         return true;
       }
       if ((cmask >> k) & 1ull) continue;
-      const int ki = shfl_i(ni, k), kj = shfl_i(nj, k);
+      const int ki = ufi(shfl_i(ni, k)), kj = ufi(shfl_i(nj, k));
       const uint32_t key = ((uint32_t)ki << 16) | (uint32_t)kj;
-      const float fprobe = shfl_f(nf, k);  // stale _node_map f, as the reference reads it
+      const float fprobe = uff(shfl_f(nf, k));  // stale _node_map f, as the reference reads it
       STAMP_T t_f = STAMP_NOW();
       const int hit = tr.find(key, fprobe);
       if (!G) STAMP_ADD(9, t_f);
@@ -321,6 +493,203 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
   return true;
 }
 
+// insert (AStar.cpp:172-183) into the LDS tree: rank-decided unless shape-dependent
+__device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc>& tr, AStarLds& L, Ring& rg, uint32_t key,
+                                           float fn, float gn, int prev, const SameCell& sc, const RankOut& rb,
+                                           int* node_out) {
+  *node_out = NIL;
+  int parent;
+  bool left;
+  if (sc.cnt >= 2 || (sc.cnt == 1 && sc.f > fn)) {  // a node of this cell lies right of fn
+    parent = tr.insert_pos(key, fn, &left);
+    if (parent == -2) return true;
+  } else {
+    if ((rb.at != NIL && rb.at_f == fn) || (rb.pred != NIL && rb.pred == sc.idx)) return true;  // dropped
+    if (rg.n == 0) {
+      parent = 0;
+      left = true;
+    } else if (rb.pred == NIL) {
+      parent = rb.at;
+      left = true;
+    } else if (rb.at == NIL || tr.R(rb.pred) == NIL) {
+      parent = rb.pred;
+      left = false;
+    } else {
+      parent = rb.at;
+      left = true;
+    }
+  }
+  const int n = tpool_alloc(tr, c.ps2, A_CAP);
+  if (n == NIL) return false;
+  tr.payload(n, key, fn, gn, prev);
+  tr.link(left, n, parent);
+  ring_insert(L, rg, rb.r, n, c.lane);
+  *node_out = n;
+  return true;
+}
+
+__device__ __forceinline__ void free_lds(SearchCtx& c, RBT<LdsAcc>& tr, int x) {
+  tr.a[x].key = 0xffffffffu;  // dead: never matches a cell
+  tpool_free(tr, c.ps2, x);
+}
+
+// AStar::a_star_search (AStar.cpp:118-186) on the LDS tree.  Returns false (without
+// popping) when the next pop could overflow the LDS pool; true when the search finished
+// (*result = cost-to-goal or FLT_MAX).
+__device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AStarLds& L, Ring& rg, int adx,
+                                               int ady, float acost, float* result) {
+  const PlannerDev& P = *c.P;
+  const SlotArena& A = *c.A;
+  const int lane = c.lane;
+  const int nact = P.diag ? 8 : 4;
+  GAS Closed2* cl = gp(A.closed2);
+  GAS uint32_t* cgen = gp(A.cgen2);
+  GAS int* cidx = gp(A.cidx2);
+  while (rg.n > 0) {
+    if (c.ps2.next + 8 > A_CAP) return false;
+    STAMP_T t_pop = STAMP_NOW();
+    const int b = tr.begin();
+    const Quad top = tr.quad(b);
+    const float top_g = uff(tr.G(b));
+    const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
+    const uint32_t tcell = (uint32_t)tx * (uint32_t)P.N + (uint32_t)ty;
+    const uint32_t tgen = ufu(cgen[tcell]);
+    const int tcidx = ufi(cidx[tcell]);
+    const int tprev = ufi(tr.PV(b));
+    const int ni = tx + adx, nj = ty + ady;
+    bool valid = false, vis = false, closed = false;
+    float nf = 0.0f;
+    if (lane < nact && ni > -1 && ni < P.N && nj > -1 && nj < P.N) {
+      const uint32_t cell = (uint32_t)ni * (uint32_t)P.N + (uint32_t)nj;
+      const float occv = gp(P.occ)[cell];
+      const uint8_t visv = gp(P.visited)[cell];
+      nf = gp(P.nm_f)[cell];
+      const uint32_t cg = cgen[cell];
+      valid = occv < P.thr;
+      vis = valid && visv != 0;
+      closed = valid && cg == c.gen2;
+    }
+    // consume every probe before the first store of this pop, so that no later register
+    // reuse has to wait on a store (vmcnt counts loads and stores in issue order)
+    const uint64_t vmask = __ballot(valid), vismask = __ballot(vis), cmask = __ballot(closed);
+    nf = __builtin_amdgcn_readfirstlane(0) + nf;  // keep nf live in a VGPR (no-op)
+    tr.unlink(b);
+    free_lds(c, tr, b);
+    ring_erase(L, rg, 0, lane);
+    int ci;
+    Closed2 cur;
+    if (tgen == c.gen2) {
+      ci = tcidx;
+      cur = gload(&cl[ci]);
+      cur.key = ufu(cur.key);
+      cur.g = uff(cur.g);
+      cur.f = uff(cur.f);
+    } else {
+      if (c.n_closed2 >= A.closed2_cap) { c.status = -75; *result = FLT_MAX; return true; }
+      ci = c.n_closed2++;
+      cur.key = top.key;
+      cur.g = top_g;
+      cur.f = top.f;
+      cur.prev = tprev;
+      gstore(&cl[ci], cur);
+      cgen[tcell] = c.gen2;
+      cidx[tcell] = ci;
+    }
+    c.apops++;
+    const int cx = (int)(cur.key >> 16), cy = (int)(cur.key & 0xffffu);
+    if (cx == P.goal_cx && cy == P.goal_cy) {
+      memoise(c, cur.f, ci);
+      *result = cur.f;
+      return true;
+    }
+    const float g0 = cur.g;
+    STAMP_ADD(8, t_pop);
+    // The expansion's HBM stores (node-map f of inserted cells, prev links of new nodes) are
+    // collected in lane k and issued together after the loop: a global store inside the
+    // loop would make every later register reuse wait for its completion (vmcnt).
+    uint32_t st_cell = 0;
+    float st_f = 0.0f;
+    int st_node = NIL;
+    bool st_on = false;
+    for (int k = 0; k < nact; ++k) {
+      if (!((vmask >> k) & 1ull)) continue;
+      const float kcost = uff(shfl_f(acost, k));
+      if ((vismask >> k) & 1ull) {
+        const float tot = uff(shfl_f(nf, k)) + g0 + kcost;
+        if (st_on) {  // this expansion's earlier node-map writes happen before the return
+          gp(P.nm_f)[st_cell] = st_f;
+          if (st_node != NIL) gp(A.prevl)[st_node] = ci;
+        }
+        STAMP_T t_m = STAMP_NOW();
+        memoise(c, tot, ci);
+        STAMP_ADD(12, t_m);
+        *result = tot;
+        return true;
+      }
+      if ((cmask >> k) & 1ull) continue;
+      const int ki = ufi(shfl_i(ni, k)), kj = ufi(shfl_i(nj, k));
+      const uint32_t key = ((uint32_t)ki << 16) | (uint32_t)kj;
+      const float fprobe = uff(shfl_f(nf, k));  // stale _node_map f, as the reference reads it
+      const float gn = g0 + kcost;
+      const float fn = gn + euclid_h(P, ki, kj);
+      STAMP_T t_f = STAMP_NOW();
+      SameCell sc = same_cell(L, c.ps2.next, key, lane);
+      RankOut ra, rb;
+      rank2(L, rg, fprobe, fn, lane, ra, rb);
+      int hit = 0, hit_rank = -1;
+      if (sc.cnt >= 2 || (sc.cnt == 1 && sc.f < fprobe)) {
+        hit = tr.find(key, fprobe);  // shape-dependent: the exact tree walk
+      } else if (ra.at != NIL && (ra.at_f == fprobe || ra.at == sc.idx)) {
+        hit = ra.at;
+        hit_rank = ra.r;
+      }
+      STAMP_ADD(9, t_f);
+      if (hit == 0) {
+        STAMP_T t_i = STAMP_NOW();
+        int nn;
+        if (!insert_lds(c, tr, L, rg, key, fn, gn, ci, sc, rb, &nn)) { c.status = -75; *result = FLT_MAX; return true; }
+        if (lane == k) {  // Node2D::set_accumulated_cost + the new node's prev link
+          st_on = true;
+          st_cell = (uint32_t)ki * (uint32_t)P.N + (uint32_t)kj;
+          st_f = fn;
+          st_node = nn;
+        }
+        STAMP_ADD(10, t_i);
+      } else if (gn < tr.G(hit)) {
+        STAMP_T t_u = STAMP_NOW();
+        if (hit_rank < 0) {
+          const float hf = tr.F(hit);
+          RankOut h1, h2;
+          rank2(L, rg, hf, hf, lane, h1, h2);
+          hit_rank = h1.r;
+        }
+        tr.unlink(hit);
+        free_lds(c, tr, hit);
+        ring_erase(L, rg, hit_rank, lane);
+        STAMP_ADD(11, t_u);
+        sc = same_cell(L, c.ps2.next, key, lane);
+        RankOut r1;
+        rank2(L, rg, fn, fn, lane, r1, rb);
+        int nn;
+        if (!insert_lds(c, tr, L, rg, key, fn, gn, ci, sc, rb, &nn)) { c.status = -75; *result = FLT_MAX; return true; }
+        if (lane == k) {
+          st_on = true;
+          st_cell = (uint32_t)ki * (uint32_t)P.N + (uint32_t)kj;
+          st_f = fn;
+          st_node = nn;
+        }
+      }
+    }
+    if (st_on) {
+      gp(P.nm_f)[st_cell] = st_f;
+      if (st_node != NIL) gp(A.prevl)[st_node] = ci;
+    }
+    wave_lds_sync();
+  }
+  *result = FLT_MAX;
+  return true;
+}
+
 // AStar::find_path(int, int) (AStar.cpp:100-113)
 __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, int sj) {
   const PlannerDev& P = *c.P;
@@ -340,7 +709,15 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   tl.b = lp(L.b);
   tl.pv = gp(A.prevl);
   tl.clear();
-  insert2(c, tl, A_CAP, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL);
+  L.a[0].key = 0xffffffffu;
+  Ring rg{0, 0};
+  {
+    const SameCell none{0, NIL, 0.0f};
+    const RankOut at0{0, NIL, 0.0f, NIL};
+    int n0;
+    insert_lds(c, tl, L, rg, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL, none, at0, &n0);
+    gp(A.prevl)[n0] = NIL;
+  }
   wave_lds_sync();
   const int nact = P.diag ? 8 : 4;
   // this lane's action (Grid2D.cpp:22-40): nibble-packed (dx + 1, dy + 1) tables
@@ -353,7 +730,7 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
     acost = (adx != 0 && ady != 0) ? P.act_cost_diag : P.act_cost_axis;
   }
   float result = FLT_MAX;
-  if (astar_loop<false>(c, tl, adx, ady, acost, &result)) return result;
+  if (astar_loop_lds(c, tl, L, rg, adx, ady, acost, &result)) return result;
   // migrate the LDS tree to HBM nodes (identical indices) and continue there
   c.amigr++;
   GAS Node2* o2 = gp(A.open2);
@@ -673,7 +1050,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
 __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners,
                                                            const SlotArena* __restrict__ arenas,
                                                            const int* __restrict__ order, int* __restrict__ next,
-                                                           int max_pops) {
+                                                           int max_pops, int n_prio) {
   __shared__ Succ sl[MAXS];
   __shared__ AStarLds alds;
   SearchCtx c;
@@ -687,6 +1064,10 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
     if (c.lane == 0) q = atomicAdd(next, 1);
     q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
     if (q >= n_planners) break;
+    // the queue is ordered longest-expected-first; the head of it runs at raised issue
+    // priority so the batch's stragglers are not slowed by the waves sharing their SIMD
+    if (q < n_prio) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(0);
     c.P = descs + order[q];
     search_one(c, sl, alds, max_pops);
   }
@@ -896,12 +1277,12 @@ __global__ __launch_bounds__(64) void k_test_dubins_path(PlannerDev P, float sx,
 }
 
 // ------------------------------------------------------------- launch wrappers -------
-hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots, const int* d_order,
+hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots, const int* d_order, int n_prio,
                          int* d_next, int max_pops, hipStream_t st) {
   hipError_t e = hipMemsetAsync(d_next, 0, sizeof(int), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(hastar_search_kernel, dim3(n_slots), dim3(64), 0, st, d_descs, n, d_arenas, d_order, d_next,
-                     max_pops);
+                     max_pops, n_prio);
   return hipGetLastError();
 }
 int search_slots_per_cu() {

@@ -25,6 +25,18 @@
 
 namespace hastar {
 
+// Tree walks are wave-uniform (every lane follows the same path): on the device the
+// loaded links/keys are moved to SGPRs so the walk compiles to scalar control flow.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ int rb_ui(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t rb_uu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ float rb_uf(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+#else
+inline int rb_ui(int v) { return v; }
+inline uint32_t rb_uu(uint32_t v) { return v; }
+inline float rb_uf(float v) { return v; }
+#endif
+
 // comparator of the reference: (ka != kb) && (fa < fb)
 RB_HD bool rb_less(uint32_t ka, float fa, uint32_t kb, float fb) { return (ka != kb) && (fa < fb); }
 
@@ -42,10 +54,10 @@ __device__ __forceinline__ Quad rb_quad(PtrT t, int x) {
   (void)sizeof(K);
   const rb_v4i v = *reinterpret_cast<decltype(&reinterpret_cast<const rb_v4i&>(t[x]))>(&t[x]);
   Quad q;
-  q.key = (uint32_t)v.x;
-  q.f = __int_as_float(v.y);
-  q.l = v.z;
-  q.r = v.w;
+  q.key = rb_uu((uint32_t)v.x);
+  q.f = __int_as_float(rb_ui(v.y));
+  q.l = rb_ui(v.z);
+  q.r = rb_ui(v.w);
   return q;
 }
 #else
@@ -61,16 +73,16 @@ inline Quad rb_quad(PtrT t, int x) {
 template <class NodeT, class PtrT = NodeT*>
 struct AosAcc {
   PtrT t;
-  RB_HD int L(int x) const { return t[x].l; }
-  RB_HD int R(int x) const { return t[x].r; }
-  RB_HD int P(int x) const { return t[x].p; }
-  RB_HD int C(int x) const { return t[x].color; }
+  RB_HD int L(int x) const { return rb_ui(t[x].l); }
+  RB_HD int R(int x) const { return rb_ui(t[x].r); }
+  RB_HD int P(int x) const { return rb_ui(t[x].p); }
+  RB_HD int C(int x) const { return rb_ui(t[x].color); }
   RB_HD void sL(int x, int v) { t[x].l = v; }
   RB_HD void sR(int x, int v) { t[x].r = v; }
   RB_HD void sP(int x, int v) { t[x].p = v; }
   RB_HD void sC(int x, int v) { t[x].color = v; }
-  RB_HD uint32_t K(int x) const { return t[x].key; }
-  RB_HD float F(int x) const { return t[x].f; }
+  RB_HD uint32_t K(int x) const { return rb_uu(t[x].key); }
+  RB_HD float F(int x) const { return rb_uf(t[x].f); }
   RB_HD Quad quad(int x) const { return rb_quad(t, x); }
   RB_HD void leaf(int x, int p) {  // new node: parent p, no children, red
     t[x].p = p;

@@ -20,7 +20,11 @@ ap.add_argument("--grid", type=int, default=1024)
 ap.add_argument("--obstacles", type=int, default=200)
 ap.add_argument("--max-pops", type=int, default=131072)
 ap.add_argument("--max-astar-nodes", type=int, default=0)
+ap.add_argument("--repeat", type=int, default=1, help="runs per batch (later runs use the longest-first order)")
+ap.add_argument("--prio", type=int, nargs="*", default=None, help="HASTAR_PRIO_N values to sweep")
+ap.add_argument("--slots", type=int, nargs="*", default=None, help="HASTAR_SLOTS values to sweep")
 args = ap.parse_args()
+import os
 Bmax = max(args.batches)
 t = time.time()
 ps, cf = [], []
@@ -34,18 +38,26 @@ for q in range(Bmax):
     cf.append(proto)
 print(json.dumps({"setup_s": time.time() - t, "planners": Bmax}), flush=True)
 for B in args.batches:
-    for p in ps[:B]:
-        p.reset()
-    t0 = time.time()
-    res, kms = gpu.find_path_batch(ps[:B], [c["vel"] for c in cf[:B]], [c["start"] for c in cf[:B]], cap=8192)
-    wall = time.time() - t0
-    pops = sum(r["stats"]["pops"] for r in res)
-    apops = sum(r["stats"]["astar_pops"] for r in res)
-    bad = [i + 1 for i, r in enumerate(res) if r["stats"]["status"] != 0]
-    modes = [p.astar_modes() for p in ps[:B]]
-    hbm = sum(m["astar_pops_hbm"] for m in modes)
-    migr = sum(m["migrations"] for m in modes)
-    print(json.dumps({"batch": B, "kernel_ms": kms, "wall_ms": wall * 1e3, "pops": pops, "astar_pops": apops,
-                      "pops_per_s": pops / (kms * 1e-3), "astar_pops_hbm": hbm, "astar_migrations": migr,
-                      "astar_searches": sum(r["stats"]["astar_searches"] for r in res), "overflow_seeds": bad[:20], "n_overflow": len(bad)}),
-          flush=True)
+  for prio, slots in [(p_, s_) for p_ in (args.prio or [None]) for s_ in (args.slots or [None])]:
+   if prio is not None:
+       os.environ["HASTAR_PRIO_N"] = str(prio)
+   if slots is not None:
+       os.environ["HASTAR_SLOTS"] = str(slots)
+   for rep in range(args.repeat):
+        for p in ps[:B]:
+            p.reset()
+        t0 = time.time()
+        res, kms = gpu.find_path_batch(ps[:B], [c["vel"] for c in cf[:B]], [c["start"] for c in cf[:B]], cap=8192)
+        wall = time.time() - t0
+        pops = sum(r["stats"]["pops"] for r in res)
+        apops = sum(r["stats"]["astar_pops"] for r in res)
+        bad = [i + 1 for i, r in enumerate(res) if r["stats"]["status"] != 0]
+        modes = [p.astar_modes() for p in ps[:B]]
+        hbm = sum(m["astar_pops_hbm"] for m in modes)
+        migr = sum(m["migrations"] for m in modes)
+        print(json.dumps({"batch": B, "prio": prio, "slots": slots, "rep": rep, "kernel_ms": kms, "wall_ms": wall * 1e3, "pops": pops, "astar_pops": apops,
+                          "pops_per_s": pops / (kms * 1e-3), "astar_pops_hbm": hbm, "astar_migrations": migr,
+                          "astar_searches": sum(r["stats"]["astar_searches"] for r in res), "overflow_seeds": bad[:20], "n_overflow": len(bad),
+                          "max_work": max(r["stats"]["pops"] + r["stats"]["astar_pops"] for r in res),
+                          "mean_work": (pops + apops) / B}),
+              flush=True)
