@@ -29,8 +29,10 @@ PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 def algorithmic_bytes(st, K):
-    """B = 40 P + 44 S + 208 A + 12 K per plan."""
-    return 40 * st["pops"] + 44 * st["successors"] + 208 * st["astar_pops"] + 12 * K
+    """B = 40 P + 44 S + 208 A + 12 K per plan, summed over the batch
+    (st: the stats structured array of one batched call)."""
+    return float(40 * st["pops"].astype(np.float64).sum() + 44 * st["successors"].astype(np.float64).sum()
+                 + 208 * st["astar_pops"].astype(np.float64).sum() + 12.0 * K * len(st))
 
 
 def shard_query_ids(rank, world, batch):
@@ -66,12 +68,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("HASTAR_BENCH_BATCH", "8192")),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("HASTAR_BENCH_BATCH", "16384")),
                     help="planners (queries) per GPU")
     ap.add_argument("--grid", type=int, default=1024)
     ap.add_argument("--bins", type=int, default=72)
     ap.add_argument("--obstacles", type=int, default=200)
-    ap.add_argument("--max-pops", type=int, default=131072)
+    ap.add_argument("--max-pops", type=int, default=0, help="0 = library default (262144)")
     ap.add_argument("--max-astar-nodes", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -112,8 +114,8 @@ def main():
     def step():
         for p in planners:
             p.reset()
-        res, kms = gpu.find_path_batch(planners, vels, starts, cap=8192)
-        return res, kms
+        br = gpu.find_path_batch_arrays(planners, vels, starts, cap=8192)
+        return br, br.kernel_ms
 
     for _ in range(args.warmup):
         step()
@@ -130,10 +132,11 @@ def main():
     for _ in range(args.steps):
         res, kms = step()
         kernel_ms.append(kms)
-        pops += sum(r["stats"]["pops"] for r in res)
-        alg_bytes.append(sum(algorithmic_bytes(r["stats"], args.obstacles) for r in res))
-        statuses |= {r["stats"]["status"] for r in res}
-        oks += sum(r["ok"] for r in res)
+        st = res.stats
+        pops += int(st["pops"].sum())
+        alg_bytes.append(algorithmic_bytes(st, args.obstacles))
+        statuses |= set(int(v) for v in np.unique(st["status"]))
+        oks += int(res.ok.sum())
         last = res
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
@@ -220,7 +223,7 @@ def cpu_baseline(cfgs, gpu_results, budget_s, replans):
             wall += r["wall_ms"] * 1e-3
             plans += 1
         n += 1
-        g = gpu_results[i]
+        g = gpu_results.result(i)
         parity &= (r["stats"]["pop_digest"] == g["stats"]["pop_digest"] and r["ok"] == g["ok"]
                    and np.float32(r["cost"]).tobytes() == np.float32(g["cost"]).tobytes())
         o.close()

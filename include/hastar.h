@@ -56,7 +56,7 @@ typedef struct hastar_params {
   const float* curvature_weights;
   /* ---- extensions (0 = default) ---- */
   int max_pops;                    /* arena: Hybrid A* pops per search (default 262144) */
-  int max_astar_nodes;             /* arena: holonomic A* nodes per inner search (default N*N) */
+  int max_astar_nodes;             /* arena: open-set nodes of one inner A* search (default min(N*N+16, 65536)) */
   int max_dubins_samples;          /* arena: samples of one Dubins shot (default from N) */
 } hastar_params;
 

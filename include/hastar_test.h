@@ -31,6 +31,9 @@ int hastar_debug_closed_keys(hastar_handle h, int* out, int cap);
 int hastar_debug_cycles(hastar_handle h, unsigned long long* out16);
 /* {inner A* searches migrated from LDS to HBM, inner A* pops done in HBM mode} of the last search. */
 int hastar_debug_astar_modes(hastar_handle h, long long* out2);
+/* Timing of the last search: {t_start, t_end} in s_memrealtime ticks (100 MHz, chip-wide
+ * clock) and the slot (persistent wavefront) that ran it. */
+int hastar_debug_timing(hastar_handle h, unsigned long long* out3);
 
 #ifdef __cplusplus
 }

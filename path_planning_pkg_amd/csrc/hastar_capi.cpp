@@ -189,12 +189,12 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
   D.n_arenas = 0;
   const size_t b_open3 = align256((size_t)r.open3 * sizeof(Node3)), b_closed3 = align256((size_t)r.closed3 * sizeof(Closed3));
   const size_t b_slots = align256((size_t)r.slots * sizeof(Slot3)), b_open2 = align256((size_t)r.open2 * sizeof(Node2));
-  const size_t b_closed2 = align256((size_t)r.closed2 * sizeof(Closed2)), b_cgen = align256(r.cells * sizeof(uint32_t));
-  const size_t b_cidx = align256(r.cells * sizeof(int)), b_gens = 256, b_dub = align256((size_t)r.dub * 3 * sizeof(float));
+  const size_t b_closed2 = align256((size_t)r.closed2 * sizeof(Closed2)), b_cell = align256(r.cells * sizeof(Cell2));
+  const size_t b_gens = 256, b_dub = align256((size_t)r.dub * 3 * sizeof(float));
   const size_t b_dubc = align256((size_t)r.dub * sizeof(float)), b_chain = align256((size_t)r.chain * sizeof(int));
   const size_t b_prevl = align256((size_t)ASTAR_LDS_CAP * sizeof(int));
   const size_t per =
-      b_open3 + b_closed3 + b_slots + b_open2 + b_closed2 + b_cgen + b_cidx + b_gens + b_dub + b_dubc + b_chain + b_prevl;
+      b_open3 + b_closed3 + b_slots + b_open2 + b_closed2 + b_cell + b_gens + b_dub + b_dubc + b_chain + b_prevl;
   // memory budget of the pool: HASTAR_ARENA_MB, else 80% of the free HBM
   size_t budget = 0;
   if (const char* e = std::getenv("HASTAR_ARENA_MB")) budget = (size_t)std::strtoull(e, nullptr, 10) << 20;
@@ -221,8 +221,7 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
     A.slots3 = reinterpret_cast<Slot3*>(q); q += b_slots;
     A.open2 = reinterpret_cast<Node2*>(q); q += b_open2;
     A.closed2 = reinterpret_cast<Closed2*>(q); q += b_closed2;
-    A.cgen2 = reinterpret_cast<uint32_t*>(q); q += b_cgen;
-    A.cidx2 = reinterpret_cast<int*>(q); q += b_cidx;
+    A.cell2 = reinterpret_cast<Cell2*>(q); q += b_cell;
     A.gens = reinterpret_cast<uint32_t*>(q); q += b_gens;
     A.dub_xyh = reinterpret_cast<float*>(q); q += b_dub;
     A.dub_curv = reinterpret_cast<float*>(q); q += b_dubc;
@@ -238,7 +237,7 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
     A.chain_cap = r.chain;
     // generation-stamped tables start at generation 0 (all stale)
     HIPCHK(hipMemsetAsync(A.slots3, 0, b_slots, D.stream));
-    HIPCHK(hipMemsetAsync(A.cgen2, 0, b_cgen, D.stream));
+    HIPCHK(hipMemsetAsync(A.cell2, 0, b_cell, D.stream));
     HIPCHK(hipMemsetAsync(A.gens, 0, b_gens, D.stream));
   }
   HIPCHK(dalloc(&D.d_arenas, (size_t)n));
@@ -268,6 +267,8 @@ struct hastar_handle_s {
   int* d_rp = nullptr;
   float* d_dl = nullptr;
   int rp_cap = 0;
+  int* d_ids = nullptr;          // box indices grouped by raster layer
+  int ids_cap = 0;
   float* d_lp = nullptr;
   float* d_seq = nullptr;
   float* d_wid = nullptr;
@@ -285,6 +286,7 @@ static void free_handle(hastar_handle h) {
   if (h->slab) hipFree(h->slab);
   if (h->d_rp) hipFree(h->d_rp);
   if (h->d_dl) hipFree(h->d_dl);
+  if (h->d_ids) hipFree(h->d_ids);
   if (h->d_lp) hipFree(h->d_lp);
   if (h->d_seq) hipFree(h->d_seq);
   if (h->d_wid) hipFree(h->d_wid);
@@ -390,9 +392,12 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   R.closed3 = h->max_pops + 1;
   R.slots = 1;
   while (R.slots < 2u * (uint32_t)h->max_pops + 64) R.slots <<= 1;
-  const int astar_cap = p->max_astar_nodes > 0 ? p->max_astar_nodes : (int)std::min<size_t>(NN + 16, 1u << 30);
+  // inner A*: the closed records are bounded by the cells (N^2); the open tree by its
+  // frontier, which stays far below N^2 (max_astar_nodes, default min(N^2 + 16, 65536))
+  const int astar_cap =
+      p->max_astar_nodes > 0 ? p->max_astar_nodes : (int)std::min<size_t>(NN + 16, (size_t)65536);
   R.open2 = astar_cap + 1;
-  R.closed2 = (int)std::min<size_t>(NN, (size_t)astar_cap);
+  R.closed2 = (int)std::min<size_t>(NN, (size_t)1 << 30);
   R.cells = NN;
   int dub_cap = p->max_dubins_samples;
   if (dub_cap <= 0) {
@@ -401,7 +406,11 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   }
   R.dub = dub_cap;
   R.chain = h->max_pops + 2;
-  D.out_cap = dub_cap + h->max_pops + 2;
+  // path buffer of the planner: Dubins samples + the prev chain of the terminal node.  A
+  // chain visits distinct (cell, bin) keys one step apart, so 8 N poses cover any
+  // realistic path; a longer one ends the search with HASTAR_ENOSPC (reported, never
+  // truncated).
+  D.out_cap = dub_cap + std::min(h->max_pops + 2, 8 * N + 64);
 
   // the planner's persistent state: one allocation
   const size_t b_occ = align256(NN * sizeof(float)), b_nm = align256(NN * sizeof(float)), b_vis = align256(NN);
@@ -428,6 +437,7 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   D.n_apf = 0;
   hipStream_t st = dc->stream;
   hipError_t he = hipMemsetAsync(D.occ, 0, NN * sizeof(float), st);
+  D.vgen = 1;
   if (he == hipSuccess) he = hipMemsetAsync(D.visited, 0, NN, st);
   if (he == hipSuccess) he = hipMemcpyAsync(D.off, off.data(), off.size() * sizeof(float), hipMemcpyHostToDevice, st);
   if (he == hipSuccess) he = hipMemcpyAsync(D.dth, dth.data(), ns * sizeof(float), hipMemcpyHostToDevice, st);
@@ -498,7 +508,15 @@ int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3
 int hastar_reset(hastar_handle h) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipMemsetAsync(h->desc.visited, 0, (size_t)h->desc.N * h->desc.N, h->dc->stream));
+  // the memo flags are generation-stamped: reset is a new generation; the map is only
+  // cleared when the 8-bit generation wraps
+  PlannerDev& D = h->desc;
+  if (D.vgen >= 255) {
+    HIPCHK(hipMemsetAsync(D.visited, 0, (size_t)D.N * D.N, h->dc->stream));
+    D.vgen = 1;
+  } else {
+    D.vgen++;
+  }
   return HASTAR_OK;
 }
 
@@ -562,10 +580,53 @@ int hastar_update_boxes(hastar_handle h, const float* boxes, const float* conf, 
     HIPCHK(hipMemcpyAsync(D.apf, apf.data(), (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, DC.stream));
     HIPCHK(hipMemcpyAsync(h->d_rp, rp.data(), (size_t)n * 4 * sizeof(int), hipMemcpyHostToDevice, DC.stream));
     HIPCHK(hipMemcpyAsync(h->d_dl, dl.data(), (size_t)n * sizeof(float), hipMemcpyHostToDevice, DC.stream));
+    // Layers: box k goes one layer above every earlier box whose cell footprint it may
+    // share, so boxes within a layer touch disjoint cells (applied concurrently) and
+    // overlapping boxes are applied in the reference's order (Grid2D.cpp:99-139 loops
+    // over obstacles in sequence).  Footprints: the rotated sub-sample rectangle's
+    // bounds plus a 2-cell margin for rounding.
+    const float cg = g_cosf(gh), sg = g_sinf(gh);
+    std::vector<int> bb((size_t)n * 4), layer(n, 0);
+    int n_layers = 0;
+    for (int k = 0; k < n; ++k) {
+      const float X = (rp[4 * k + 2] - 1) * 0.5f, Y = (rp[4 * k + 3] - 1) * 0.5f;
+      const float xs[4] = {0.0f, X * cg, Y * sg, X * cg + Y * sg};
+      const float ys[4] = {0.0f, -X * sg, Y * cg, -X * sg + Y * cg};
+      bb[4 * k] = rp[4 * k] + (int)std::floor(*std::min_element(xs, xs + 4)) - 2;
+      bb[4 * k + 1] = rp[4 * k] + (int)std::ceil(*std::max_element(xs, xs + 4)) + 2;
+      bb[4 * k + 2] = rp[4 * k + 1] + (int)std::floor(*std::min_element(ys, ys + 4)) - 2;
+      bb[4 * k + 3] = rp[4 * k + 1] + (int)std::ceil(*std::max_element(ys, ys + 4)) + 2;
+      int l = 0;
+      for (int j = 0; j < k; ++j)
+        if (layer[j] >= l && bb[4 * j] <= bb[4 * k + 1] && bb[4 * k] <= bb[4 * j + 1] && bb[4 * j + 2] <= bb[4 * k + 3] &&
+            bb[4 * k + 2] <= bb[4 * j + 3])
+          l = layer[j] + 1;
+      layer[k] = l;
+      n_layers = std::max(n_layers, l + 1);
+    }
+    std::vector<int> ids;
+    std::vector<int> first(n_layers + 1, 0);
+    ids.reserve(n);
+    for (int l = 0; l < n_layers; ++l) {
+      first[l] = (int)ids.size();
+      for (int k = 0; k < n; ++k)
+        if (layer[k] == l) ids.push_back(k);
+    }
+    first[n_layers] = n;
+    if (n > h->ids_cap) {
+      HIPCHK(hipStreamSynchronize(DC.stream));
+      if (h->d_ids) hipFree(h->d_ids);
+      h->d_ids = nullptr;
+      h->ids_cap = 0;
+      HIPCHK(dalloc(&h->d_ids, (size_t)n));
+      h->ids_cap = n;
+    }
+    HIPCHK(hipMemcpyAsync(h->d_ids, ids.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice, DC.stream));
     std::lock_guard<std::mutex> lk(DC.mu);
     if (int rc = scratch_acquire(DC, (size_t)D.N * D.N)) return rc;
-    HIPCHK(launch_raster_boxes(D.occ, DC.cnt, D.N, h->d_rp, h->d_dl, n, g_cosf(gh), g_sinf(gh), h->lp_min,
-                               h->lp_max, DC.stream));
+    for (int l = 0; l < n_layers; ++l)
+      HIPCHK(launch_raster_boxes(D.occ, DC.cnt, D.N, h->d_rp, h->d_dl, h->d_ids + first[l], first[l + 1] - first[l], cg,
+                                 sg, h->lp_min, h->lp_max, DC.stream));
   }
   return HASTAR_OK;
 }
@@ -931,6 +992,7 @@ int hastar_debug_memo(hastar_handle h, float* f_out, unsigned char* visited_out)
   const size_t NN = (size_t)h->desc.N * h->desc.N;
   HIPCHK(hipMemcpy(f_out, h->desc.nm_f, NN * sizeof(float), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(visited_out, h->desc.visited, NN, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < NN; ++i) visited_out[i] = visited_out[i] == (unsigned char)h->desc.vgen ? 1 : 0;
   return HASTAR_OK;
 }
 
@@ -963,6 +1025,14 @@ int hastar_debug_motion(hastar_handle h, float* off, float* dth, float* cost, fl
 int hastar_debug_cycles(hastar_handle h, unsigned long long* out8) {
   if (!h || !h->have_last) return fail(HASTAR_EINVAL, "no search result");
   for (int q = 0; q < 16; ++q) out8[q] = h->last.cycles[q];
+  return HASTAR_OK;
+}
+
+int hastar_debug_timing(hastar_handle h, unsigned long long* out3) {
+  if (!h || !h->have_last) return fail(HASTAR_EINVAL, "no search result");
+  out3[0] = h->last.t_start;
+  out3[1] = h->last.t_end;
+  out3[2] = (unsigned long long)h->last.slot;
   return HASTAR_OK;
 }
 

@@ -237,10 +237,13 @@ __device__ __forceinline__ float apf_field(const PlannerDev& P, float px, float 
     const int k = base + lane;
     float term = 0.0f;
     bool near = false;
-    if (k < P.n_apf) {
-      const GAS float* apf = gp(P.apf);
-      const float ox = apf[3 * k], oy = apf[3 * k + 1], orad = apf[3 * k + 2];
-      const float dx = ox - px, dy = oy - py;
+    const GAS float* apf = gp(P.apf);
+    const float ox = k < P.n_apf ? apf[3 * k] : 0.0f, oy = k < P.n_apf ? apf[3 * k + 1] : 0.0f;
+    const float orad = k < P.n_apf ? apf[3 * k + 2] : 0.0f;
+    const float dx = ox - px, dy = oy - py;
+    // exact pre-test: the correctly rounded hypotf(dx, dy) >= max(|dx|, |dy|), so an
+    // obstacle outside the axis-aligned square of half-width r cannot have d < r
+    if (k < P.n_apf && fabsf(dx) < orad && fabsf(dy) < orad) {
       const float d = g_hypotf(dx, dy);
       if (d < orad) {
         near = true;

@@ -13,8 +13,8 @@ hipError_t launch_init_nodemap(const PlannerDev& P, hipStream_t st);
 hipError_t launch_decay(float* occ, size_t NN, float lp_free, float lp_min, float lp_max, hipStream_t st);
 hipError_t launch_relocate(int N, float c, float s, float ox, float oy, const float* src, float* dst, int* winner,
                            hipStream_t st);
-hipError_t launch_raster_boxes(float* occ, int* cnt, int N, const int* rp, const float* dl, int nbox, float c,
-                               float s, float lp_min, float lp_max, hipStream_t st);
+hipError_t launch_raster_boxes(float* occ, int* cnt, int N, const int* rp, const float* dl, const int* ids, int nid,
+                               float c, float s, float lp_min, float lp_max, hipStream_t st);
 hipError_t launch_raster_lines(float* occ, int* cnt, int N, int n45, int n2, float res, const float* lp,
                                const float* seq_len, const float* seq_wid, int seq_stride, int nline, float lp_min,
                                float lp_max, hipStream_t st);

@@ -361,7 +361,7 @@ __device__ __forceinline__ void memoise(SearchCtx& c, float total, int from) {
   for (int i = from; i != NIL;) {
     const Closed2 r = gload(&cl[i]);
     const size_t cell = (size_t)(r.key >> 16) * P.N + (r.key & 0xffffu);
-    gp(P.visited)[cell] = 1;
+    gp(P.visited)[cell] = (uint8_t)P.vgen;
     gp(P.nm_f)[cell] = total - r.g;
     i = r.prev;
   }
@@ -389,8 +389,7 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
   GAS Closed2* cl = gp(A.closed2);
-  GAS uint32_t* cgen = gp(A.cgen2);
-  GAS int* cidx = gp(A.cidx2);
+  GAS Cell2* cells = gp(A.cell2);
   const int cap = G ? A.open2_cap : A_CAP;
   while (!tr.empty()) {
     if (!G && c.ps2.next + 8 > A_CAP) return false;
@@ -403,8 +402,8 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     // one HBM round trip: the popped cell's closed state and prev link, and the
     // neighbour probes (bounds, occupancy, memo flag, node-map f, closed membership —
     // loop-invariant during this expansion; Grid2D::get_neighbors, Grid2D.cpp:72-96)
-    const uint32_t tgen = ufu(cgen[tcell]);
-    const int tcidx = ufi(cidx[tcell]);
+    const uint32_t tgen = ufu(cells[tcell].cgen);
+    const int tcidx = ufi(cells[tcell].cidx);
     const int tprev = ufi(tr.PV(b));
     const int ni = tx + adx, nj = ty + ady;
     bool valid = false, vis = false, closed = false;
@@ -414,9 +413,9 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
       const float occv = gp(P.occ)[cell];
       const uint8_t visv = gp(P.visited)[cell];
       nf = gp(P.nm_f)[cell];
-      const uint32_t cg = cgen[cell];
+      const uint32_t cg = cells[cell].cgen;
       valid = occv < P.thr;
-      vis = valid && visv != 0;
+      vis = valid && visv == (uint8_t)P.vgen;
       closed = valid && cg == c.gen2;
     }
     tr.unlink(b);
@@ -438,8 +437,8 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
       cur.f = top.f;
       cur.prev = tprev;
       gstore(&cl[ci], cur);
-      cgen[tcell] = c.gen2;
-      cidx[tcell] = ci;
+      cells[tcell].cgen = c.gen2;
+      cells[tcell].cidx = ci;
     }
     c.apops++;
     if (G) c.apops_g++;
@@ -543,8 +542,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
   GAS Closed2* cl = gp(A.closed2);
-  GAS uint32_t* cgen = gp(A.cgen2);
-  GAS int* cidx = gp(A.cidx2);
+  GAS Cell2* cells = gp(A.cell2);
   while (rg.n > 0) {
     if (c.ps2.next + 8 > A_CAP) return false;
     STAMP_T t_pop = STAMP_NOW();
@@ -553,21 +551,23 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     const float top_g = uff(tr.G(b));
     const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
     const uint32_t tcell = (uint32_t)tx * (uint32_t)P.N + (uint32_t)ty;
-    const uint32_t tgen = ufu(cgen[tcell]);
-    const int tcidx = ufi(cidx[tcell]);
+    const uint32_t tgen = ufu(cells[tcell].cgen);
+    const int tcidx = ufi(cells[tcell].cidx);
     const int tprev = ufi(tr.PV(b));
     const int ni = tx + adx, nj = ty + ady;
     bool valid = false, vis = false, closed = false;
     float nf = 0.0f;
+    uint32_t ohint = 0xffffffffu;  // this lane's cell: last open node (| dup << 16), or none
     if (lane < nact && ni > -1 && ni < P.N && nj > -1 && nj < P.N) {
       const uint32_t cell = (uint32_t)ni * (uint32_t)P.N + (uint32_t)nj;
       const float occv = gp(P.occ)[cell];
       const uint8_t visv = gp(P.visited)[cell];
       nf = gp(P.nm_f)[cell];
-      const uint32_t cg = cgen[cell];
+      const Cell2 cr = gload(&cells[cell]);
       valid = occv < P.thr;
-      vis = valid && visv != 0;
-      closed = valid && cg == c.gen2;
+      vis = valid && visv == (uint8_t)P.vgen;
+      closed = valid && cr.cgen == c.gen2;
+      if (cr.ogen == c.gen2) ohint = cr.oinfo;
     }
     // consume every probe before the first store of this pop, so that no later register
     // reuse has to wait on a store (vmcnt counts loads and stores in issue order)
@@ -592,8 +592,8 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
       cur.f = top.f;
       cur.prev = tprev;
       gstore(&cl[ci], cur);
-      cgen[tcell] = c.gen2;
-      cidx[tcell] = ci;
+      cells[tcell].cgen = c.gen2;
+      cells[tcell].cidx = ci;
     }
     c.apops++;
     const int cx = (int)(cur.key >> 16), cy = (int)(cur.key & 0xffffu);
@@ -607,7 +607,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     // The expansion's HBM stores (node-map f of inserted cells, prev links of new nodes) are
     // collected in lane k and issued together after the loop: a global store inside the
     // loop would make every later register reuse wait for its completion (vmcnt).
-    uint32_t st_cell = 0;
+    uint32_t st_cell = 0, st_hint = 0;
     float st_f = 0.0f;
     int st_node = NIL;
     bool st_on = false;
@@ -618,7 +618,11 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
         const float tot = uff(shfl_f(nf, k)) + g0 + kcost;
         if (st_on) {  // this expansion's earlier node-map writes happen before the return
           gp(P.nm_f)[st_cell] = st_f;
-          if (st_node != NIL) gp(A.prevl)[st_node] = ci;
+          if (st_node != NIL) {
+            gp(A.prevl)[st_node] = ci;
+            cells[st_cell].ogen = c.gen2;
+            cells[st_cell].oinfo = st_hint;
+          }
         }
         STAMP_T t_m = STAMP_NOW();
         memoise(c, tot, ci);
@@ -633,7 +637,20 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
       const float gn = g0 + kcost;
       const float fn = gn + euclid_h(P, ki, kj);
       STAMP_T t_f = STAMP_NOW();
-      SameCell sc = same_cell(L, c.ps2.next, key, lane);
+      // nodes of this cell in the open tree: from the cell's hint (its last inserted node;
+      // exact unless a duplicate was ever inserted in this search, then scan the pool)
+      const uint32_t hint = ufu((uint32_t)__builtin_amdgcn_readlane((int)ohint, k));
+      bool dup = false;
+      SameCell sc{0, NIL, 0.0f};
+      if (hint != 0xffffffffu) {
+        dup = (hint >> 16) & 1u;
+        if (dup) {
+          sc = same_cell(L, c.ps2.next, key, lane);
+        } else {
+          const int y = (int)(hint & 0xffffu);
+          if (ufu(L.a[y].key) == key) sc = SameCell{1, y, uff(L.a[y].f)};
+        }
+      }
       RankOut ra, rb;
       rank2(L, rg, fprobe, fn, lane, ra, rb);
       int hit = 0, hit_rank = -1;
@@ -648,11 +665,12 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
         STAMP_T t_i = STAMP_NOW();
         int nn;
         if (!insert_lds(c, tr, L, rg, key, fn, gn, ci, sc, rb, &nn)) { c.status = -75; *result = FLT_MAX; return true; }
-        if (lane == k) {  // Node2D::set_accumulated_cost + the new node's prev link
-          st_on = true;
+        if (lane == k) {  // Node2D::set_accumulated_cost; the cell's nm_f is written even
+          st_on = true;   // when the insert is dropped (AStar.cpp:172-183)
           st_cell = (uint32_t)ki * (uint32_t)P.N + (uint32_t)kj;
           st_f = fn;
           st_node = nn;
+          st_hint = nn == NIL ? ohint : ((uint32_t)nn | (uint32_t)(dup || sc.cnt > 0) << 16);
         }
         STAMP_ADD(10, t_i);
       } else if (gn < tr.G(hit)) {
@@ -667,7 +685,8 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
         free_lds(c, tr, hit);
         ring_erase(L, rg, hit_rank, lane);
         STAMP_ADD(11, t_u);
-        sc = same_cell(L, c.ps2.next, key, lane);
+        if (dup) sc = same_cell(L, c.ps2.next, key, lane);
+        else if (hit == sc.idx) sc = SameCell{0, NIL, 0.0f};
         RankOut r1;
         rank2(L, rg, fn, fn, lane, r1, rb);
         int nn;
@@ -677,12 +696,17 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
           st_cell = (uint32_t)ki * (uint32_t)P.N + (uint32_t)kj;
           st_f = fn;
           st_node = nn;
+          st_hint = nn == NIL ? ohint : ((uint32_t)nn | (uint32_t)(dup || sc.cnt > 0) << 16);
         }
       }
     }
     if (st_on) {
       gp(P.nm_f)[st_cell] = st_f;
-      if (st_node != NIL) gp(A.prevl)[st_node] = ci;
+      if (st_node != NIL) {
+        gp(A.prevl)[st_node] = ci;
+        cells[st_cell].ogen = c.gen2;
+        cells[st_cell].oinfo = st_hint;
+      }
     }
     wave_lds_sync();
   }
@@ -696,7 +720,7 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   const SlotArena& A = *c.A;
   const int lane = c.lane;
   const size_t s_cell = (size_t)si * P.N + sj;
-  if (gp(P.visited)[s_cell]) return gp(P.nm_f)[s_cell];
+  if (gp(P.visited)[s_cell] == (uint8_t)P.vgen) return gp(P.nm_f)[s_cell];
   const float h0 = euclid_h(P, si, sj);
   gp(P.nm_f)[s_cell] = h0;  // Grid2D::set_start_node_grid -> Node2D::soft_reset
   c.asearch++;
@@ -717,6 +741,8 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
     int n0;
     insert_lds(c, tl, L, rg, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL, none, at0, &n0);
     gp(A.prevl)[n0] = NIL;
+    gp(A.cell2)[s_cell].ogen = c.gen2;
+    gp(A.cell2)[s_cell].oinfo = (uint32_t)n0;
   }
   wave_lds_sync();
   const int nact = P.diag ? 8 : 4;
@@ -786,6 +812,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
 #ifdef HASTAR_STAMPS
   for (int q = 0; q < 16; ++q) c.cyc[q] = 0;
 #endif
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   c.o3.t = gp(A.open3);
   c.gen3 += 1;
   c.n_closed3 = 0;
@@ -1035,6 +1062,9 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
     R->dubins_len = dub_n;
     R->astar_migrations = c.amigr;
     R->astar_pops_hbm = c.apops_g;
+    R->t_start = t_start;
+    R->t_end = __builtin_amdgcn_s_memrealtime();
+    R->slot = (int)blockIdx.x;
 #ifdef HASTAR_STAMPS
     for (int q = 0; q < 16; ++q) R->cycles[q] = c.cyc[q];
 #else
@@ -1146,10 +1176,16 @@ __global__ void k_relocate_gather(size_t NN, const float* __restrict__ src, int*
 // workgroup walks them); inside one box every sub-sample adds the same delta and clamps,
 // so a cell hit m times gets that step m times — counted with atomics, applied once per
 // cell.  rp: per box {start_i, start_j, 2*end_i, 2*end_j}; dl: per box delta.
-__global__ __launch_bounds__(1024) void k_raster_boxes(float* __restrict__ occ, int* __restrict__ cnt, int N,
-                                                       const int* __restrict__ rp, const float* __restrict__ dl,
-                                                       int nbox, float c, float s, float lp_min, float lp_max) {
-  for (int k = 0; k < nbox; ++k) {
+// Boxes of one "layer" (no two of them touch a common cell; the host orders layers so
+// that overlapping boxes are applied in the reference's index order): one workgroup per
+// box.  Within a box every sub-sample applies the same update, so counting the hits per
+// cell and applying them m times in a row equals the reference's sequential loop.
+__global__ __launch_bounds__(256) void k_raster_boxes(float* __restrict__ occ, int* __restrict__ cnt, int N,
+                                                      const int* __restrict__ rp, const float* __restrict__ dl,
+                                                      const int* __restrict__ ids, int nid, float c, float s,
+                                                      float lp_min, float lp_max) {
+  for (int q = blockIdx.x; q < nid; q += gridDim.x) {
+    const int k = ids[q];
     const int si = rp[4 * k], sj = rp[4 * k + 1], ni = rp[4 * k + 2], nj = rp[4 * k + 3];
     const float d = dl[k];
     const int total = ni * nj;
@@ -1167,7 +1203,7 @@ __global__ __launch_bounds__(1024) void k_raster_boxes(float* __restrict__ occ, 
           } else {
             const int m = atomicExch(&cnt[cell], 0);
             float v = occ[cell];
-            for (int q = 0; q < m; ++q) {
+            for (int r = 0; r < m; ++r) {
               v += d;
               v = stl_max(stl_min(v, lp_max), lp_min);
             }
@@ -1313,9 +1349,10 @@ hipError_t launch_relocate(int N, float c, float s, float ox, float oy, const fl
   hipLaunchKernelGGL(k_relocate_gather, dim3(blocks), dim3(256), 0, st, NN, src, winner, dst);
   return hipGetLastError();
 }
-hipError_t launch_raster_boxes(float* occ, int* cnt, int N, const int* rp, const float* dl, int nbox, float c,
-                               float s, float mn, float mx, hipStream_t st) {
-  hipLaunchKernelGGL(k_raster_boxes, dim3(1), dim3(1024), 0, st, occ, cnt, N, rp, dl, nbox, c, s, mn, mx);
+hipError_t launch_raster_boxes(float* occ, int* cnt, int N, const int* rp, const float* dl, const int* ids, int nid,
+                               float c, float s, float mn, float mx, hipStream_t st) {
+  if (nid <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_raster_boxes, dim3(nid), dim3(256), 0, st, occ, cnt, N, rp, dl, ids, nid, c, s, mn, mx);
   return hipGetLastError();
 }
 hipError_t launch_raster_lines(float* occ, int* cnt, int N, int n45, int n2, float res, const float* lp,

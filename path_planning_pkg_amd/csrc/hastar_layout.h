@@ -60,6 +60,18 @@ struct alignas(16) Closed2 {
   int prev;
 };
 
+// Per-cell record of the inner A* (slot arena, N*N, generation-stamped so a new search
+// needs no clearing): closed membership (cgen == search generation -> closed record cidx)
+// and a hint for the open tree (ogen == generation -> the cell's last inserted open node
+// is onode = oinfo & 0xffff; bit 16 set once a second node of the cell was inserted while
+// another was still open).
+struct alignas(16) Cell2 {
+  uint32_t cgen;
+  int cidx;
+  uint32_t ogen;
+  uint32_t oinfo;
+};
+
 // Closed-set hash slot (open addressing; generation-stamped so clear() is O(1)).
 struct Slot3 {
   uint32_t gen;
@@ -78,6 +90,8 @@ struct SearchResult {
   int dubins_len;         // samples of the successful shot
   int astar_migrations;   // inner A* searches that outgrew LDS
   unsigned long long cycles[16]; // diagnostic build (-DHASTAR_STAMPS): s_memtime per phase
+  unsigned long long t_start, t_end;  // s_memrealtime (100 MHz, chip-wide) around the search
+  int slot, pad_r;                    // slot (wavefront) that ran it
 };
 
 // Descriptor of one planner: constants + device pointers.  Lives in HBM; the kernel
@@ -86,7 +100,7 @@ struct PlannerDev {
   // --- grid / vehicle constants (Grid2D.cpp:7-62, VehicleModel.cpp:7-47, HybridAStar.cpp:7-24)
   int N, n2, n45, diag;
   int bins, nsteer, na, shot_interval;
-  int shot_decay, n_apf, pad_i0, pad_i1;
+  int shot_decay, n_apf, vgen, pad_i1;  // vgen: generation that marks visited cells
   float res, thr, apf_rep, apf_ang;
   float ts, a_lat, a_lat2, prec;
   float r_min, step, ang_step, act_cost_diag;   // Dubins radius/step; 2D diagonal move cost
@@ -102,7 +116,7 @@ struct PlannerDev {
   // --- state arrays
   float* occ;            // N*N log-odds (_obstacle_map), row i = x cell
   float* nm_f;           // N*N Node2D::_cost_f of _node_map (A* memo + stale f)
-  uint8_t* visited;      // N*N AStar::_visted
+  uint8_t* visited;      // N*N AStar::_visted: cell is visited iff visited[cell] == vgen
   float* apf;            // n_apf x {x, y, r} (Grid3D::_apf_obstacles)
   float* off;            // nsteer x (bins + 1) x {dx, dy} (VehicleModel::_offset_xy + zero row)
   float* dth;            // nsteer  _offset_heading
@@ -128,9 +142,8 @@ struct SlotArena {
   Slot3* slots3;    uint32_t slots3_mask; int pad2;
   Node2* open2;     int open2_cap;   int pad3;
   Closed2* closed2; int closed2_cap; int pad4;
-  uint32_t* cgen2;  // N*N generation stamps (cell -> closed record of the current A* search)
-  int* cidx2;
-  size_t cells;     // capacity of cgen2/cidx2 (max N*N served)
+  Cell2* cell2;     // N*N per-cell records of the current inner A* search
+  size_t cells;     // capacity of cell2 (max N*N served)
   uint32_t* gens;   // [0] closed-set generation, [1] A* closed generation
   float* dub_xyh; float* dub_curv; int dub_cap; int pad5;
   int* out_chain;   int chain_cap;   int pad6;

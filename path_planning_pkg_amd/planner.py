@@ -64,6 +64,7 @@ def load_library():
     L.hastar_debug_closed_keys.argtypes = [vp, ip, C.c_int]
     L.hastar_debug_cycles.argtypes = [vp, C.POINTER(C.c_ulonglong)]
     L.hastar_debug_astar_modes.argtypes = [vp, C.POINTER(C.c_longlong)]
+    L.hastar_debug_timing.argtypes = [vp, C.POINTER(C.c_ulonglong)]
     _lib = L
     return L
 
@@ -192,6 +193,12 @@ class HybridAStar:
         _check(load_library().hastar_debug_astar_modes(self.h, out))
         return {"migrations": out[0], "astar_pops_hbm": out[1]}
 
+    def timing(self):
+        """(t_start, t_end, slot) of the last search; times in 10 ns ticks."""
+        out = (C.c_ulonglong * 3)()
+        _check(load_library().hastar_debug_timing(self.h, out))
+        return out[0], out[1], int(out[2])
+
     def field(self, poses):
         p = _f32(poses, (-1, 3))
         out = np.empty(len(p), np.float32)
@@ -207,6 +214,45 @@ class HybridAStar:
                                                       C.byref(n), C.byref(length), C.byref(flag)))
         k = n.value
         return xyh[:max(k, 0)].copy(), curv[:max(k, 0)].copy(), length.value, bool(flag.value)
+
+
+class BatchResult:
+    """Array view of one hastar_find_path_batch call (no per-planner Python objects)."""
+
+    def __init__(self, cost, ok, lens, xyh, curv, stats, kernel_ms):
+        self.cost, self.ok, self.lens, self.xyh, self.curv = cost, ok, lens, xyh, curv
+        self.stats = stats            # numpy structured array with the hastar_stats fields
+        self.kernel_ms = kernel_ms
+
+    def __len__(self):
+        return len(self.cost)
+
+    def result(self, i):
+        k = int(self.lens[i])
+        st = {name: self.stats[name][i].item() for name in self.stats.dtype.names}
+        return dict(cost=float(self.cost[i]), ok=bool(self.ok[i]), path=self.xyh[i, :k].copy(),
+                    curvature=self.curv[i, :k].copy(), stats=st)
+
+
+def find_path_batch_arrays(planners, vels, starts, cap=4096):
+    """hastar_find_path_batch with array outputs (BatchResult)."""
+    L = load_library()
+    n = len(planners)
+    hs = (C.c_void_p * n)(*[p.h.value for p in planners])
+    v = _f32(vels)
+    s = _f32(starts, (n, 3))
+    xyh = np.empty((n, cap, 3), np.float32)
+    curv = np.empty((n, cap), np.float32)
+    ln = np.zeros(n, np.int32)
+    ok = np.zeros(n, np.int32)
+    cost = np.zeros(n, np.float32)
+    stats = (HastarStats * n)()
+    rc = L.hastar_find_path_batch(hs, n, fptr(v), fptr(s), fptr(xyh), fptr(curv), cap, iptr(ln), fptr(cost),
+                                  iptr(ok), stats)
+    if rc != HASTAR_EOVERFLOW:  # per-planner arena overflows are reported in stats["status"]
+        _check(rc)
+    st = np.ctypeslib.as_array(stats)
+    return BatchResult(cost, ok, ln, xyh, curv, st, float(L.hastar_last_search_ms()))
 
 
 def find_path_batch(planners, vels, starts, cap=4096):

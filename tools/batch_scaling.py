@@ -18,13 +18,30 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batches", type=int, nargs="+", default=[64, 256, 1024])
 ap.add_argument("--grid", type=int, default=1024)
 ap.add_argument("--obstacles", type=int, default=200)
-ap.add_argument("--max-pops", type=int, default=131072)
+ap.add_argument("--max-pops", type=int, default=0)
 ap.add_argument("--max-astar-nodes", type=int, default=0)
 ap.add_argument("--repeat", type=int, default=1, help="runs per batch (later runs use the longest-first order)")
 ap.add_argument("--prio", type=int, nargs="*", default=None, help="HASTAR_PRIO_N values to sweep")
 ap.add_argument("--slots", type=int, nargs="*", default=None, help="HASTAR_SLOTS values to sweep")
 args = ap.parse_args()
 import os
+
+
+def timing_summary(planners, res):
+    """Per-planner start/end times (s_memrealtime, 10 ns) -> span, straggler and balance."""
+    import numpy as np
+    t = np.array([p.timing() for p in planners], dtype=np.float64)
+    t0 = t[:, 0].min()
+    dur = (t[:, 1] - t[:, 0]) * 1e-5          # ms
+    end = (t[:, 1] - t0) * 1e-5
+    i = int(np.argmax(dur))
+    work = np.array([r["stats"]["pops"] + r["stats"]["astar_pops"] for r in res], np.float64)
+    slots = t[:, 2].astype(int)
+    busy = np.bincount(slots, weights=dur)
+    return {"span_ms": float(end.max()), "max_dur_ms": float(dur.max()), "max_dur_seed": i + 1,
+            "max_dur_start_ms": float((t[i, 0] - t0) * 1e-5), "max_dur_work": float(work[i]),
+            "mean_slot_busy_ms": float(busy[busy > 0].mean()), "n_slots": int((busy > 0).sum()),
+            "ns_per_work": float(dur.sum() * 1e6 / work.sum())}
 Bmax = max(args.batches)
 t = time.time()
 ps, cf = [], []
@@ -59,5 +76,6 @@ for B in args.batches:
                           "pops_per_s": pops / (kms * 1e-3), "astar_pops_hbm": hbm, "astar_migrations": migr,
                           "astar_searches": sum(r["stats"]["astar_searches"] for r in res), "overflow_seeds": bad[:20], "n_overflow": len(bad),
                           "max_work": max(r["stats"]["pops"] + r["stats"]["astar_pops"] for r in res),
+                          **timing_summary(ps[:B], res),
                           "mean_work": (pops + apops) / B}),
               flush=True)
