@@ -231,15 +231,50 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 // obstacle list.  Terms of obstacles farther than their radius are exactly +0.0f in
 // the reference, so only in-radius terms are accumulated — in obstacle order, one at a
 // time, exactly like std::accumulate.
-__device__ __forceinline__ float apf_field(const PlannerDev& P, float px, float py, float ph, int lane) {
+// The first APF_REG_ROUNDS x 64 obstacles of a planner are held in registers for the
+// whole search (loaded once); any further ones are read from HBM per call.
+constexpr int APF_REG_ROUNDS = 4;
+struct ApfRegs {
+  float ox[APF_REG_ROUNDS], oy[APF_REG_ROUNDS], orad[APF_REG_ROUNDS];
+};
+__device__ __forceinline__ void apf_load_regs(const PlannerDev& P, ApfRegs& R, int lane) {
+  const GAS float* apf = gp(P.apf);
+#pragma unroll
+  for (int q = 0; q < APF_REG_ROUNDS; ++q) {
+    const int k = 64 * q + lane;
+    const bool in = k < P.n_apf;
+    R.ox[q] = in ? apf[3 * k] : 0.0f;
+    R.oy[q] = in ? apf[3 * k + 1] : 0.0f;
+    R.orad[q] = in ? apf[3 * k + 2] : 0.0f;
+  }
+}
+
+__device__ __forceinline__ float apf_field(const PlannerDev& P, const ApfRegs& R, float px, float py, float ph,
+                                           int lane) {
   float acc = 0.0f;
-  for (int base = 0; base < P.n_apf; base += 64) {
+  for (int base = 0, q = 0; base < P.n_apf; base += 64, ++q) {
     const int k = base + lane;
     float term = 0.0f;
     bool near = false;
-    const GAS float* apf = gp(P.apf);
-    const float ox = k < P.n_apf ? apf[3 * k] : 0.0f, oy = k < P.n_apf ? apf[3 * k + 1] : 0.0f;
-    const float orad = k < P.n_apf ? apf[3 * k + 2] : 0.0f;
+    float ox, oy, orad;
+    if (q < APF_REG_ROUNDS) {
+      // static register index: select through the unrolled rounds
+      ox = R.ox[0];
+      oy = R.oy[0];
+      orad = R.orad[0];
+#pragma unroll
+      for (int u = 1; u < APF_REG_ROUNDS; ++u)
+        if (q == u) {
+          ox = R.ox[u];
+          oy = R.oy[u];
+          orad = R.orad[u];
+        }
+    } else {
+      const GAS float* apf = gp(P.apf);
+      ox = k < P.n_apf ? apf[3 * k] : 0.0f;
+      oy = k < P.n_apf ? apf[3 * k + 1] : 0.0f;
+      orad = k < P.n_apf ? apf[3 * k + 2] : 0.0f;
+    }
     const float dx = ox - px, dy = oy - py;
     // exact pre-test: the correctly rounded hypotf(dx, dy) >= max(|dx|, |dy|), so an
     // obstacle outside the axis-aligned square of half-width r cannot have d < r

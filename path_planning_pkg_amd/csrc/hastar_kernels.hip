@@ -43,7 +43,7 @@ struct SearchCtx {
   const PlannerDev* __restrict__ P;   // planner descriptor in HBM (uniform, read-only: scalar loads)
   const SlotArena* __restrict__ A;    // this wave's search arena
   int lane;
-  RBTree<Node3, GAS Node3*> o3;
+  RBT<CachedAcc<Node3>> o3;  // outer open tree: HBM nodes behind a register node cache
   PoolState ps3, ps2;
   int n_closed3, n_closed2;
   uint32_t gen3, gen2;
@@ -164,6 +164,7 @@ struct LdsAcc {
     q.r = w >> 16;
     return q;
   }
+  __device__ __forceinline__ Quad quad_at(int x, int) const { return quad(x); }
   __device__ __forceinline__ void leaf(int x, int p) {
     *(LAS int*)&a[x].l = -1;  // l = r = NIL
     *(LAS int*)&b[x] = (RB_RED << 16) | (p & 0xffff);
@@ -786,11 +787,10 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, in
   const uint32_t key = key3(s.cx, s.cy, s.bin);
   const int pos = c.o3.insert_pos(key, f, &left);
   if (pos == -2) return true;
-  const int n = pool_alloc(gp(c.A->open3), c.ps3, c.A->open3_cap);
+  const int n = tpool_alloc(c.o3, c.ps3, c.A->open3_cap);
   if (n == NIL) return false;
   auto d = &gp(c.A->open3)[n];
-  d->key = key;
-  d->f = f;
+  c.o3.set_kf(n, key, f);
   d->g = s.g;
   d->vmin = s.vmin;
   d->x = s.x;
@@ -813,7 +813,11 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
   for (int q = 0; q < 16; ++q) c.cyc[q] = 0;
 #endif
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  ApfRegs apr;
+  apf_load_regs(P, apr, lane);
   c.o3.t = gp(A.open3);
+  c.o3.lane = lane;
+  c.o3.reset_cache();
   c.gen3 += 1;
   c.n_closed3 = 0;
   c.n_closed2 = 0;
@@ -856,7 +860,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
     const int ci = closed3_insert(c, top);
     if (ci == NIL) { c.status = -75; break; }
     c.o3.unlink(b);
-    pool_free(gp(A.open3), c.ps3, b);
+    tpool_free(c.o3, c.ps3, b);
     c.pops++;
     const Closed3 cur = gload(&gp(A.closed3)[ci]);
     const int cx = key3_x(cur.key), cy = key3_y(cur.key), cbin = key3_bin(cur.key);
@@ -900,37 +904,44 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
     shot_allowed = cur.vmin < 1.0f;
     int lo = cur.ci - P.na;
     lo = lo < 0 ? 0 : lo;
+    // one lane per action of the window [lo, lo + span) ∩ [0, nsteer); kept successors
+    // are compacted in action order (the reference's push_back order)
     int ns = 0;
-    for (int i = lo; i < lo + span && i < P.nsteer; ++i) {
+    {
+      const int i = lo + lane;
+      bool keep = lane < span && i < P.nsteer;
+      Succ s;
       float vm = 0.0f;
-      if (!shot_allowed) {
+      if (keep && !shot_allowed) {
         const float lat = cur.vmin * gp(P.curv_abs)[i];
-        if (lat > P.a_lat) continue;
+        if (lat > P.a_lat) keep = false;
         const float al = (float)sqrt(1.0 - (double)((lat * lat) / P.a_lat2));
         vm = cur.vmin - 2.0f * al * P.ts;
       }
-      const GAS float* o = &gp(P.off)[2 * ((size_t)i * (P.bins + 1) + cbin)];
-      Succ s;
-      s.x = cur.x + o[0];
-      s.y = cur.y + o[1];
-      s.h = wrap_pi_f(cur.h + gp(P.dth)[i]);
-      s.g = cur.g + gp(P.act_cost)[i];
-      s.vmin = vm;
-      s.ci = i;
-      s.bin = heading_bin(s.h, P.prec);
-      s.cx = trunc_f(s.x / P.res);
-      s.cy = trunc_f(s.y / P.res);
-      if (!(s.cx > -1 && s.cx < P.N && s.cy > -1 && s.cy < P.N)) continue;
-      if (!(gp(P.occ)[(size_t)s.cx * P.N + s.cy] < P.thr)) continue;
-      s.dub = 0.0f;
-      if (lane == 0) sl[ns] = s;
-      ++ns;
+      if (keep) {
+        const GAS float* o = &gp(P.off)[2 * ((size_t)i * (P.bins + 1) + cbin)];
+        s.x = cur.x + o[0];
+        s.y = cur.y + o[1];
+        s.h = wrap_pi_f(cur.h + gp(P.dth)[i]);
+        s.g = cur.g + gp(P.act_cost)[i];
+        s.vmin = vm;
+        s.ci = i;
+        s.bin = heading_bin(s.h, P.prec);
+        s.cx = trunc_f(s.x / P.res);
+        s.cy = trunc_f(s.y / P.res);
+        s.dub = 0.0f;
+        keep = s.cx > -1 && s.cx < P.N && s.cy > -1 && s.cy < P.N;
+        if (keep) keep = gp(P.occ)[(size_t)s.cx * P.N + s.cy] < P.thr;
+      }
+      const uint64_t km = __ballot(keep);
+      ns = __popcll(km);
+      if (keep) sl[__popcll(km & ((1ull << lane) - 1))] = s;
     }
     wave_lds_sync();
     c.succ += ns;
     // APF field of every kept successor (lanes over obstacles)
     for (int q = 0; q < ns; ++q) {
-      const float fc = apf_field(P, sl[q].x, sl[q].y, sl[q].h, lane);
+      const float fc = apf_field(P, apr, sl[q].x, sl[q].y, sl[q].h, lane);
       wave_lds_sync();
       if (lane == 0) sl[q].g = sl[q].g + fc;
       wave_lds_sync();
@@ -958,25 +969,41 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
     // ---- HybridAStar.cpp:159-193
     STAMP_T tb = STAMP_NOW();
     bool fail = false;
+    // closed-set membership of all successors at once (lane q probes successor q; the
+    // closed set does not change while the successors are processed)
+    uint64_t closed_m;
+    {
+      bool isc = false;
+      if (lane < ns) isc = closed3_contains(c, key3(sl[lane].cx, sl[lane].cy, sl[lane].bin));
+      closed_m = __ballot(isc);
+    }
     for (int q = 0; q < ns; ++q) {
       const Succ s = sl[q];
       const uint32_t key = key3(s.cx, s.cy, s.bin);
-      if (closed3_contains(c, key)) continue;
+      if ((closed_m >> q) & 1ull) continue;
+      STAMP_T tf3 = STAMP_NOW();
       const int hit = c.o3.find(key, s.g);  // f == g before the heuristic is added
+      STAMP_ADD(13, tf3);
       if (hit == 0) {
         STAMP_T ta = STAMP_NOW();
         const float h1 = holonomic(c, alds, s.cx, s.cy);
         STAMP_ADD(3, ta);
         const float f = s.g + stl_max(h1, s.dub);
+        STAMP_T ti3 = STAMP_NOW();
         if (!insert3(c, s, f, ci)) { fail = true; break; }
+        STAMP_ADD(14, ti3);
       } else if (s.g < gp(A.open3)[hit].g) {
+        STAMP_T tu3 = STAMP_NOW();
         c.o3.unlink(hit);
-        pool_free(gp(A.open3), c.ps3, hit);
+        tpool_free(c.o3, c.ps3, hit);
+        STAMP_ADD(15, tu3);
         STAMP_T ta = STAMP_NOW();
         const float h1 = holonomic(c, alds, s.cx, s.cy);
         STAMP_ADD(3, ta);
         const float f = s.g + stl_max(h1, s.dub);
+        STAMP_T ti3 = STAMP_NOW();
         if (!insert3(c, s, f, ci)) { fail = true; break; }
+        STAMP_ADD(14, ti3);
       }
       if (c.status != 0) break;
     }
@@ -1282,7 +1309,9 @@ __global__ void k_test_math(int fn, const float* a, const float* b, float* out, 
 
 __global__ __launch_bounds__(64) void k_test_field(PlannerDev P, const float* poses, int n, float* out) {
   for (int q = blockIdx.x; q < n; q += gridDim.x) {
-    const float f = apf_field(P, poses[3 * q], poses[3 * q + 1], poses[3 * q + 2], threadIdx.x);
+    ApfRegs apr;
+    apf_load_regs(P, apr, threadIdx.x);
+    const float f = apf_field(P, apr, poses[3 * q], poses[3 * q + 1], poses[3 * q + 2], threadIdx.x);
     if (threadIdx.x == 0) out[q] = f;
   }
 }

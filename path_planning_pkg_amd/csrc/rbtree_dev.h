@@ -27,10 +27,16 @@ namespace hastar {
 
 // Tree walks are wave-uniform (every lane follows the same path): on the device the
 // loaded links/keys are moved to SGPRs so the walk compiles to scalar control flow.
+#if defined(__HIPCC__)
+__host__ __device__ __forceinline__ int rb_ui(int v) {
 #if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ int rb_ui(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ uint32_t rb_uu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-__device__ __forceinline__ float rb_uf(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+  return __builtin_amdgcn_readfirstlane(v);
+#else
+  return v;
+#endif
+}
+__host__ __device__ __forceinline__ uint32_t rb_uu(uint32_t v) { return (uint32_t)rb_ui((int)v); }
+__host__ __device__ __forceinline__ float rb_uf(float v) { return __int_as_float(rb_ui(__float_as_int(v))); }
 #else
 inline int rb_ui(int v) { return v; }
 inline uint32_t rb_uu(uint32_t v) { return v; }
@@ -62,7 +68,7 @@ __device__ __forceinline__ Quad rb_quad(PtrT t, int x) {
 }
 #else
 template <class PtrT>
-inline Quad rb_quad(PtrT t, int x) {
+RB_HD Quad rb_quad(PtrT t, int x) {
   return Quad{t[x].key, t[x].f, t[x].l, t[x].r};
 }
 #endif
@@ -84,6 +90,7 @@ struct AosAcc {
   RB_HD uint32_t K(int x) const { return rb_uu(t[x].key); }
   RB_HD float F(int x) const { return rb_uf(t[x].f); }
   RB_HD Quad quad(int x) const { return rb_quad(t, x); }
+  RB_HD Quad quad_at(int x, int depth) { return quad(x); }  // walk step at depth (cache hook)
   RB_HD void leaf(int x, int p) {  // new node: parent p, no children, red
     t[x].p = p;
     t[x].l = NIL;
@@ -105,9 +112,9 @@ struct RBT : Acc {
   using Acc::K;
   using Acc::F;
 
-  RB_HD int root() const { return P(0); }
-  RB_HD int begin() const { return L(0); }          // == 0 (header) when empty
-  RB_HD bool empty() const { return P(0) == NIL; }
+  RB_HD int root() { return P(0); }
+  RB_HD int begin() { return L(0); }  // == 0 (header) when empty
+  RB_HD bool empty() { return P(0) == NIL; }
 
   RB_HD void clear() {
     sP(0, NIL);
@@ -144,7 +151,7 @@ struct RBT : Acc {
     sP(x, y);
   }
 
-  RB_HD int decrement(int x) const {
+  RB_HD int decrement(int x) {
     if (C(x) == RB_RED && P(x) != NIL && P(P(x)) == x) return R(x);  // header
     if (L(x) != NIL) {
       int y = L(x);
@@ -161,12 +168,12 @@ struct RBT : Acc {
 
   // std::set::find (stl_tree.h _M_lower_bound + key_compare check).  Returns 0 (= end)
   // when not "found".
-  RB_HD int find(uint32_t k, float f) const {
-    int y = 0, x = P(0);
+  RB_HD int find(uint32_t k, float f) {
+    int y = 0, x = P(0), depth = 0;
     uint32_t yk = 0;
     float yf = 0.0f;
     while (x != NIL) {
-      const Quad q = this->quad(x);
+      const Quad q = this->quad_at(x, depth++);
       if (!rb_less(q.key, q.f, k, f)) {
         y = x;
         yk = q.key;
@@ -182,13 +189,13 @@ struct RBT : Acc {
 
   // _M_get_insert_unique_pos: returns the parent for the new node (>= 0) or -2 when an
   // "equivalent" element exists (insert dropped).  *left = insert_left of _M_insert_.
-  RB_HD int insert_pos(uint32_t k, float f, bool* left) const {
-    int x = P(0), y = 0;
+  RB_HD int insert_pos(uint32_t k, float f, bool* left) {
+    int x = P(0), y = 0, depth = 0;
     bool comp = true;
     uint32_t yk = 0;
     float yf = 0.0f;
     while (x != NIL) {
-      const Quad q = this->quad(x);
+      const Quad q = this->quad_at(x, depth++);
       y = x;
       yk = q.key;
       yf = q.f;
@@ -269,11 +276,11 @@ struct RBT : Acc {
     sC(P(0), RB_BLACK);
   }
 
-  RB_HD int minimum(int x) const {
+  RB_HD int minimum(int x) {
     while (L(x) != NIL) x = L(x);
     return x;
   }
-  RB_HD int maximum(int x) const {
+  RB_HD int maximum(int x) {
     while (R(x) != NIL) x = R(x);
     return x;
   }
@@ -383,6 +390,88 @@ struct RBT : Acc {
 
 template <class NodeT, class PtrT = NodeT*>
 using RBTree = RBT<AosAcc<NodeT, PtrT>>;
+
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+// HBM nodes behind a 64-entry, fully associative, write-through node cache held in the
+// wavefront's registers (lane i caches one node: id, key, f, l, r, p, color).  A tree
+// walk step that hits costs a ballot and a few lane reads instead of a dependent HBM
+// round trip.  Walk steps at depth d < 32 fill lane d (the top of the tree stays
+// resident); other misses fill lanes 32..63 round-robin.  Every link/key write goes to
+// HBM and to any lane caching that node, so the cache is never stale; it is reset when
+// the arena starts a new search.
+template <class NodeT>
+struct CachedAcc {
+  __attribute__((address_space(1))) NodeT* t;
+  int lane;
+  int cid;      // this lane's cached node (walk steps only: key, f, l, r)
+  uint32_t ck;
+  float cf;
+  int cl, cr;
+  int rr;
+
+  __device__ __forceinline__ void reset_cache() {
+    cid = -1;
+    rr = 0;
+  }
+  __device__ __forceinline__ int L(int x) const { return rb_ui(t[x].l); }
+  __device__ __forceinline__ int R(int x) const { return rb_ui(t[x].r); }
+  __device__ __forceinline__ int P(int x) const { return rb_ui(t[x].p); }
+  __device__ __forceinline__ int C(int x) const { return rb_ui(t[x].color); }
+  __device__ __forceinline__ void sL(int x, int v) {
+    t[x].l = v;
+    cl = cid == x ? v : cl;
+  }
+  __device__ __forceinline__ void sR(int x, int v) {
+    t[x].r = v;
+    cr = cid == x ? v : cr;
+  }
+  __device__ __forceinline__ void sP(int x, int v) { t[x].p = v; }
+  __device__ __forceinline__ void sC(int x, int v) { t[x].color = v; }
+  __device__ __forceinline__ uint32_t K(int x) const { return rb_uu(t[x].key); }
+  __device__ __forceinline__ float F(int x) const { return rb_uf(t[x].f); }
+  __device__ __forceinline__ Quad quad_at(int x, int depth) {
+    const uint64_t m = __ballot(cid == x);
+    Quad q;
+    if (m) {
+      const int h = (int)__ffsll((unsigned long long)m) - 1;
+      q.key = (uint32_t)__builtin_amdgcn_readlane((int)ck, h);
+      q.f = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), h));
+      q.l = __builtin_amdgcn_readlane(cl, h);
+      q.r = __builtin_amdgcn_readlane(cr, h);
+      return q;
+    }
+    q = rb_quad(t, x);
+    int slot = depth;
+    if (depth >= 32) {
+      slot = 32 + (rr & 31);
+      rr = rr + 1;
+    }
+    if (lane == slot) {
+      cid = x;
+      ck = q.key;
+      cf = q.f;
+      cl = q.l;
+      cr = q.r;
+    }
+    return q;
+  }
+  __device__ __forceinline__ Quad quad(int x) { return rb_quad(t, x); }
+  __device__ __forceinline__ void leaf(int x, int p) {
+    t[x].p = p;
+    t[x].l = NIL;
+    t[x].r = NIL;
+    t[x].color = RB_RED;
+    cl = cid == x ? NIL : cl;
+    cr = cid == x ? NIL : cr;
+  }
+  __device__ __forceinline__ void set_kf(int x, uint32_t key, float f) {
+    t[x].key = key;
+    t[x].f = f;
+    ck = cid == x ? key : ck;
+    cf = cid == x ? f : cf;
+  }
+};
+#endif
 
 // Pool allocator for tree nodes: bump pointer + intrusive free list through .l.
 struct PoolState {

@@ -41,4 +41,6 @@ for s in args.seeds:
                           cyc_per_apop_hbm=cyc[7] / max(modes["astar_pops_hbm"], 1),
                           lds_astar_per_apop={n: round(cyc[8 + i] / max(st["astar_pops"] - modes["astar_pops_hbm"], 1))
                                               for i, n in enumerate(["pop_probe", "find", "insert", "unlink_hit",
-                                                                     "memoise"])})))
+                                                                     "memoise"])},
+                          outer_per_pop={n: round(cyc[13 + i] / max(st["pops"], 1))
+                                         for i, n in enumerate(["find3", "insert3", "unlink3"])})))
