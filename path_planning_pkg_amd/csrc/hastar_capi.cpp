@@ -310,6 +310,7 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   if (p->num_steering < 1 || p->num_steering > 16 || !p->steering || !p->curvature_weights)
     return fail(HASTAR_EINVAL, "num_steering must be in [1, 16] with steering/curvature_weights arrays");
   if (p->num_actions < 0) return fail(HASTAR_EINVAL, "num_actions must be >= 0");
+  if (p->max_pops > (int)SLOT3_IDX_MASK - 1) return fail(HASTAR_EINVAL, "max_pops must be below 2^20 - 1");
   if (!(p->grid_resolution > 0) || !(p->step_size > 0)) return fail(HASTAR_EINVAL, "resolution/step must be > 0");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -388,7 +389,11 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   const size_t NN = (size_t)N * N;
   h->max_pops = p->max_pops > 0 ? p->max_pops : 262144;
   ArenaReq& R = h->areq;
-  R.open3 = 3 * h->max_pops + 64;
+  // live open nodes: each pop removes one and adds at most `span` successors (a
+  // replacement erases before it inserts), so after max_pops pops at most
+  // 1 + max_pops * (span - 1) are live; freed nodes are reused before the pool grows
+  const int span = std::max(2, std::min(2 * D.na + 1, D.nsteer));
+  R.open3 = 2 + (span - 1) * h->max_pops + 64;
   R.closed3 = h->max_pops + 1;
   R.slots = 1;
   while (R.slots < 2u * (uint32_t)h->max_pops + 64) R.slots <<= 1;
@@ -1024,7 +1029,7 @@ int hastar_debug_motion(hastar_handle h, float* off, float* dth, float* cost, fl
 
 int hastar_debug_cycles(hastar_handle h, unsigned long long* out8) {
   if (!h || !h->have_last) return fail(HASTAR_EINVAL, "no search result");
-  for (int q = 0; q < 16; ++q) out8[q] = h->last.cycles[q];
+  for (int q = 0; q < NSTAMP; ++q) out8[q] = h->last.cycles[q];
   return HASTAR_OK;
 }
 

@@ -22,7 +22,9 @@ constexpr int MAXS = 16;   // max steering actions (checked at create)
 
 // Diagnostic build only (-DHASTAR_STAMPS): cycles per phase of the search loop,
 // 0 pop+closed insert, 1 successors+APF+Dubins, 2 open/closed bookkeeping, 3 holonomic A*,
-// 4 Dubins shot, 5 reconstruct+stats, 6 whole loop.
+// 4 Dubins shot, 5 reconstruct+stats, 6 whole loop, 7 A* in HBM mode, 8-12 LDS A* pop /
+// find / insert / unlink-hit / memoise, 13-15 outer find / insert / unlink, 16-18 successor
+// generation / APF / Dubins lengths, 19-20 outer insert walk / link.
 #ifdef HASTAR_STAMPS
 #define STAMP_T unsigned long long
 #define STAMP_NOW() __builtin_amdgcn_s_memtime()
@@ -43,18 +45,19 @@ struct SearchCtx {
   const PlannerDev* __restrict__ P;   // planner descriptor in HBM (uniform, read-only: scalar loads)
   const SlotArena* __restrict__ A;    // this wave's search arena
   int lane;
-  RBT<CachedAcc<Node3>> o3;  // outer open tree: HBM nodes behind a register node cache
+  RBT<CachedAcc3> o3;        // outer open tree: HBM nodes behind a register node cache
   PoolState ps3, ps2;
   int n_closed3, n_closed2;
   uint32_t gen3, gen2;
   long long pops, succ, apops, asearch, shots, amigr, apops_g;
   int status;
 #ifdef HASTAR_STAMPS
-  unsigned long long cyc[16];
+  unsigned long long cyc[NSTAMP];
 #endif
 };
 
 // ---------------------------------------------------------------- closed sets --------
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t slot_hash(uint32_t k) {
   k ^= k >> 16;
   k *= 0x7feb352du;
@@ -64,32 +67,36 @@ __device__ __forceinline__ uint32_t slot_hash(uint32_t k) {
   return k;
 }
 
-// unordered_set<Node3D>::insert(*it).first (HybridAStar.cpp:110): existing record or a new
-// copy of the popped open node.
-__device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n) {
+// unordered_set<Node3D>::insert(*it).first (HybridAStar.cpp:110): the existing record of
+// the popped node's key, or a new copy of the popped open node.  *fresh tells which.
+__device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n, bool* fresh) {
   const SlotArena& A = *c.A;
   uint32_t h = slot_hash(n.key) & A.slots3_mask;
+  const uint32_t gbits = (c.gen3 & SLOT3_GEN_MASK) << SLOT3_IDX_BITS;
   for (;;) {
-    auto s = &gp(A.slots3)[h];
-    if (s->gen != c.gen3) {
+    GAS v2u* s = (GAS v2u*)&gp(A.slots3)[h];
+    const v2u sv = *s;  // {key, gi}
+    if ((sv.y & ~SLOT3_IDX_MASK) != gbits) {
+      *fresh = true;
       if (c.n_closed3 >= A.closed3_cap) return NIL;
       const int idx = c.n_closed3++;
-      auto r = &gp(A.closed3)[idx];
-      r->key = n.key;
-      r->g = n.g;
-      r->f = n.f;
-      r->vmin = n.vmin;
-      r->x = n.x;
-      r->y = n.y;
-      r->h = n.h;
-      r->ci = n.ci;
-      r->prev = n.prev;
-      s->key = n.key;
-      s->idx = idx;
-      s->gen = c.gen3;
+      Closed3 r;
+      r.key = n.key;
+      r.g = n.g;
+      r.vmin = n.vmin;
+      r.prev = n.prev;
+      r.x = n.x;
+      r.y = n.y;
+      r.h = n.h;
+      r.ci = (int)(n.cc >> 8);
+      gstore(&gp(A.closed3)[idx], r);
+      *s = v2u{n.key, gbits | (uint32_t)idx};
       return idx;
     }
-    if (s->key == n.key) return s->idx;
+    if (sv.x == n.key) {
+      *fresh = false;
+      return (int)(sv.y & SLOT3_IDX_MASK);
+    }
     h = (h + 1) & A.slots3_mask;
   }
 }
@@ -97,11 +104,27 @@ __device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n) {
 __device__ __forceinline__ bool closed3_contains(const SearchCtx& c, uint32_t key) {
   const SlotArena& A = *c.A;
   uint32_t h = slot_hash(key) & A.slots3_mask;
+  const uint32_t gbits = (c.gen3 & SLOT3_GEN_MASK) << SLOT3_IDX_BITS;
   for (;;) {
-    const Slot3 s = gload(&gp(A.slots3)[h]);
-    if (s.gen != c.gen3) return false;
-    if (s.key == key) return true;
+    const v2u s = *(const GAS v2u*)&gp(A.slots3)[h];  // {key, gi}
+    if ((s.y & ~SLOT3_IDX_MASK) != gbits) return false;
+    if (s.x == key) return true;
     h = (h + 1) & A.slots3_mask;
+  }
+}
+
+// next closed-set generation of this slot; when the 12-bit generation wraps, the wave
+// zeroes its hash table (every 4095 searches)
+__device__ __forceinline__ void closed3_next_gen(SearchCtx& c) {
+  c.gen3 = (c.gen3 + 1) & SLOT3_GEN_MASK;
+  if (c.gen3 == 0) {
+    const SlotArena& A = *c.A;
+    typedef int v4 __attribute__((ext_vector_type(4)));
+    GAS v4* t = (GAS v4*)gp(A.slots3);
+    const size_t n4 = ((size_t)A.slots3_mask + 1) / 2;  // two 8-B slots per 16-B store
+    for (size_t i = c.lane; i < n4; i += 64) t[i] = v4{0, 0, 0, 0};
+    wave_lds_sync();
+    c.gen3 = 1;
   }
 }
 
@@ -138,6 +161,7 @@ __device__ __forceinline__ LAS T* lp(T* p) {
 
 // compact LDS layout for RBT<>: {key, f, g, l|r} (16 B) + {p, color} (4 B), prev in HBM
 struct LdsAcc {
+  static constexpr bool kPathWalk = false;
   LAS NodeA2* a;
   LAS NodeB2* b;
   GAS int* pv;
@@ -785,20 +809,30 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
 __device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, int prev) {
   bool left;
   const uint32_t key = key3(s.cx, s.cy, s.bin);
+  STAMP_T tw = STAMP_NOW();
   const int pos = c.o3.insert_pos(key, f, &left);
+  STAMP_ADD(19, tw);
   if (pos == -2) return true;
   const int n = tpool_alloc(c.o3, c.ps3, c.A->open3_cap);
   if (n == NIL) return false;
-  auto d = &gp(c.A->open3)[n];
-  c.o3.set_kf(n, key, f);
-  d->g = s.g;
-  d->vmin = s.vmin;
-  d->x = s.x;
-  d->y = s.y;
-  d->h = s.h;
-  d->ci = s.ci;
-  d->prev = prev;
+  Node3 d;
+  d.key = key;
+  d.f = f;
+  d.l = NIL;
+  d.r = NIL;
+  d.p = pos;
+  d.cc = (uint32_t)RB_RED | ((uint32_t)s.ci << 8);
+  d.g = s.g;
+  d.vmin = s.vmin;
+  d.x = s.x;
+  d.y = s.y;
+  d.h = s.h;
+  d.prev = prev;
+  gstore(&gp(c.A->open3)[n], d);
+  c.o3.fresh(n, key, f, NIL, NIL, pos, RB_RED);
+  STAMP_T tl = STAMP_NOW();
   c.o3.link(left, n, pos);
+  STAMP_ADD(20, tl);
   return true;
 }
 
@@ -810,7 +844,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
   const SlotArena& A = *c.A;
   const int lane = c.lane;
 #ifdef HASTAR_STAMPS
-  for (int q = 0; q < 16; ++q) c.cyc[q] = 0;
+  for (int q = 0; q < NSTAMP; ++q) c.cyc[q] = 0;
 #endif
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   ApfRegs apr;
@@ -818,7 +852,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
   c.o3.t = gp(A.open3);
   c.o3.lane = lane;
   c.o3.reset_cache();
-  c.gen3 += 1;
+  closed3_next_gen(c);
   c.n_closed3 = 0;
   c.n_closed2 = 0;
   c.pops = c.succ = c.apops = c.asearch = c.shots = c.amigr = c.apops_g = 0;
@@ -857,12 +891,26 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
     STAMP_T tp = STAMP_NOW();
     const int b = c.o3.begin();
     const Node3 top = gload(&gp(A.open3)[b]);
-    const int ci = closed3_insert(c, top);
+    bool fresh;
+    const int ci = closed3_insert(c, top, &fresh);
     if (ci == NIL) { c.status = -75; break; }
+    // a duplicate key expands the OLD record; a new record is the popped node itself
+    Closed3 cur;
+    if (fresh) {
+      cur.key = top.key;
+      cur.g = top.g;
+      cur.vmin = top.vmin;
+      cur.prev = top.prev;
+      cur.x = top.x;
+      cur.y = top.y;
+      cur.h = top.h;
+      cur.ci = (int)(top.cc >> 8);
+    } else {
+      cur = gload(&gp(A.closed3)[ci]);
+    }
     c.o3.unlink(b);
     tpool_free(c.o3, c.ps3, b);
     c.pops++;
-    const Closed3 cur = gload(&gp(A.closed3)[ci]);
     const int cx = key3_x(cur.key), cy = key3_y(cur.key), cbin = key3_bin(cur.key);
     dig = mix64(dig ^ digest_key(cur.key)) + (uint64_t)fbits(cur.g);
     STAMP_ADD(0, tp);
@@ -938,6 +986,8 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
       if (keep) sl[__popcll(km & ((1ull << lane) - 1))] = s;
     }
     wave_lds_sync();
+    STAMP_ADD(16, tx);
+    STAMP_T tapf = STAMP_NOW();
     c.succ += ns;
     // APF field of every kept successor (lanes over obstacles)
     for (int q = 0; q < ns; ++q) {
@@ -946,6 +996,8 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
       if (lane == 0) sl[q].g = sl[q].g + fc;
       wave_lds_sync();
     }
+    STAMP_ADD(17, tapf);
+    STAMP_T tdub = STAMP_NOW();
     // Dubins lengths: lane = 4 * successor + word
     {
       const int q = lane >> 2, w = lane & 3;
@@ -965,6 +1017,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
       }
     }
     wave_lds_sync();
+    STAMP_ADD(18, tdub);
     STAMP_ADD(1, tx);
     // ---- HybridAStar.cpp:159-193
     STAMP_T tb = STAMP_NOW();
@@ -982,7 +1035,18 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
       const uint32_t key = key3(s.cx, s.cy, s.bin);
       if ((closed_m >> q) & 1ull) continue;
       STAMP_T tf3 = STAMP_NOW();
-      const int hit = c.o3.find(key, s.g);  // f == g before the heuristic is added
+      // std::set::find with f == g (the heuristic is not added yet).  The tree's in-order
+      // f sequence is strictly increasing, so when g <= f(leftmost) the lower_bound
+      // predicate (key != k && f < g) is false at every node: the walk ends at the
+      // leftmost node whatever the shape, and it matches iff its key is k or f == g.
+      int hit;
+      {
+        const int lm = c.o3.begin();
+        const float lf = lm != 0 ? c.o3.F(lm) : 0.0f;
+        if (lm == 0) hit = 0;
+        else if (s.g <= lf) hit = (c.o3.K(lm) == key || s.g >= lf) ? lm : 0;
+        else hit = c.o3.find(key, s.g);
+      }
       STAMP_ADD(13, tf3);
       if (hit == 0) {
         STAMP_T ta = STAMP_NOW();
@@ -1093,9 +1157,9 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
     R->t_end = __builtin_amdgcn_s_memrealtime();
     R->slot = (int)blockIdx.x;
 #ifdef HASTAR_STAMPS
-    for (int q = 0; q < 16; ++q) R->cycles[q] = c.cyc[q];
+    for (int q = 0; q < NSTAMP; ++q) R->cycles[q] = c.cyc[q];
 #else
-    for (int q = 0; q < 16; ++q) R->cycles[q] = 0;
+    for (int q = 0; q < NSTAMP; ++q) R->cycles[q] = 0;
 #endif
   }
   wave_lds_sync();

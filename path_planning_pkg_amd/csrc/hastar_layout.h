@@ -14,33 +14,35 @@ constexpr int NIL = -1;
 constexpr int RB_RED = 0;
 constexpr int RB_BLACK = 1;
 
-// Open-set (std::set<Node3D<float>>, HybridAStar.h:72) tree node.  Index 0 of the pool
-// is the libstdc++ header: p = root, l = leftmost, r = rightmost, color = red.
-// key = cell x << 20 | cell y << 8 | angle bin  (Node3D::operator!=, Node3D.h:44-47).
+// Open-set (std::set<Node3D<float>>, HybridAStar.h:72) tree node, 48 B = three 16-B
+// quads.  Index 0 of the pool is the libstdc++ header: p = root, l = leftmost,
+// r = rightmost, color = red.  key = cell x << 20 | cell y << 8 | angle bin
+// (Node3D::operator!=, Node3D.h:44-47).  The RB color lives in byte 0 of `cc` (written
+// with byte stores, so rebalancing never rewrites ci) and the curvature index in byte 1.
 struct alignas(16) Node3 {
   uint32_t key;           // (x, y, bin)
   float f;                // _cost_f: the comparator's order key
   int l, r;               // tree links (pool indices, NIL = null): {key, f, l, r} = one 16-B load per walk step
-  int p, color;
+  int p;                  // parent link
+  uint32_t cc;            // color (byte 0) | _curvature_index << 8
   float g;                // _cost_g
   float vmin;             // _vmin_sqr
   float x, y, h;          // _pose2D (grid frame)
-  int ci;                 // _curvature_index
   int prev;               // closed-record index of the predecessor (NIL for the start)
-  int pad0, pad1;
 };
+static_assert(sizeof(Node3) == 48, "Node3 is three quads");
 
 // Closed-set record (unordered_set<Node3D>, HybridAStar.h:73-74): a copy of the popped
-// open node.  Records never move, so prev links stay valid like the reference's
-// pointers into the node-based hash set.
+// open node (its f is never read again).  Records never move, so prev links stay valid
+// like the reference's pointers into the node-based hash set.
 struct alignas(16) Closed3 {
   uint32_t key;
-  float g, f, vmin;
+  float g, vmin;
+  int prev;
   float x, y, h;
   int ci;
-  int prev;
-  int pad0, pad1, pad2;
 };
+static_assert(sizeof(Closed3) == 32, "Closed3 is two quads");
 
 // Holonomic A* open-set node (std::set<Node2D<float>>, AStar.h:70).
 // key = x << 16 | y (Node2D::operator!=, Node2D.h:35-38).
@@ -72,13 +74,19 @@ struct alignas(16) Cell2 {
   uint32_t oinfo;
 };
 
-// Closed-set hash slot (open addressing; generation-stamped so clear() is O(1)).
+// Closed-set hash slot (open addressing).  gi = generation (12 bits) << 20 | record
+// index; a slot is live iff its generation is the search's, so clear() is O(1).  The
+// generation cycles through 1..4095; when it wraps the wave zeroes its table.
 struct Slot3 {
-  uint32_t gen;
   uint32_t key;
-  int idx;
-  int pad;
+  uint32_t gi;
 };
+constexpr int SLOT3_IDX_BITS = 20;
+constexpr uint32_t SLOT3_IDX_MASK = (1u << SLOT3_IDX_BITS) - 1;
+constexpr uint32_t SLOT3_GEN_MASK = 0xfffu;
+
+// diagnostic phase counters of the search kernel (-DHASTAR_STAMPS)
+constexpr int NSTAMP = 24;
 
 // Per-search result block (written by the search kernel, read by the host).
 struct SearchResult {
@@ -89,7 +97,7 @@ struct SearchResult {
   int terminal;           // closed record index the path is rebuilt from
   int dubins_len;         // samples of the successful shot
   int astar_migrations;   // inner A* searches that outgrew LDS
-  unsigned long long cycles[16]; // diagnostic build (-DHASTAR_STAMPS): s_memtime per phase
+  unsigned long long cycles[NSTAMP]; // diagnostic build (-DHASTAR_STAMPS): s_memtime per phase
   unsigned long long t_start, t_end;  // s_memrealtime (100 MHz, chip-wide) around the search
   int slot, pad_r;                    // slot (wavefront) that ran it
 };

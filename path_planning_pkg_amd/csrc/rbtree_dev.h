@@ -78,6 +78,7 @@ RB_HD Quad rb_quad(PtrT t, int x) {
 // Node2; 32-bit links) and on the compact LDS nodes of the inner A* (16-bit links).
 template <class NodeT, class PtrT = NodeT*>
 struct AosAcc {
+  static constexpr bool kPathWalk = false;
   PtrT t;
   RB_HD int L(int x) const { return rb_ui(t[x].l); }
   RB_HD int R(int x) const { return rb_ui(t[x].r); }
@@ -172,6 +173,11 @@ struct RBT : Acc {
     int y = 0, x = P(0), depth = 0;
     uint32_t yk = 0;
     float yf = 0.0f;
+    if constexpr (Acc::kPathWalk) {
+      bool unused;
+      this->path_walk(k, f, false, &y, &yk, &yf, &unused);
+      x = NIL;
+    }
     while (x != NIL) {
       const Quad q = this->quad_at(x, depth++);
       if (!rb_less(q.key, q.f, k, f)) {
@@ -194,6 +200,10 @@ struct RBT : Acc {
     bool comp = true;
     uint32_t yk = 0;
     float yf = 0.0f;
+    if constexpr (Acc::kPathWalk) {
+      this->path_walk(k, f, true, &y, &yk, &yf, &comp);
+      x = NIL;
+    }
     while (x != NIL) {
       const Quad q = this->quad_at(x, depth++);
       y = x;
@@ -392,31 +402,101 @@ template <class NodeT, class PtrT = NodeT*>
 using RBTree = RBT<AosAcc<NodeT, PtrT>>;
 
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
-// HBM nodes behind a 64-entry, fully associative, write-through node cache held in the
-// wavefront's registers (lane i caches one node: id, key, f, l, r, p, color).  A tree
-// walk step that hits costs a ballot and a few lane reads instead of a dependent HBM
-// round trip.  Walk steps at depth d < 32 fill lane d (the top of the tree stays
-// resident); other misses fill lanes 32..63 round-robin.  Every link/key write goes to
-// HBM and to any lane caching that node, so the cache is never stale; it is reset when
-// the arena starts a new search.
-template <class NodeT>
-struct CachedAcc {
-  __attribute__((address_space(1))) NodeT* t;
+// Outer open tree: Node3 records in HBM behind a 64-entry, fully associative,
+// write-through node cache held in the wavefront's registers.  Lane i caches the whole
+// tree part of one node (id, key, f, l, r, p, color), so every accessor the libstdc++
+// algorithms use (walks, link/rebalance, erase/rebalance, the pool's free list) costs a
+// ballot and one lane read on a hit instead of a dependent HBM round trip.  A miss loads
+// the node's first two quads (one round trip) and fills a lane.  Lanes 0..PATH-1 hold the
+// root-to-leaf path of the last walk (lane d = the node at depth d), the header lives in
+// lane 63, other misses rotate through lanes PATH..62.  Every tree write goes to HBM and
+// to every lane caching that node, so the cache is never stale.
+//
+// Path walks: a new walk follows the cached path for as long as its own branch decision
+// at depth d leads to the cached node at depth d + 1.  Every path lane evaluates that
+// decision on its own node at once, so the shared prefix costs one ballot instead of a
+// chain of dependent steps; the walk continues step by step only below the point where
+// it leaves the cached path (consecutive inserts of similar f share most of it).
+// All calls are wave-uniform.
+struct CachedAcc3 {
+  static constexpr bool kPathWalk = true;
+  static constexpr int PATH = 48;
+  __attribute__((address_space(1))) Node3* t;
   int lane;
-  int cid;      // this lane's cached node (walk steps only: key, f, l, r)
+  int cid;      // this lane's cached node (-1: empty)
   uint32_t ck;
   float cf;
-  int cl, cr;
-  int rr;
+  int cl, cr, cp, cc;
+  int rr;       // round-robin victim counter (wave-uniform)
+  int plen;     // lanes [0, plen) hold the last walk's path (wave-uniform)
 
   __device__ __forceinline__ void reset_cache() {
     cid = -1;
     rr = 0;
+    plen = 0;
   }
-  __device__ __forceinline__ int L(int x) const { return rb_ui(t[x].l); }
-  __device__ __forceinline__ int R(int x) const { return rb_ui(t[x].r); }
-  __device__ __forceinline__ int P(int x) const { return rb_ui(t[x].p); }
-  __device__ __forceinline__ int C(int x) const { return rb_ui(t[x].color); }
+  __device__ __forceinline__ int hit(int x) const {
+    const uint64_t m = __ballot(cid == x);
+    return m ? (int)__ffsll((unsigned long long)m) - 1 : -1;
+  }
+  __device__ __forceinline__ int victim(int x) {
+    if (x == 0) return 63;
+    const int v = PATH + rr;
+    rr = rr == 62 - PATH ? 0 : rr + 1;
+    return v;
+  }
+  struct Full {
+    uint32_t key;
+    float f;
+    int l, r, p, c;
+  };
+  // one round trip: quads 0 and 1 of node x; cached in lane `slot`
+  __device__ __forceinline__ Full fill(int x, int slot) {
+    typedef int v4 __attribute__((ext_vector_type(4)));
+    const __attribute__((address_space(1))) v4* q = (const __attribute__((address_space(1))) v4*)&t[x];
+    const v4 a = q[0], b = q[1];
+    Full n;
+    n.key = rb_uu((uint32_t)a.x);
+    n.f = __int_as_float(rb_ui(a.y));
+    n.l = rb_ui(a.z);
+    n.r = rb_ui(a.w);
+    n.p = rb_ui(b.x);
+    n.c = rb_ui(b.y) & 0xff;
+    if (lane == slot) {
+      cid = x;
+      ck = n.key;
+      cf = n.f;
+      cl = n.l;
+      cr = n.r;
+      cp = n.p;
+      cc = n.c;
+    }
+    return n;
+  }
+  __device__ __forceinline__ int L(int x) {
+    const int h = hit(x);
+    return h >= 0 ? __builtin_amdgcn_readlane(cl, h) : fill(x, victim(x)).l;
+  }
+  __device__ __forceinline__ int R(int x) {
+    const int h = hit(x);
+    return h >= 0 ? __builtin_amdgcn_readlane(cr, h) : fill(x, victim(x)).r;
+  }
+  __device__ __forceinline__ int P(int x) {
+    const int h = hit(x);
+    return h >= 0 ? __builtin_amdgcn_readlane(cp, h) : fill(x, victim(x)).p;
+  }
+  __device__ __forceinline__ int C(int x) {
+    const int h = hit(x);
+    return h >= 0 ? __builtin_amdgcn_readlane(cc, h) : fill(x, victim(x)).c;
+  }
+  __device__ __forceinline__ uint32_t K(int x) {
+    const int h = hit(x);
+    return h >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)ck, h) : fill(x, victim(x)).key;
+  }
+  __device__ __forceinline__ float F(int x) {
+    const int h = hit(x);
+    return h >= 0 ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), h)) : fill(x, victim(x)).f;
+  }
   __device__ __forceinline__ void sL(int x, int v) {
     t[x].l = v;
     cl = cid == x ? v : cl;
@@ -425,51 +505,120 @@ struct CachedAcc {
     t[x].r = v;
     cr = cid == x ? v : cr;
   }
-  __device__ __forceinline__ void sP(int x, int v) { t[x].p = v; }
-  __device__ __forceinline__ void sC(int x, int v) { t[x].color = v; }
-  __device__ __forceinline__ uint32_t K(int x) const { return rb_uu(t[x].key); }
-  __device__ __forceinline__ float F(int x) const { return rb_uf(t[x].f); }
+  __device__ __forceinline__ void sP(int x, int v) {
+    t[x].p = v;
+    cp = cid == x ? v : cp;
+  }
+  __device__ __forceinline__ void sC(int x, int v) {
+    *(__attribute__((address_space(1))) uint8_t*)&t[x].cc = (uint8_t)v;  // byte 0 only: ci stays
+    cc = cid == x ? v : cc;
+  }
+  // the walk step at `depth`: node x, kept in path lane `depth` (copied there on a hit
+  // in another lane)
   __device__ __forceinline__ Quad quad_at(int x, int depth) {
-    const uint64_t m = __ballot(cid == x);
+    const int h = hit(x);
     Quad q;
-    if (m) {
-      const int h = (int)__ffsll((unsigned long long)m) - 1;
+    if (h >= 0) {
       q.key = (uint32_t)__builtin_amdgcn_readlane((int)ck, h);
       q.f = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), h));
       q.l = __builtin_amdgcn_readlane(cl, h);
       q.r = __builtin_amdgcn_readlane(cr, h);
+      if (depth < PATH && h != depth) {
+        const int p = __builtin_amdgcn_readlane(cp, h), c = __builtin_amdgcn_readlane(cc, h);
+        if (lane == depth) {
+          cid = x;
+          ck = q.key;
+          cf = q.f;
+          cl = q.l;
+          cr = q.r;
+          cp = p;
+          cc = c;
+        }
+      }
       return q;
     }
-    q = rb_quad(t, x);
-    int slot = depth;
-    if (depth >= 32) {
-      slot = 32 + (rr & 31);
-      rr = rr + 1;
-    }
-    if (lane == slot) {
-      cid = x;
-      ck = q.key;
-      cf = q.f;
-      cl = q.l;
-      cr = q.r;
-    }
+    const Full n = fill(x, depth < PATH ? depth : victim(x));
+    q.key = n.key;
+    q.f = n.f;
+    q.l = n.l;
+    q.r = n.r;
     return q;
   }
-  __device__ __forceinline__ Quad quad(int x) { return rb_quad(t, x); }
-  __device__ __forceinline__ void leaf(int x, int p) {
-    t[x].p = p;
-    t[x].l = NIL;
-    t[x].r = NIL;
-    t[x].color = RB_RED;
-    cl = cid == x ? NIL : cl;
-    cr = cid == x ? NIL : cr;
+
+  // The walks of std::set::find (ins = false: go left iff !(node < probe), remember the
+  // last node where it went left) and _M_get_insert_unique_pos (ins = true: go left iff
+  // probe < node, remember the last node and the last decision), comparator
+  // (ka != kb) && (fa < fb).  Outputs as RBT::find / RBT::insert_pos expect them.
+  __device__ __forceinline__ void path_walk(uint32_t k, float f, bool ins, int* y_, uint32_t* yk_, float* yf_,
+                                            bool* comp_) {
+    int y = 0, depth = 0;
+    uint32_t yk = 0;
+    float yf = 0.0f;
+    bool comp = true;
+    int x = P(0);
+    if (x != NIL && plen > 0 && __builtin_amdgcn_readlane(cid, 0) == x) {
+      const bool inpath = lane < plen;
+      const bool left = ins ? rb_less(k, f, ck, cf) : !rb_less(ck, cf, k, f);
+      const int child = left ? cl : cr;
+      const int nxt = __shfl_down(cid, 1, 64);
+      const bool cont = inpath && lane + 1 < plen && child == nxt;
+      const uint64_t stop = __ballot(!cont);
+      const int D = (int)__ffsll((unsigned long long)stop) - 1;  // node D is on the path; leave it via child
+      const uint64_t lmask = __ballot(inpath && left) & (D >= 63 ? ~0ull : ((2ull << D) - 1));
+      if (ins) {
+        y = __builtin_amdgcn_readlane(cid, D);
+        yk = (uint32_t)__builtin_amdgcn_readlane((int)ck, D);
+        yf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), D));
+        comp = (lmask >> D) & 1ull;
+      } else if (lmask) {
+        const int h = 63 - __builtin_clzll(lmask);
+        y = __builtin_amdgcn_readlane(cid, h);
+        yk = (uint32_t)__builtin_amdgcn_readlane((int)ck, h);
+        yf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), h));
+      }
+      x = __builtin_amdgcn_readlane(child, D);
+      depth = D + 1;
+    }
+    while (x != NIL) {
+      const Quad q = quad_at(x, depth++);
+      if (ins) {
+        y = x;
+        yk = q.key;
+        yf = q.f;
+        comp = rb_less(k, f, q.key, q.f);
+        x = comp ? q.l : q.r;
+      } else if (!rb_less(q.key, q.f, k, f)) {
+        y = x;
+        yk = q.key;
+        yf = q.f;
+        x = q.l;
+      } else {
+        x = q.r;
+      }
+    }
+    plen = depth < PATH ? depth : PATH;
+    *y_ = y;
+    *yk_ = yk;
+    *yf_ = yf;
+    *comp_ = comp;
   }
-  __device__ __forceinline__ void set_kf(int x, uint32_t key, float f) {
-    t[x].key = key;
-    t[x].f = f;
-    ck = cid == x ? key : ck;
-    cf = cid == x ? f : cf;
+  // a node just written in full by the caller (pool allocation): drop stale copies of
+  // the index and cache the new contents (no HBM traffic)
+  __device__ __forceinline__ void fresh(int x, uint32_t key, float f, int l, int r, int p, int c) {
+    cid = cid == x ? -1 : cid;
+    const int slot = victim(x);
+    if (lane == slot) {
+      cid = x;
+      ck = key;
+      cf = f;
+      cl = l;
+      cr = r;
+      cp = p;
+      cc = c;
+    }
   }
+  // RBT::link's first step: the caller has already stored the leaf fields with the node
+  __device__ __forceinline__ void leaf(int, int) {}
 };
 #endif
 

@@ -184,7 +184,7 @@ class HybridAStar:
         return out[:min(n, cap)].copy()
 
     def cycles(self):
-        out = (C.c_ulonglong * 16)()
+        out = (C.c_ulonglong * 24)()
         _check(load_library().hastar_debug_cycles(self.h, out))
         return list(out)
 

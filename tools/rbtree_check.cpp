@@ -25,8 +25,8 @@ int main(int argc, char** argv) {
     const int keyspace = 8 + (int)(rng() % 200);
     const int fspace = 2 + (int)(rng() % 40);
     std::set<E, Less> ref;
-    std::vector<Node3> pool(ops + 2);
-    RBTree<Node3> tr{{pool.data()}};
+    std::vector<Node2> pool(ops + 2);
+    RBTree<Node2> tr{{pool.data()}};
     tr.clear();
     PoolState ps{1, NIL};
     std::vector<int> id_of_node(ops + 2, -1);
