@@ -34,6 +34,8 @@ int hastar_debug_astar_modes(hastar_handle h, long long* out2);
 /* Timing of the last search: {t_start, t_end} in s_memrealtime ticks (100 MHz, chip-wide
  * clock) and the slot (persistent wavefront) that ran it. */
 int hastar_debug_timing(hastar_handle h, unsigned long long* out3);
+/* Search-slot pool of the handle's device: {resident wavefronts, search waves per CU, arenas, MiB per arena}. */
+int hastar_debug_slots(hastar_handle h, long long* out4);
 
 #ifdef __cplusplus
 }

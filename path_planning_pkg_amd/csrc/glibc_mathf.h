@@ -49,37 +49,25 @@ GM_HD uint64_t dbits(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
 GM_HD double bitsd(uint64_t u) { double x; memcpy(&x, &u, 8); return x; }
 
 // ---------------------------------------------------------------- sinf / cosf --
-// sincos_t layout as compiled into glibc 2.35: sign[4], hpi_inv, hpi,
-// c0, c1, s1, c2, s2, c3, s3, c4 (two copies; table 1 negates the cosine terms).
-struct SinCosTab { double sign[4]; double hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4; };
-
-#define GM_SINCOS_TAB_INIT                                                                      \
-  {{{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,                        \
-    0x1.0p+0, -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,               \
-    0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16}, \
-   {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,                        \
-    -0x1.0p+0, 0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5,              \
-    0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16}}
+// glibc's sincos_t (sincosf.h) comes in two copies: the sine coefficients are identical,
+// copy 1 negates every cosine coefficient, and sign[4] = {1, -1, -1, 1}.  fma() and the
+// double -> float conversion round symmetrically, so the copy-1 cosine polynomial is
+// exactly the negated copy-0 one, and sign[] only negates x (exact).  The polynomials
+// below therefore take the copy-0 constants as immediates and never index a table (a
+// per-lane table index would be a vector memory load on the GPU).
+//   copy 0: hpi_inv 0x1.45f306dc9c883p+23, hpi 0x1.921fb54442d18p+0, c0 1, c1 -0x1.ffffffd0c621cp-2,
+//   s1 -0x1.555545995a603p-3, c2 0x1.55553e1068f19p-5, s2 0x1.1107605230bc4p-7,
+//   c3 -0x1.6c087e89a359dp-10, s3 -0x1.994eb3774cf24p-13, c4 0x1.99343027bf8c3p-16.
 #define GM_INV_PIO4_INIT                                                                        \
   {0xa2u, 0xa2f9u, 0xa2f983u, 0xa2f9836eu, 0xf9836e4eu, 0x836e4e44u, 0x6e4e4415u, 0x4e441529u,  \
    0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u, 0x2757d1f5u, 0x57d1f534u, 0xd1f534ddu,    \
    0xf534ddc0u, 0x34ddc0dbu, 0xddc0db62u, 0xc0db6295u, 0xdb629599u, 0x6295993cu, 0x95993c43u,    \
    0x993c4390u, 0x3c439041u}
 
-static const SinCosTab kSinCosHost[2] = GM_SINCOS_TAB_INIT;
 static const uint32_t kInvPio4Host[24] = GM_INV_PIO4_INIT;
 #if defined(__HIPCC__)
-__constant__ SinCosTab kSinCosDev[2] = GM_SINCOS_TAB_INIT;
 __constant__ uint32_t kInvPio4Dev[24] = GM_INV_PIO4_INIT;
 #endif
-
-GM_HD const SinCosTab& sincos_tab(int which) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return kSinCosDev[which];
-#else
-  return kSinCosHost[which];
-#endif
-}
 
 GM_HD uint32_t inv_pio4(int i) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -91,21 +79,23 @@ GM_HD uint32_t inv_pio4(int i) {
 
 GM_HD uint32_t abstop12(float x) { return (fbits(x) >> 20) & 0x7ffu; }
 
-// Odd/even polynomial of sinf_poly() with the FMA grouping of the -mfma build.
-GM_HD float sincos_poly(double x, double x2, const SinCosTab& p, int n) {
+// sinf_poly() with the FMA grouping of the -mfma build: odd (n even: sine) or even
+// (n odd: cosine) polynomial; tab1 selects copy 1 of the table.
+GM_HD float sincos_poly_t(double x, double x2, bool tab1, int n) {
   if ((n & 1) == 0) {
     double x3 = x * x2;
-    double s1 = fma(x2, p.s3, p.s2);
+    double s1 = fma(x2, -0x1.994eb3774cf24p-13, 0x1.1107605230bc4p-7);
     double x7 = x3 * x2;
-    double s = fma(x3, p.s1, x);
+    double s = fma(x3, -0x1.555545995a603p-3, x);
     return (float)fma(s1, x7, s);
   }
   double x4 = x2 * x2;
-  double c1 = fma(x2, p.c1, p.c0);
-  double c2 = fma(x2, p.c4, p.c3);
+  double c1 = fma(x2, -0x1.ffffffd0c621cp-2, 0x1.0p+0);
+  double c2 = fma(x2, 0x1.99343027bf8c3p-16, -0x1.6c087e89a359dp-10);
   double x6 = x4 * x2;
-  double c = fma(x4, p.c2, c1);
-  return (float)fma(c2, x6, c);
+  double c = fma(x4, 0x1.55553e1068f19p-5, c1);
+  const float v = (float)fma(c2, x6, c);
+  return tab1 ? -v : v;
 }
 
 // reduce_large(): Payne-Hanek style reduction for |y| >= 120, 64-bit integer exact.
@@ -126,69 +116,39 @@ GM_HD double reduce_large(uint32_t xi, int* np) {
 
 GM_HD float nan_of(float y) { return (y - y) / (y - y); }
 
-GM_HD float g_sinf(float y) {
+// sinf(y) (cosine = false) or cosf(y) (cosine = true): one code path for both, so a
+// wavefront whose lanes need different functions evaluates them in a single pass.
+// sinf and cosf differ only in the |y| < 2^-12 result and in which polynomial an odd
+// quadrant takes.
+GM_HD float g_sincosf_sel(float y, bool cosine) {
   double x = y;
   uint32_t t = abstop12(y);
   if (t < 0x3f4u) {                      // |y| < pi/4
     double s = x * x;
-    if (t < 0x398u) return y;            // |y| < 2^-12
-    return sincos_poly(x, s, sincos_tab(0), 0);
+    if (t < 0x398u) return cosine ? 1.0f : y;  // |y| < 2^-12
+    return sincos_poly_t(x, s, false, cosine ? 1 : 0);
   }
+  int n, ns;
+  double xr;
   if (t < 0x42fu) {                      // |y| < 120
-    const SinCosTab& t0 = sincos_tab(0);
-    double r = x * t0.hpi_inv;
-    int n = (((int32_t)r) + 0x800000) >> 24;
-    double xr = fma(-(double)n, t0.hpi, x);     // vfnmadd: x - n*hpi, one rounding
-    const SinCosTab& p = sincos_tab((n & 2) ? 1 : 0);
-    double x2 = xr * xr;
-    if (n & 1) return sincos_poly(xr, x2, p, 1);
-    return sincos_poly(xr * t0.sign[n & 3], x2, p, 0);
-  }
-  if (t < 0x7f8u) {
+    double r = x * 0x1.45f306dc9c883p+23;
+    n = (((int32_t)r) + 0x800000) >> 24;
+    xr = fma(-(double)n, 0x1.921fb54442d18p+0, x);  // vfnmadd: x - n*hpi, one rounding
+    ns = n;
+  } else if (t < 0x7f8u) {
     uint32_t xi = fbits(y);
-    int sign = (int)(xi >> 31);
-    int n;
-    double xr = reduce_large(xi, &n);
-    const SinCosTab& t0 = sincos_tab(0);
-    const SinCosTab& p = sincos_tab(((n + sign) & 2) ? 1 : 0);
-    double x2 = xr * xr;
-    if (n & 1) return sincos_poly(xr, x2, p, 1);
-    return sincos_poly(xr * t0.sign[(n + sign) & 3], x2, p, 0);
+    xr = reduce_large(xi, &n);
+    ns = n + (int)(xi >> 31);
+  } else {
+    return nan_of(y);
   }
-  return nan_of(y);
+  double x2 = xr * xr;
+  const bool tab1 = (ns & 2) != 0;
+  if (cosine ? ((n ^ 1) & 1) : (n & 1)) return sincos_poly_t(xr, x2, tab1, 1);
+  return sincos_poly_t(((ns + 1) & 2) ? -xr : xr, x2, tab1, 0);  // xr * sign[ns & 3]
 }
-
-GM_HD float g_cosf(float y) {
-  double x = y;
-  uint32_t t = abstop12(y);
-  if (t < 0x3f4u) {
-    double s = x * x;
-    if (t < 0x398u) return 1.0f;
-    return sincos_poly(x, s, sincos_tab(0), 1);
-  }
-  if (t < 0x42fu) {
-    const SinCosTab& t0 = sincos_tab(0);
-    double r = x * t0.hpi_inv;
-    int n = (((int32_t)r) + 0x800000) >> 24;
-    double xr = fma(-(double)n, t0.hpi, x);
-    const SinCosTab& p = sincos_tab((n & 2) ? 1 : 0);
-    double x2 = xr * xr;
-    if ((n ^ 1) & 1) return sincos_poly(xr, x2, p, 1);
-    return sincos_poly(xr * t0.sign[n & 3], x2, p, 0);
-  }
-  if (t < 0x7f8u) {
-    uint32_t xi = fbits(y);
-    int sign = (int)(xi >> 31);
-    int n;
-    double xr = reduce_large(xi, &n);
-    const SinCosTab& t0 = sincos_tab(0);
-    const SinCosTab& p = sincos_tab(((n + sign) & 2) ? 1 : 0);
-    double x2 = xr * xr;
-    if ((n ^ 1) & 1) return sincos_poly(xr, x2, p, 1);
-    return sincos_poly(xr * t0.sign[(n + sign) & 3], x2, p, 0);
-  }
-  return nan_of(y);
-}
+GM_HD float g_sinf(float y) { return g_sincosf_sel(y, false); }
+GM_HD float g_cosf(float y) { return g_sincosf_sel(y, true); }
 
 // ---------------------------------------------------------------- atanf -------
 GM_HD float g_atanf(float x) {

@@ -119,6 +119,7 @@ struct DeviceCtx {
   int fit_arenas = 1 << 30;     // pool size the memory budget allowed at the last build
   void* slab = nullptr;
   SlotArena* d_arenas = nullptr;
+  size_t arena_bytes = 0;       // bytes per arena of the current pool
   // batch buffers
   PlannerDev* d_descs = nullptr;
   int* d_order = nullptr;
@@ -245,6 +246,7 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
   HIPCHK(hipStreamSynchronize(D.stream));
   D.areq = r;
   D.n_arenas = n;
+  D.arena_bytes = per;
   D.fit_arenas = n < n_want ? n : (1 << 30);
   return 0;
 }
@@ -379,6 +381,11 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   }
   h->curv_abs.resize(ns);
   for (int i = 0; i < ns; ++i) h->curv_abs[i] = std::fabs(curv[i]);
+  // APF culling radius: a successor lies within max |offset| per axis of its parent (plus
+  // the rounding of parent + offset; the margin covers it many times over)
+  float max_off = 0.0f;
+  for (float v : off) max_off = std::max(max_off, std::fabs(v));
+  D.apf_reach = max_off * 1.001f + 0.01f;
   // Dubins radius (HybridAStar.cpp:22-24, tan_max HybridAStar.h:20-25)
   const float tmax = std::tan(*std::max_element(p->steering, p->steering + ns));
   D.r_min = p->wheelbase / (g_cosf(g_atan2f(p->rear_to_cg * tmax, p->wheelbase)) * tmax);
@@ -1038,6 +1045,18 @@ int hastar_debug_timing(hastar_handle h, unsigned long long* out3) {
   out3[0] = h->last.t_start;
   out3[1] = h->last.t_end;
   out3[2] = (unsigned long long)h->last.slot;
+  return HASTAR_OK;
+}
+
+// Search-slot pool of the handle's device: {resident wavefronts (occupancy x CUs), search
+// waves per CU, arenas in the pool, MiB per arena}.
+int hastar_debug_slots(hastar_handle h, long long* out4) {
+  if (!h || !h->dc) return fail(HASTAR_EINVAL, "bad handle");
+  const DeviceCtx& D = *h->dc;
+  out4[0] = D.resident_slots;
+  out4[1] = search_slots_per_cu();
+  out4[2] = D.n_arenas;
+  out4[3] = (long long)(D.arena_bytes >> 20);
   return HASTAR_OK;
 }
 

@@ -119,57 +119,89 @@ __device__ __forceinline__ float euclid_h(const PlannerDev& P, int i, int j) {
 // ------------------------------------------------------------- Dubins (Dubins.cpp) --
 struct Centres { float srx, sry, slx, sly, grx, gry, glx, gly; };
 
-// Dubins.cpp:19-32: circle centres of a start and a goal pose
-__device__ __forceinline__ Centres dubins_centres(float r, float sx, float sy, float sh, float gx, float gy,
-                                                  float gh) {
+// Dubins.cpp:19-32: circle centres of a start and a goal pose.  The goal half is the same
+// for every evaluation of one search, so it is computed once (GoalC).
+struct GoalC { float grx, gry, glx, gly; };
+__device__ __forceinline__ GoalC goal_centres(float r, float gx, float gy, float gh) {
+  const float sg = g_sinf(gh), cg = g_cosf(gh);
+  return GoalC{gx + r * sg, gy - r * cg, gx - r * sg, gy + r * cg};
+}
+// start half from sin/cos of the start heading
+__device__ __forceinline__ Centres centres_from(float r, float sx, float sy, float ss, float cs, const GoalC& G) {
   Centres c;
-  const float ss = g_sinf(sh), cs = g_cosf(sh), sg = g_sinf(gh), cg = g_cosf(gh);
   c.srx = sx + r * ss;
   c.sry = sy - r * cs;
   c.slx = sx - r * ss;
   c.sly = sy + r * cs;
-  c.grx = gx + r * sg;
-  c.gry = gy - r * cg;
-  c.glx = gx - r * sg;
-  c.gly = gy + r * cg;
+  c.grx = G.grx;
+  c.gry = G.gry;
+  c.glx = G.glx;
+  c.gly = G.gly;
   return c;
 }
+__device__ __forceinline__ Centres dubins_centres_g(float r, float sx, float sy, float sh, const GoalC& G) {
+  return centres_from(r, sx, sy, g_sinf(sh), g_cosf(sh), G);
+}
+__device__ __forceinline__ Centres dubins_centres(float r, float sx, float sy, float sh, float gx, float gy,
+                                                  float gh) {
+  return dubins_centres_g(r, sx, sy, sh, goal_centres(r, gx, gy, gh));
+}
 
-// Dubins.cpp:180-323 — length of CSC word w (0 RSR, 1 RSL, 2 LSR, 3 LSL) and its params.
-__device__ __forceinline__ float dubins_word(int w, float r, const Centres& C, float sh, float gh, float q[4]) {
-  const float csx = (w < 2) ? C.srx : C.slx, csy = (w < 2) ? C.sry : C.sly;
-  const float cgx = (w == 0 || w == 2) ? C.grx : C.glx, cgy = (w == 0 || w == 2) ? C.gry : C.gly;
-  const float dx = cgx - csx, dy = cgy - csy;
+// Dubins.cpp:180-323 — CSC word w (0 RSR, 1 RSL, 2 LSR, 3 LSL) in stages, so that a
+// wavefront can spread one word's libm calls over several lanes:
+//   word_geo      centre-to-centre vector of the word's circles;
+//   (caller)      th = atan2f(dy, dx); for RSL/LSR ac = acosf(2r / dist);
+//   word_arcs     the tangent angles t1 and q[2] of RSL/LSR;
+//   (caller)      cos/sin of t1 and q[2] for RSL/LSR;
+//   word_len      params and length.
+struct WordGeo { float csx, csy, cgx, cgy, dx, dy, dist; };
+__device__ __forceinline__ WordGeo word_geo(int w, const Centres& C) {
+  WordGeo g;
+  g.csx = (w < 2) ? C.srx : C.slx;
+  g.csy = (w < 2) ? C.sry : C.sly;
+  g.cgx = (w == 0 || w == 2) ? C.grx : C.glx;
+  g.cgy = (w == 0 || w == 2) ? C.gry : C.gly;
+  g.dx = g.cgx - g.csx;
+  g.dy = g.cgy - g.csy;
+  g.dist = sqrtf(g.dx * g.dx + g.dy * g.dy);
+  return g;
+}
+__device__ __forceinline__ float word_acos_arg(float r, const WordGeo& g) { return 2.0f * r / g.dist; }
+__device__ __forceinline__ void word_arcs(int w, float th, float ac, float* t1, float* q2) {
+  if (w == 1) {
+    *t1 = ac + th;
+    *q2 = (float)((double)*t1 - M_PI);
+  } else {
+    *t1 = -ac + th;
+    *q2 = (float)((double)*t1 + M_PI);
+  }
+}
+__device__ __forceinline__ float word_len(int w, float r, const WordGeo& g, float sh, float gh, float th, float t1,
+                                          float ct1, float st1, float cq2, float sq2, float q[4]) {
   if (w == 0 || w == 3) {
-    const float th = g_atan2f(dy, dx);
     if (w == 0) {
       q[0] = (float)(M_PI_2 + (double)sh);
-      const float t1 = (float)(M_PI_2 + (double)th);
-      q[2] = t1;
+      const float a1 = (float)(M_PI_2 + (double)th);
+      q[2] = a1;
       const float tg = (float)(M_PI_2 + (double)gh);
-      q[1] = t1 - q[0];
+      q[1] = a1 - q[0];
       if (q[1] > 0) q[1] = (float)((double)q[1] - 2 * M_PI);
       q[3] = tg - q[2];
       if (q[3] > 0) q[3] = (float)((double)q[3] - 2 * M_PI);
     } else {
       q[0] = (float)(-M_PI_2 + (double)sh);
-      const float t1 = (float)(-M_PI_2 + (double)th);
-      q[2] = t1;
+      const float a1 = (float)(-M_PI_2 + (double)th);
+      q[2] = a1;
       const float tg = (float)(-M_PI_2 + (double)gh);
-      q[1] = t1 - q[0];
+      q[1] = a1 - q[0];
       if (q[1] < 0) q[1] = (float)((double)q[1] + 2 * M_PI);
       q[3] = tg - q[2];
       if (q[3] < 0) q[3] = (float)((double)q[3] + 2 * M_PI);
     }
-    const float dst = sqrtf(dx * dx + dy * dy);
-    return (w == 0) ? dst + r * -(q[1] + q[3]) : dst + r * (q[1] + q[3]);
+    return (w == 0) ? g.dist + r * -(q[1] + q[3]) : g.dist + r * (q[1] + q[3]);
   }
-  const float dist = sqrtf(dx * dx + dy * dy);
-  const float th = g_atan2f(dy, dx);
-  float t1;
   if (w == 1) {
     q[0] = (float)(M_PI_2 + (double)sh);
-    t1 = g_acosf(2.0f * r / dist) + th;
     q[2] = (float)((double)t1 - M_PI);
     const float tg = (float)(-M_PI_2 + (double)gh);
     q[1] = t1 - q[0];
@@ -178,7 +210,6 @@ __device__ __forceinline__ float dubins_word(int w, float r, const Centres& C, f
     if (q[3] < 0) q[3] = (float)((double)q[3] + 2 * M_PI);
   } else {
     q[0] = (float)(-M_PI_2 + (double)sh);
-    t1 = -g_acosf(2.0f * r / dist) + th;
     q[2] = (float)((double)t1 + M_PI);
     const float tg = (float)(M_PI_2 + (double)gh);
     q[1] = t1 - q[0];
@@ -186,14 +217,29 @@ __device__ __forceinline__ float dubins_word(int w, float r, const Centres& C, f
     q[3] = tg - q[2];
     if (q[3] > 0) q[3] = (float)((double)q[3] - 2 * M_PI);
   }
-  float ax = csx, ay = csy, bx = cgx, by = cgy;
-  ax += r * g_cosf(t1);
-  ay += r * g_sinf(t1);
-  bx += r * g_cosf(q[2]);
-  by += r * g_sinf(q[2]);
+  float ax = g.csx, ay = g.csy, bx = g.cgx, by = g.cgy;
+  ax += r * ct1;
+  ay += r * st1;
+  bx += r * cq2;
+  by += r * sq2;
   const float ex = bx - ax, ey = by - ay;
   const float dst = sqrtf(ex * ex + ey * ey);
   return (w == 1) ? dst + r * (-q[1] + q[3]) : dst + r * (q[1] - q[3]);
+}
+
+// One lane evaluates the whole word.
+__device__ __forceinline__ float dubins_word(int w, float r, const Centres& C, float sh, float gh, float q[4]) {
+  const WordGeo g = word_geo(w, C);
+  const float th = g_atan2f(g.dy, g.dx);
+  float t1 = 0.0f, q2 = 0.0f, ct1 = 0.0f, st1 = 0.0f, cq2 = 0.0f, sq2 = 0.0f;
+  if (w == 1 || w == 2) {
+    word_arcs(w, th, g_acosf(word_acos_arg(r, g)), &t1, &q2);
+    ct1 = g_cosf(t1);
+    st1 = g_sinf(t1);
+    cq2 = g_cosf(q2);
+    sq2 = g_sinf(q2);
+  }
+  return word_len(w, r, g, sh, gh, th, t1, ct1, st1, cq2, sq2, q);
 }
 
 // Dubins.cpp:19-69: shortest of the four words in RSR, RSL, LSR, LSL order (strict <).
@@ -219,6 +265,52 @@ __device__ __forceinline__ float dubins_shortest(float r, float sx, float sy, fl
 // ------------------------------------------------------------ wave helpers ----------
 __device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src, 64); }
 __device__ __forceinline__ int shfl_i(int v, int src) { return __shfl(v, src, 64); }
+// lane L's value as a wave-uniform (scalar) value
+__device__ __forceinline__ float rl_f(float v, int L) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), L));
+}
+__device__ __forceinline__ int rl_i(int v, int L) { return __builtin_amdgcn_readlane(v, L); }
+
+// Dubins::get_shortest_path_length (Dubins.cpp:19-69) of every candidate successor of an
+// expansion: candidate a's pose (sx, sy, sh) is held by all lanes of its group
+// [a * gs, (a + 1) * gs); every lane of the group returns the candidate's length, the
+// minimum of the four CSC words in RSR, RSL, LSR, LSL order (strict <).
+//   gs = 16: the libm calls of one candidate are spread over its group — lanes 0/1 take
+//            sin/cos of the heading, word lanes 0..3 atan2f/acosf, lanes 4..11 the cos/sin
+//            of the RSL and LSR tangent angles — so the dependent chain is 4 calls long;
+//   gs = 4:  lane w of the group evaluates word w alone.
+__device__ __forceinline__ float cand_dubins(float r, const GoalC& GC, float gh, float sx, float sy, float sh, int gs,
+                                            int lane) {
+  const int base = lane & ~(gs - 1), sub = lane & (gs - 1), w = sub & 3;
+  float len;
+  if (gs == 16) {
+    const float t0 = g_sincosf_sel(sh, (sub & 1) != 0);
+    const Centres C = centres_from(r, sx, sy, shfl_f(t0, base), shfl_f(t0, base + 1), GC);
+    const WordGeo g = word_geo(w, C);
+    const float th = g_atan2f(g.dy, g.dx);
+    const float ac = g_acosf(word_acos_arg(r, g));  // used by RSL / LSR only
+    float t1, q2;
+    word_arcs(w == 2 ? 2 : 1, th, ac, &t1, &q2);
+    // lanes 4..7: cos t1, sin t1, cos q2, sin q2 of RSL (word lane 1); lanes 8..11: of LSR
+    const int ws = base + ((sub >> 2) == 2 ? 2 : 1), which = sub & 3;
+    const float t1s = shfl_f(t1, ws), q2s = shfl_f(q2, ws);  // both unconditionally (no divergent shuffle)
+    const float at = which < 2 ? t1s : q2s;
+    const float tv = g_sincosf_sel(at, (which & 1) == 0);
+    const int tb = base + (w == 2 ? 8 : 4);
+    float q[4];
+    len = word_len(w, r, g, sh, gh, th, t1, shfl_f(tv, tb), shfl_f(tv, tb + 1), shfl_f(tv, tb + 2),
+                   shfl_f(tv, tb + 3), q);
+  } else {
+    float q[4];
+    len = dubins_word(w, r, dubins_centres_g(r, sx, sy, sh, GC), sh, gh, q);
+  }
+  float best = shfl_f(len, base);
+  for (int w2 = 1; w2 < 4; ++w2) {
+    const float v = shfl_f(len, base + w2);
+    if (v < best) best = v;
+  }
+  return best;
+}
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) {
     const uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
@@ -247,6 +339,16 @@ __device__ __forceinline__ void apf_load_regs(const PlannerDev& P, ApfRegs& R, i
     R.oy[q] = in ? apf[3 * k + 1] : 0.0f;
     R.orad[q] = in ? apf[3 * k + 2] : 0.0f;
   }
+}
+
+// the in-radius term of one obstacle (Grid3D.cpp:212-223), d = hypotf(dx, dy) < orad
+__device__ __forceinline__ float apf_term(const PlannerDev& P, float dx, float dy, float d, float orad, float ph) {
+  float ang = fabsf(wrap_pi_f(ph - g_atan2f(dy, dx)));
+  ang = stl_max(P.apf_ang - ang, 0.0f);
+  const double t = 1.0 / (double)d - 1.0 / (double)orad;
+  float fp = (float)((double)P.apf_rep * (t * t));  // std::pow(t, 2) folded to t*t (GCC)
+  fp = fp * ang / P.apf_ang;
+  return fp;
 }
 
 __device__ __forceinline__ float apf_field(const PlannerDev& P, const ApfRegs& R, float px, float py, float ph,
@@ -282,12 +384,7 @@ __device__ __forceinline__ float apf_field(const PlannerDev& P, const ApfRegs& R
       const float d = g_hypotf(dx, dy);
       if (d < orad) {
         near = true;
-        float ang = fabsf(wrap_pi_f(ph - g_atan2f(dy, dx)));
-        ang = stl_max(P.apf_ang - ang, 0.0f);
-        const double t = 1.0 / (double)d - 1.0 / (double)orad;
-        float fp = (float)((double)P.apf_rep * (t * t));  // std::pow(t, 2) folded to t*t (GCC)
-        fp = fp * ang / P.apf_ang;
-        term = fp;
+        term = apf_term(P, dx, dy, d, orad, ph);
       }
     }
     uint64_t m = __ballot(near);
@@ -298,6 +395,82 @@ __device__ __forceinline__ float apf_field(const PlannerDev& P, const ApfRegs& R
     }
   }
   return acc;
+}
+
+// APF fields of all candidate successors of one expansion at once.  Candidate a of the
+// window sits in lane a * gs (its pose in sx/sy/sh there); cmask has bit a * gs set for
+// every candidate to evaluate; the result is in lane a * gs.  Every successor lies within
+// P.apf_reach (per axis) of the expanded pose (cx, cy), so an obstacle whose square of
+// half-width r + apf_reach around it misses (cx, cy) cannot pass the exact pre-test of any
+// successor: the obstacle list is culled once, then lanes run over (candidate, kept
+// obstacle) pairs, and every successor's in-radius terms are summed in obstacle order.
+constexpr int APF_MAXC = 64;  // kept obstacles staged in LDS (more: per-candidate fallback)
+struct ApfCand { float x, y, r; };
+__device__ __forceinline__ float apf_fused(const PlannerDev& P, const ApfRegs& R, float cx, float cy, float sx,
+                                           float sy, float sh, uint64_t cmask, int gs, int lane,
+                                           ApfCand* __restrict__ kept) {
+  float fc = 0.0f;
+  if (cmask == 0) return fc;
+  int C = APF_MAXC + 1;
+#ifdef HASTAR_DBG_APFOLD
+  if (false) {
+#else
+  if (P.n_apf <= 64 * APF_REG_ROUNDS) {
+#endif
+    C = 0;
+#pragma unroll
+    for (int u = 0; u < APF_REG_ROUNDS; ++u) {
+      const float lim = R.orad[u] + P.apf_reach;
+      const bool in = 64 * u + lane < P.n_apf && fabsf(R.ox[u] - cx) < lim && fabsf(R.oy[u] - cy) < lim;
+      const uint64_t bm = __ballot(in);
+      const int pos = C + __popcll(bm & ((1ull << lane) - 1));
+      if (in && pos < APF_MAXC) kept[pos] = ApfCand{R.ox[u], R.oy[u], R.orad[u]};
+      C += __popcll(bm);
+    }
+    if (C == 0) return 0.0f;
+  }
+  if (C > APF_MAXC) {  // many obstacles near: one candidate at a time over the whole list
+    for (uint64_t m = cmask; m; m &= m - 1) {
+      const int L = __ffsll((unsigned long long)m) - 1;
+      const float f = apf_field(P, R, uff(shfl_f(sx, L)), uff(shfl_f(sy, L)), uff(shfl_f(sh, L)), lane);
+      if (lane == L) fc = f;
+    }
+    return fc;
+  }
+  wave_lds_sync();
+  const int na = (63 - __builtin_clzll(cmask)) / gs + 1;  // candidates 0 .. na-1
+  const int npair = na * C;
+  for (int base = 0; base < npair; base += 64) {
+    const int p = base + lane;
+    const bool act = p < npair;
+    const int a = act ? p / C : 0;
+    const int j = act ? p - a * C : 0;
+    const float px = shfl_f(sx, a * gs), py = shfl_f(sy, a * gs), ph = shfl_f(sh, a * gs);
+    float term = 0.0f;
+    bool near = false;
+    if (act && ((cmask >> (a * gs)) & 1ull)) {
+      const ApfCand o = kept[j];
+      const float dx = o.x - px, dy = o.y - py;
+      if (fabsf(dx) < o.r && fabsf(dy) < o.r) {
+        const float d = g_hypotf(dx, dy);
+        if (d < o.r) {
+          near = true;
+          term = apf_term(P, dx, dy, d, o.r, ph);
+        }
+      }
+    }
+    // pairs are candidate-major, obstacles ascending: lane order is summation order
+    uint64_t m = __ballot(near);
+    while (m) {
+      const int b = __ffsll((unsigned long long)m) - 1;
+      const float t = shfl_f(term, b);
+      const int ab = __builtin_amdgcn_readlane(a, b);
+      if (lane == ab * gs) fc = fc + t;
+      m &= m - 1;
+    }
+  }
+  wave_lds_sync();
+  return fc;
 }
 
 // Dubins.cpp:326-563 sampling of the chosen word, wave-parallel (64 samples per step).

@@ -19,6 +19,7 @@
 namespace hastar {
 
 constexpr int MAXS = 16;   // max steering actions (checked at create)
+static_assert(64 / 4 >= MAXS, "4 lanes per candidate action must cover MAXS actions");
 
 // Diagnostic build only (-DHASTAR_STAMPS): cycles per phase of the search loop,
 // 0 pop+closed insert, 1 successors+APF+Dubins, 2 open/closed bookkeeping, 3 holonomic A*,
@@ -829,7 +830,7 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, in
   d.h = s.h;
   d.prev = prev;
   gstore(&gp(c.A->open3)[n], d);
-  c.o3.fresh(n, key, f, NIL, NIL, pos, RB_RED);
+  c.o3.fresh(n, d);
   STAMP_T tl = STAMP_NOW();
   c.o3.link(left, n, pos);
   STAMP_ADD(20, tl);
@@ -839,7 +840,7 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, in
 // ------------------------------------------------------------------- the search -------
 // One find_path (HybridAStar.cpp:68-88 incl. hybrid_a_star_search 93-199 and
 // reconstruct_path 208-262) of planner *c.P in arena *c.A, run by one wavefront.
-__device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& alds, int max_pops) {
+__device__ __forceinline__ void search_one(SearchCtx& c, ApfCand* akept, AStarLds& alds, int max_pops) {
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
@@ -878,19 +879,27 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
   }
   // goal circles are the same for every Dubins evaluation of this search
   const float r = P.r_min;
+  const GoalC GC = goal_centres(r, P.goal_x, P.goal_y, P.goal_h);
   int counter = 0, interval = P.shot_interval;
   bool shot_allowed = false;
   uint64_t dig = 0x243f6a8885a308d3ull;
   int ok = 0, via_shot = 0, terminal = NIL, dub_n = 0;
   float cost = FLT_MAX;
   const int span = 2 * P.na + 1;
+  // lanes per candidate action: 16 when the window has at most 4 actions (the Dubins
+  // libm calls then spread over the group), else 4 (one Dubins word per lane)
+#ifdef HASTAR_DBG_NARROW
+  const int gsh = 2, gs = 4;
+#else
+  const int gsh = span <= 4 ? 4 : 2, gs = 1 << gsh;
+#endif
   STAMP_T tloop = STAMP_NOW();
 
   while (!c.o3.empty()) {
     if (c.pops >= max_pops) { c.status = -75; break; }
     STAMP_T tp = STAMP_NOW();
     const int b = c.o3.begin();
-    const Node3 top = gload(&gp(A.open3)[b]);
+    const Node3 top = c.o3.node(b);  // usually cached: the leftmost node was touched by the last walks
     bool fresh;
     const int ci = closed3_insert(c, top, &fresh);
     if (ci == NIL) { c.status = -75; break; }
@@ -947,93 +956,111 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
         STAMP_ADD(4, tsh);
       }
     }
-    // ---- successors: VehicleModel::get_neighbors (VehicleModel.cpp:63-105) + Grid3D filter
+    // ---- successors (VehicleModel::get_neighbors, VehicleModel.cpp:63-105; Grid3D filter and
+    // field, Grid3D.cpp:47-74, 206-227) and their Dubins lengths (Dubins.cpp:19-69), fused.
+    // Candidate a of the action window [lo, lo + span) is evaluated by lanes
+    // [a * gs, (a + 1) * gs).  The HBM probes of every candidate (occupancy, closed-set slot,
+    // memo flag and value) are issued first, so their latency hides behind the Dubins and
+    // APF arithmetic; the kept successors keep the reference's push_back (action) order.
     STAMP_T tx = STAMP_NOW();
     shot_allowed = cur.vmin < 1.0f;
     int lo = cur.ci - P.na;
     lo = lo < 0 ? 0 : lo;
-    // one lane per action of the window [lo, lo + span) ∩ [0, nsteer); kept successors
-    // are compacted in action order (the reference's push_back order)
-    int ns = 0;
-    {
-      const int i = lo + lane;
-      bool keep = lane < span && i < P.nsteer;
-      Succ s;
-      float vm = 0.0f;
-      if (keep && !shot_allowed) {
-        const float lat = cur.vmin * gp(P.curv_abs)[i];
-        if (lat > P.a_lat) keep = false;
-        const float al = (float)sqrt(1.0 - (double)((lat * lat) / P.a_lat2));
-        vm = cur.vmin - 2.0f * al * P.ts;
-      }
-      if (keep) {
-        const GAS float* o = &gp(P.off)[2 * ((size_t)i * (P.bins + 1) + cbin)];
-        s.x = cur.x + o[0];
-        s.y = cur.y + o[1];
-        s.h = wrap_pi_f(cur.h + gp(P.dth)[i]);
-        s.g = cur.g + gp(P.act_cost)[i];
-        s.vmin = vm;
-        s.ci = i;
-        s.bin = heading_bin(s.h, P.prec);
-        s.cx = trunc_f(s.x / P.res);
-        s.cy = trunc_f(s.y / P.res);
-        s.dub = 0.0f;
-        keep = s.cx > -1 && s.cx < P.N && s.cy > -1 && s.cy < P.N;
-        if (keep) keep = gp(P.occ)[(size_t)s.cx * P.N + s.cy] < P.thr;
-      }
-      const uint64_t km = __ballot(keep);
-      ns = __popcll(km);
-      if (keep) sl[__popcll(km & ((1ull << lane) - 1))] = s;
+    const int ca = lane >> gsh, sub = lane & (gs - 1);
+    const int ai = lo + ca;
+    bool cand = ca < span && ai < P.nsteer;
+    const int ia = cand ? ai : lo;  // in-range index: the table loads are unconditional
+    const float cabs = gp(P.curv_abs)[ia];
+    const GAS float* ofs = &gp(P.off)[2 * ((size_t)ia * (P.bins + 1) + cbin)];
+    const float ofx = ofs[0], ofy = ofs[1], odth = gp(P.dth)[ia], oact = gp(P.act_cost)[ia];
+    float vm = 0.0f;
+    if (cand && !shot_allowed) {
+      const float lat = cur.vmin * cabs;
+      if (lat > P.a_lat) cand = false;
+      const float al = (float)sqrt(1.0 - (double)((lat * lat) / P.a_lat2));
+      vm = cur.vmin - 2.0f * al * P.ts;
     }
-    wave_lds_sync();
+    float sx = 0.0f, sy = 0.0f, sh = 0.0f, sg = 0.0f;
+    int sbin = 0, scx = 0, scy = 0;
+    bool inb = false;
+    if (cand) {
+      sx = cur.x + ofx;
+      sy = cur.y + ofy;
+      sh = wrap_pi_f(cur.h + odth);
+      sg = cur.g + oact;
+      sbin = heading_bin(sh, P.prec);
+      scx = trunc_f(sx / P.res);
+      scy = trunc_f(sy / P.res);
+      inb = scx > -1 && scx < P.N && scy > -1 && scy < P.N;
+    }
+    const bool lead = inb && sub == 0;
+    const uint32_t skey = key3(scx, scy, sbin);
+    uint32_t sh0 = 0;
+    v2u slot0{0u, 0u};
+    float occv = 0.0f, pnf = 0.0f;
+    uint32_t pvis = 0;
+    if (lead) {
+      const size_t cell = (size_t)scx * P.N + scy;
+      occv = gp(P.occ)[cell];
+      sh0 = slot_hash(skey) & A.slots3_mask;
+      slot0 = *(const GAS v2u*)&gp(A.slots3)[sh0];
+      pvis = gp(P.visited)[cell];
+      pnf = gp(P.nm_f)[cell];
+    }
     STAMP_ADD(16, tx);
-    STAMP_T tapf = STAMP_NOW();
-    c.succ += ns;
-    // APF field of every kept successor (lanes over obstacles)
-    for (int q = 0; q < ns; ++q) {
-      const float fc = apf_field(P, apr, sl[q].x, sl[q].y, sl[q].h, lane);
-      wave_lds_sync();
-      if (lane == 0) sl[q].g = sl[q].g + fc;
-      wave_lds_sync();
-    }
-    STAMP_ADD(17, tapf);
     STAMP_T tdub = STAMP_NOW();
-    // Dubins lengths: lane = 4 * successor + word
-    {
-      const int q = lane >> 2, w = lane & 3;
-      float len = 0.0f;
-      if (q < ns) {
-        const Centres C = dubins_centres(r, sl[q].x, sl[q].y, sl[q].h, P.goal_x, P.goal_y, P.goal_h);
-        float prm[4];
-        len = dubins_word(w, r, C, sl[q].h, P.goal_h, prm);
-      }
-      for (int s = 0; s < ns; ++s) {
-        float best = shfl_f(len, 4 * s);
-        for (int w2 = 1; w2 < 4; ++w2) {
-          const float v = shfl_f(len, 4 * s + w2);
-          if (v < best) best = v;
+    const float dub = cand_dubins(r, GC, P.goal_h, sx, sy, sh, gs, lane);
+    STAMP_ADD(18, tdub);
+    STAMP_T tapf = STAMP_NOW();
+    const float fc = apf_fused(P, apr, cur.x, cur.y, sx, sy, sh, __ballot(lead), gs, lane, akept);
+    STAMP_ADD(17, tapf);
+    STAMP_T tw = STAMP_NOW();
+    const bool kept = lead && occv < P.thr;
+    const uint64_t km = __ballot(kept);
+    c.succ += __popcll(km);
+    // closed-set membership (continuing each kept candidate's probe sequence; the closed
+    // set does not change while the successors are processed)
+    bool isc = false;
+    if (kept) {
+      const uint32_t gbits = (c.gen3 & SLOT3_GEN_MASK) << SLOT3_IDX_BITS;
+      uint32_t hs = sh0;
+      v2u sv = slot0;
+      for (;;) {
+        if ((sv.y & ~SLOT3_IDX_MASK) != gbits) break;
+        if (sv.x == skey) {
+          isc = true;
+          break;
         }
-        if (lane == 0) sl[s].dub = best;
+        hs = (hs + 1) & A.slots3_mask;
+        sv = *(const GAS v2u*)&gp(A.slots3)[hs];
       }
     }
-    wave_lds_sync();
-    STAMP_ADD(18, tdub);
+    const uint64_t closed_m = __ballot(isc);
+    const uint64_t vis_m = __ballot(kept && (uint8_t)pvis == (uint8_t)P.vgen);
+    STAMP_ADD(21, tw);
     STAMP_ADD(1, tx);
-    // ---- HybridAStar.cpp:159-193
+    // ---- HybridAStar.cpp:159-193, successors in action order
     STAMP_T tb = STAMP_NOW();
     bool fail = false;
-    // closed-set membership of all successors at once (lane q probes successor q; the
-    // closed set does not change while the successors are processed)
-    uint64_t closed_m;
-    {
-      bool isc = false;
-      if (lane < ns) isc = closed3_contains(c, key3(sl[lane].cx, sl[lane].cy, sl[lane].bin));
-      closed_m = __ballot(isc);
-    }
-    for (int q = 0; q < ns; ++q) {
-      const Succ s = sl[q];
+#ifdef HASTAR_DBG_NOPREF
+    bool memo_ok = false;
+#else
+    bool memo_ok = true;  // no inner A* search has run since the memo probes were issued
+#endif
+    for (uint64_t m = km & ~closed_m; m; m &= m - 1) {
+      const int L = __ffsll((unsigned long long)m) - 1;
+      Succ s;
+      s.x = rl_f(sx, L);
+      s.y = rl_f(sy, L);
+      s.h = rl_f(sh, L);
+      s.g = rl_f(sg, L) + rl_f(fc, L);  // Grid3D.cpp:66-69: g += field
+      s.vmin = rl_f(vm, L);
+      s.ci = lo + (L >> gsh);
+      s.bin = rl_i(sbin, L);
+      s.cx = rl_i(scx, L);
+      s.cy = rl_i(scy, L);
+      s.dub = rl_f(dub, L);
       const uint32_t key = key3(s.cx, s.cy, s.bin);
-      if ((closed_m >> q) & 1ull) continue;
       STAMP_T tf3 = STAMP_NOW();
       // std::set::find with f == g (the heuristic is not added yet).  The tree's in-order
       // f sequence is strictly increasing, so when g <= f(leftmost) the lower_bound
@@ -1048,21 +1075,25 @@ __device__ __forceinline__ void search_one(SearchCtx& c, Succ* sl, AStarLds& ald
         else hit = c.o3.find(key, s.g);
       }
       STAMP_ADD(13, tf3);
-      if (hit == 0) {
+      const bool repl = hit != 0 && s.g < c.o3.G(hit);
+      if (hit == 0 || repl) {
+        if (repl) {
+          STAMP_T tu3 = STAMP_NOW();
+          c.o3.unlink(hit);
+          tpool_free(c.o3, c.ps3, hit);
+          STAMP_ADD(15, tu3);
+        }
+        // AStar::find_path(int, int): a memo hit probed above is still valid while no
+        // A* search has run in this expansion (only a search writes the memo)
         STAMP_T ta = STAMP_NOW();
-        const float h1 = holonomic(c, alds, s.cx, s.cy);
-        STAMP_ADD(3, ta);
-        const float f = s.g + stl_max(h1, s.dub);
-        STAMP_T ti3 = STAMP_NOW();
-        if (!insert3(c, s, f, ci)) { fail = true; break; }
-        STAMP_ADD(14, ti3);
-      } else if (s.g < gp(A.open3)[hit].g) {
-        STAMP_T tu3 = STAMP_NOW();
-        c.o3.unlink(hit);
-        tpool_free(c.o3, c.ps3, hit);
-        STAMP_ADD(15, tu3);
-        STAMP_T ta = STAMP_NOW();
-        const float h1 = holonomic(c, alds, s.cx, s.cy);
+        float h1;
+        if (memo_ok && ((vis_m >> L) & 1ull)) {
+          h1 = rl_f(pnf, L);
+        } else {
+          const long long a0 = c.asearch;
+          h1 = holonomic(c, alds, s.cx, s.cy);
+          if (c.asearch != a0) memo_ok = false;
+        }
         STAMP_ADD(3, ta);
         const float f = s.g + stl_max(h1, s.dub);
         STAMP_T ti3 = STAMP_NOW();
@@ -1172,7 +1203,7 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
                                                            const SlotArena* __restrict__ arenas,
                                                            const int* __restrict__ order, int* __restrict__ next,
                                                            int max_pops, int n_prio) {
-  __shared__ Succ sl[MAXS];
+  __shared__ ApfCand akept[APF_MAXC];
   __shared__ AStarLds alds;
   SearchCtx c;
   c.A = arenas + blockIdx.x;
@@ -1190,7 +1221,7 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
     if (q < n_prio) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(0);
     c.P = descs + order[q];
-    search_one(c, sl, alds, max_pops);
+    search_one(c, akept, alds, max_pops);
   }
   if (c.lane == 0) {
     gp(A.gens)[0] = c.gen3;

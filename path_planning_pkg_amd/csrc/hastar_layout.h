@@ -112,7 +112,7 @@ struct PlannerDev {
   float res, thr, apf_rep, apf_ang;
   float ts, a_lat, a_lat2, prec;
   float r_min, step, ang_step, act_cost_diag;   // Dubins radius/step; 2D diagonal move cost
-  float act_cost_axis, pad_f0, pad_f1, pad_f2;
+  float act_cost_axis, apf_reach, pad_f1, pad_f2;  // apf_reach: max |successor offset| per axis (+ margin)
   // --- goal (grid frame) and world transform for path reconstruction
   float goal_x, goal_y, goal_h;                // _goal_node._pose2D
   int goal_cx, goal_cy, goal_bin;

@@ -426,7 +426,10 @@ struct CachedAcc3 {
   int cid;      // this lane's cached node (-1: empty)
   uint32_t ck;
   float cf;
-  int cl, cr, cp, cc;
+  int cl, cr, cp;
+  uint32_t cc;  // color (byte 0) | curvature index << 8
+  float cg, cvm, cx, cy, ch;  // payload: g, vmin, pose
+  int cpv;                    // payload: prev
   int rr;       // round-robin victim counter (wave-uniform)
   int plen;     // lanes [0, plen) hold the last walk's path (wave-uniform)
 
@@ -445,33 +448,71 @@ struct CachedAcc3 {
     rr = rr == 62 - PATH ? 0 : rr + 1;
     return v;
   }
-  struct Full {
-    uint32_t key;
-    float f;
-    int l, r, p, c;
-  };
-  // one round trip: quads 0 and 1 of node x; cached in lane `slot`
-  __device__ __forceinline__ Full fill(int x, int slot) {
+  // lane `slot` takes node x from registers of lane `h` (h may be any lane)
+  __device__ __forceinline__ void copy_from(int x, int h, int slot) {
+    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)ck, h);
+    const float f = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), h));
+    const int l = __builtin_amdgcn_readlane(cl, h), r = __builtin_amdgcn_readlane(cr, h);
+    const int p = __builtin_amdgcn_readlane(cp, h);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cc, h);
+    const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cg), h));
+    const float vm = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cvm), h));
+    const float px = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), h));
+    const float py = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), h));
+    const float ph = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ch), h));
+    const int pv = __builtin_amdgcn_readlane(cpv, h);
+    if (lane == slot) {
+      cid = x;
+      ck = k;
+      cf = f;
+      cl = l;
+      cr = r;
+      cp = p;
+      cc = c;
+      cg = g;
+      cvm = vm;
+      cx = px;
+      cy = py;
+      ch = ph;
+      cpv = pv;
+    }
+  }
+  // one round trip: the whole 48-B record of node x, cached in lane `slot`; returns the
+  // record as wave-uniform values
+  __device__ __forceinline__ Node3 fill(int x, int slot) {
     typedef int v4 __attribute__((ext_vector_type(4)));
     const __attribute__((address_space(1))) v4* q = (const __attribute__((address_space(1))) v4*)&t[x];
-    const v4 a = q[0], b = q[1];
-    Full n;
+    const v4 a = q[0], b = q[1], d = q[2];
+    Node3 n;
     n.key = rb_uu((uint32_t)a.x);
     n.f = __int_as_float(rb_ui(a.y));
     n.l = rb_ui(a.z);
     n.r = rb_ui(a.w);
     n.p = rb_ui(b.x);
-    n.c = rb_ui(b.y) & 0xff;
-    if (lane == slot) {
-      cid = x;
-      ck = n.key;
-      cf = n.f;
-      cl = n.l;
-      cr = n.r;
-      cp = n.p;
-      cc = n.c;
-    }
+    n.cc = rb_uu((uint32_t)b.y);
+    n.g = __int_as_float(rb_ui(b.z));
+    n.vmin = __int_as_float(rb_ui(b.w));
+    n.x = __int_as_float(rb_ui(d.x));
+    n.y = __int_as_float(rb_ui(d.y));
+    n.h = __int_as_float(rb_ui(d.z));
+    n.prev = rb_ui(d.w);
+    if (lane == slot) set_lane(x, n);
     return n;
+  }
+  __device__ __forceinline__ void set_lane(int x, const Node3& n) {
+    cid = x;
+    ck = n.key;
+    cf = n.f;
+    cl = n.l;
+    cr = n.r;
+    cp = n.p;
+    cc = n.cc;
+    cg = n.g;
+    cvm = n.vmin;
+    cx = n.x;
+    cy = n.y;
+    ch = n.h;
+    cpv = n.prev;
   }
   __device__ __forceinline__ int L(int x) {
     const int h = hit(x);
@@ -487,7 +528,7 @@ struct CachedAcc3 {
   }
   __device__ __forceinline__ int C(int x) {
     const int h = hit(x);
-    return h >= 0 ? __builtin_amdgcn_readlane(cc, h) : fill(x, victim(x)).c;
+    return (int)((h >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)cc, h) : fill(x, victim(x)).cc) & 0xffu);
   }
   __device__ __forceinline__ uint32_t K(int x) {
     const int h = hit(x);
@@ -496,6 +537,33 @@ struct CachedAcc3 {
   __device__ __forceinline__ float F(int x) {
     const int h = hit(x);
     return h >= 0 ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), h)) : fill(x, victim(x)).f;
+  }
+  __device__ __forceinline__ float G(int x) {
+    const int h = hit(x);
+    return h >= 0 ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cg), h)) : fill(x, victim(x)).g;
+  }
+  // the whole record of node x (the pop reads the payload from the cache when it can)
+  __device__ __forceinline__ Node3 node(int x) {
+#ifdef HASTAR_DBG_NOPAY
+    const int h = -1;
+#else
+    const int h = hit(x);
+#endif
+    if (h < 0) return fill(x, victim(x));
+    Node3 n;
+    n.key = (uint32_t)__builtin_amdgcn_readlane((int)ck, h);
+    n.f = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), h));
+    n.l = __builtin_amdgcn_readlane(cl, h);
+    n.r = __builtin_amdgcn_readlane(cr, h);
+    n.p = __builtin_amdgcn_readlane(cp, h);
+    n.cc = (uint32_t)__builtin_amdgcn_readlane((int)cc, h);
+    n.g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cg), h));
+    n.vmin = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cvm), h));
+    n.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), h));
+    n.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), h));
+    n.h = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ch), h));
+    n.prev = __builtin_amdgcn_readlane(cpv, h);
+    return n;
   }
   __device__ __forceinline__ void sL(int x, int v) {
     t[x].l = v;
@@ -511,7 +579,7 @@ struct CachedAcc3 {
   }
   __device__ __forceinline__ void sC(int x, int v) {
     *(__attribute__((address_space(1))) uint8_t*)&t[x].cc = (uint8_t)v;  // byte 0 only: ci stays
-    cc = cid == x ? v : cc;
+    cc = cid == x ? ((cc & ~0xffu) | (uint32_t)(v & 0xff)) : cc;
   }
   // the walk step at `depth`: node x, kept in path lane `depth` (copied there on a hit
   // in another lane)
@@ -523,21 +591,10 @@ struct CachedAcc3 {
       q.f = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), h));
       q.l = __builtin_amdgcn_readlane(cl, h);
       q.r = __builtin_amdgcn_readlane(cr, h);
-      if (depth < PATH && h != depth) {
-        const int p = __builtin_amdgcn_readlane(cp, h), c = __builtin_amdgcn_readlane(cc, h);
-        if (lane == depth) {
-          cid = x;
-          ck = q.key;
-          cf = q.f;
-          cl = q.l;
-          cr = q.r;
-          cp = p;
-          cc = c;
-        }
-      }
+      if (depth < PATH && h != depth) copy_from(x, h, depth);
       return q;
     }
-    const Full n = fill(x, depth < PATH ? depth : victim(x));
+    const Node3 n = fill(x, depth < PATH ? depth : victim(x));
     q.key = n.key;
     q.f = n.f;
     q.l = n.l;
@@ -604,18 +661,10 @@ struct CachedAcc3 {
   }
   // a node just written in full by the caller (pool allocation): drop stale copies of
   // the index and cache the new contents (no HBM traffic)
-  __device__ __forceinline__ void fresh(int x, uint32_t key, float f, int l, int r, int p, int c) {
+  __device__ __forceinline__ void fresh(int x, const Node3& n) {
     cid = cid == x ? -1 : cid;
     const int slot = victim(x);
-    if (lane == slot) {
-      cid = x;
-      ck = key;
-      cf = f;
-      cl = l;
-      cr = r;
-      cp = p;
-      cc = c;
-    }
+    if (lane == slot) set_lane(x, n);
   }
   // RBT::link's first step: the caller has already stored the leaf fields with the node
   __device__ __forceinline__ void leaf(int, int) {}

@@ -65,6 +65,7 @@ def load_library():
     L.hastar_debug_cycles.argtypes = [vp, C.POINTER(C.c_ulonglong)]
     L.hastar_debug_astar_modes.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_timing.argtypes = [vp, C.POINTER(C.c_ulonglong)]
+    L.hastar_debug_slots.argtypes = [vp, C.POINTER(C.c_longlong)]
     _lib = L
     return L
 
@@ -192,6 +193,12 @@ class HybridAStar:
         out = (C.c_longlong * 2)()
         _check(load_library().hastar_debug_astar_modes(self.h, out))
         return {"migrations": out[0], "astar_pops_hbm": out[1]}
+
+    def slots(self):
+        """Search-slot pool of this planner's device (after a find_path)."""
+        out = (C.c_longlong * 4)()
+        _check(load_library().hastar_debug_slots(self.h, out))
+        return {"resident_slots": out[0], "waves_per_cu": out[1], "arenas": out[2], "arena_mib": out[3]}
 
     def timing(self):
         """(t_start, t_end, slot) of the last search; times in 10 ns ticks."""

@@ -77,5 +77,6 @@ for B in args.batches:
                           "astar_searches": sum(r["stats"]["astar_searches"] for r in res), "overflow_seeds": bad[:20], "n_overflow": len(bad),
                           "max_work": max(r["stats"]["pops"] + r["stats"]["astar_pops"] for r in res),
                           **timing_summary(ps[:B], res),
+                          "pool": ps[0].slots(),
                           "mean_work": (pops + apops) / B}),
               flush=True)

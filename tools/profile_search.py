@@ -43,4 +43,6 @@ for s in args.seeds:
                                               for i, n in enumerate(["pop_probe", "find", "insert", "unlink_hit",
                                                                      "memoise"])},
                           outer_per_pop={n: round(cyc[13 + i] / max(st["pops"], 1))
-                                         for i, n in enumerate(["find3", "insert3", "unlink3"])})))
+                                         for i, n in enumerate(["find3", "insert3", "unlink3", "succ_gen", "apf",
+                                                                "dubins", "insert_walk", "insert_link",
+                                                                "probe_wait"])})))
