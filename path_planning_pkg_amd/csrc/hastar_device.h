@@ -323,22 +323,25 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 // obstacle list.  Terms of obstacles farther than their radius are exactly +0.0f in
 // the reference, so only in-radius terms are accumulated — in obstacle order, one at a
 // time, exactly like std::accumulate.
-// The first APF_REG_ROUNDS x 64 obstacles of a planner are held in registers for the
-// whole search (loaded once); any further ones are read from HBM per call.
-constexpr int APF_REG_ROUNDS = 4;
-struct ApfRegs {
-  float ox[APF_REG_ROUNDS], oy[APF_REG_ROUNDS], orad[APF_REG_ROUNDS];
+// The first APF_LDS_CAP obstacles of a planner are staged in LDS for the whole search
+// (loaded once); any further ones are read from HBM per call.
+constexpr int APF_LDS_CAP = 256;
+constexpr int APF_MAXC = 64;  // obstacles kept by the per-expansion cull (more: per-candidate fallback)
+struct ApfCand { float x, y, r; };
+struct ApfStage {
+  ApfCand obs[APF_LDS_CAP];
+  ApfCand kept[APF_MAXC];
 };
-__device__ __forceinline__ void apf_load_regs(const PlannerDev& P, ApfRegs& R, int lane) {
+__device__ __forceinline__ void apf_stage(const PlannerDev& P, ApfStage& S, int lane) {
   const GAS float* apf = gp(P.apf);
-#pragma unroll
-  for (int q = 0; q < APF_REG_ROUNDS; ++q) {
-    const int k = 64 * q + lane;
-    const bool in = k < P.n_apf;
-    R.ox[q] = in ? apf[3 * k] : 0.0f;
-    R.oy[q] = in ? apf[3 * k + 1] : 0.0f;
-    R.orad[q] = in ? apf[3 * k + 2] : 0.0f;
-  }
+  const int n = P.n_apf < APF_LDS_CAP ? P.n_apf : APF_LDS_CAP;
+  for (int k = lane; k < n; k += 64) S.obs[k] = ApfCand{apf[3 * k], apf[3 * k + 1], apf[3 * k + 2]};
+  wave_lds_sync();
+}
+__device__ __forceinline__ ApfCand apf_obstacle(const PlannerDev& P, const ApfStage& S, int k) {
+  if (k < APF_LDS_CAP) return S.obs[k];
+  const GAS float* apf = gp(P.apf);
+  return ApfCand{apf[3 * k], apf[3 * k + 1], apf[3 * k + 2]};
 }
 
 // the in-radius term of one obstacle (Grid3D.cpp:212-223), d = hypotf(dx, dy) < orad
@@ -351,32 +354,15 @@ __device__ __forceinline__ float apf_term(const PlannerDev& P, float dx, float d
   return fp;
 }
 
-__device__ __forceinline__ float apf_field(const PlannerDev& P, const ApfRegs& R, float px, float py, float ph,
+__device__ __forceinline__ float apf_field(const PlannerDev& P, const ApfStage& S, float px, float py, float ph,
                                            int lane) {
   float acc = 0.0f;
-  for (int base = 0, q = 0; base < P.n_apf; base += 64, ++q) {
+  for (int base = 0; base < P.n_apf; base += 64) {
     const int k = base + lane;
     float term = 0.0f;
     bool near = false;
-    float ox, oy, orad;
-    if (q < APF_REG_ROUNDS) {
-      // static register index: select through the unrolled rounds
-      ox = R.ox[0];
-      oy = R.oy[0];
-      orad = R.orad[0];
-#pragma unroll
-      for (int u = 1; u < APF_REG_ROUNDS; ++u)
-        if (q == u) {
-          ox = R.ox[u];
-          oy = R.oy[u];
-          orad = R.orad[u];
-        }
-    } else {
-      const GAS float* apf = gp(P.apf);
-      ox = k < P.n_apf ? apf[3 * k] : 0.0f;
-      oy = k < P.n_apf ? apf[3 * k + 1] : 0.0f;
-      orad = k < P.n_apf ? apf[3 * k + 2] : 0.0f;
-    }
+    const ApfCand o = apf_obstacle(P, S, k < P.n_apf ? k : 0);
+    const float ox = o.x, oy = o.y, orad = o.r;
     const float dx = ox - px, dy = oy - py;
     // exact pre-test: the correctly rounded hypotf(dx, dy) >= max(|dx|, |dy|), so an
     // obstacle outside the axis-aligned square of half-width r cannot have d < r
@@ -404,27 +390,26 @@ __device__ __forceinline__ float apf_field(const PlannerDev& P, const ApfRegs& R
 // half-width r + apf_reach around it misses (cx, cy) cannot pass the exact pre-test of any
 // successor: the obstacle list is culled once, then lanes run over (candidate, kept
 // obstacle) pairs, and every successor's in-radius terms are summed in obstacle order.
-constexpr int APF_MAXC = 64;  // kept obstacles staged in LDS (more: per-candidate fallback)
-struct ApfCand { float x, y, r; };
-__device__ __forceinline__ float apf_fused(const PlannerDev& P, const ApfRegs& R, float cx, float cy, float sx,
-                                           float sy, float sh, uint64_t cmask, int gs, int lane,
-                                           ApfCand* __restrict__ kept) {
+__device__ __forceinline__ float apf_fused(const PlannerDev& P, ApfStage& S, float cx, float cy, float sx,
+                                           float sy, float sh, uint64_t cmask, int gs, int lane) {
+  ApfCand* __restrict__ kept = S.kept;
   float fc = 0.0f;
   if (cmask == 0) return fc;
   int C = APF_MAXC + 1;
 #ifdef HASTAR_DBG_APFOLD
   if (false) {
 #else
-  if (P.n_apf <= 64 * APF_REG_ROUNDS) {
+  if (P.n_apf <= APF_LDS_CAP) {
 #endif
     C = 0;
 #pragma unroll
-    for (int u = 0; u < APF_REG_ROUNDS; ++u) {
-      const float lim = R.orad[u] + P.apf_reach;
-      const bool in = 64 * u + lane < P.n_apf && fabsf(R.ox[u] - cx) < lim && fabsf(R.oy[u] - cy) < lim;
+    for (int u = 0; u < APF_LDS_CAP / 64; ++u) {
+      const ApfCand o = S.obs[64 * u + lane];
+      const float lim = o.r + P.apf_reach;
+      const bool in = 64 * u + lane < P.n_apf && fabsf(o.x - cx) < lim && fabsf(o.y - cy) < lim;
       const uint64_t bm = __ballot(in);
       const int pos = C + __popcll(bm & ((1ull << lane) - 1));
-      if (in && pos < APF_MAXC) kept[pos] = ApfCand{R.ox[u], R.oy[u], R.orad[u]};
+      if (in && pos < APF_MAXC) kept[pos] = o;
       C += __popcll(bm);
     }
     if (C == 0) return 0.0f;
@@ -432,7 +417,7 @@ __device__ __forceinline__ float apf_fused(const PlannerDev& P, const ApfRegs& R
   if (C > APF_MAXC) {  // many obstacles near: one candidate at a time over the whole list
     for (uint64_t m = cmask; m; m &= m - 1) {
       const int L = __ffsll((unsigned long long)m) - 1;
-      const float f = apf_field(P, R, uff(shfl_f(sx, L)), uff(shfl_f(sy, L)), uff(shfl_f(sh, L)), lane);
+      const float f = apf_field(P, S, uff(shfl_f(sx, L)), uff(shfl_f(sy, L)), uff(shfl_f(sh, L)), lane);
       if (lane == L) fc = f;
     }
     return fc;

@@ -18,6 +18,9 @@
 
 namespace hastar {
 
+#ifndef HASTAR_WAVES_PER_EU
+#define HASTAR_WAVES_PER_EU 2  // search waves per SIMD the register budget must allow
+#endif
 constexpr int MAXS = 16;   // max steering actions (checked at create)
 static_assert(64 / 4 >= MAXS, "4 lanes per candidate action must cover MAXS actions");
 
@@ -840,7 +843,7 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, in
 // ------------------------------------------------------------------- the search -------
 // One find_path (HybridAStar.cpp:68-88 incl. hybrid_a_star_search 93-199 and
 // reconstruct_path 208-262) of planner *c.P in arena *c.A, run by one wavefront.
-__device__ __forceinline__ void search_one(SearchCtx& c, ApfCand* akept, AStarLds& alds, int max_pops) {
+__device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLds& alds, int max_pops) {
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
@@ -848,8 +851,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfCand* akept, AStarLd
   for (int q = 0; q < NSTAMP; ++q) c.cyc[q] = 0;
 #endif
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  ApfRegs apr;
-  apf_load_regs(P, apr, lane);
+  apf_stage(P, apfs, lane);
   c.o3.t = gp(A.open3);
   c.o3.lane = lane;
   c.o3.reset_cache();
@@ -1012,7 +1014,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfCand* akept, AStarLd
     const float dub = cand_dubins(r, GC, P.goal_h, sx, sy, sh, gs, lane);
     STAMP_ADD(18, tdub);
     STAMP_T tapf = STAMP_NOW();
-    const float fc = apf_fused(P, apr, cur.x, cur.y, sx, sy, sh, __ballot(lead), gs, lane, akept);
+    const float fc = apf_fused(P, apfs, cur.x, cur.y, sx, sy, sh, __ballot(lead), gs, lane);
     STAMP_ADD(17, tapf);
     STAMP_T tw = STAMP_NOW();
     const bool kept = lead && occv < P.thr;
@@ -1188,6 +1190,8 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfCand* akept, AStarLd
     R->t_end = __builtin_amdgcn_s_memrealtime();
     R->slot = (int)blockIdx.x;
 #ifdef HASTAR_STAMPS
+    c.cyc[22] = c.o3.n_fill;
+    c.cyc[23] = c.o3.n_step;
     for (int q = 0; q < NSTAMP; ++q) R->cycles[q] = c.cyc[q];
 #else
     for (int q = 0; q < NSTAMP; ++q) R->cycles[q] = 0;
@@ -1199,11 +1203,11 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfCand* akept, AStarLd
 // Persistent work-queue kernel: grid = W resident slots (one wavefront each).  Each slot
 // pulls planner indices (in `order`, longest-expected-first when the host knows) from a
 // device counter until the queue is drained, so early finishers take the next planner.
-__global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners,
+__global__ __launch_bounds__(64, HASTAR_WAVES_PER_EU) void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners,
                                                            const SlotArena* __restrict__ arenas,
                                                            const int* __restrict__ order, int* __restrict__ next,
                                                            int max_pops, int n_prio) {
-  __shared__ ApfCand akept[APF_MAXC];
+  __shared__ ApfStage apfs;
   __shared__ AStarLds alds;
   SearchCtx c;
   c.A = arenas + blockIdx.x;
@@ -1221,7 +1225,7 @@ __global__ __launch_bounds__(64) void hastar_search_kernel(const PlannerDev* __r
     if (q < n_prio) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(0);
     c.P = descs + order[q];
-    search_one(c, akept, alds, max_pops);
+    search_one(c, apfs, alds, max_pops);
   }
   if (c.lane == 0) {
     gp(A.gens)[0] = c.gen3;
@@ -1404,9 +1408,9 @@ __global__ void k_test_math(int fn, const float* a, const float* b, float* out, 
 
 __global__ __launch_bounds__(64) void k_test_field(PlannerDev P, const float* poses, int n, float* out) {
   for (int q = blockIdx.x; q < n; q += gridDim.x) {
-    ApfRegs apr;
-    apf_load_regs(P, apr, threadIdx.x);
-    const float f = apf_field(P, apr, poses[3 * q], poses[3 * q + 1], poses[3 * q + 2], threadIdx.x);
+    __shared__ ApfStage apfs;
+    apf_stage(P, apfs, threadIdx.x);
+    const float f = apf_field(P, apfs, poses[3 * q], poses[3 * q + 1], poses[3 * q + 2], threadIdx.x);
     if (threadIdx.x == 0) out[q] = f;
   }
 }

@@ -432,11 +432,17 @@ struct CachedAcc3 {
   int cpv;                    // payload: prev
   int rr;       // round-robin victim counter (wave-uniform)
   int plen;     // lanes [0, plen) hold the last walk's path (wave-uniform)
+#ifdef HASTAR_STAMPS
+  unsigned long long n_fill, n_step;  // diagnostic: round trips (misses) and walk steps
+#endif
 
   __device__ __forceinline__ void reset_cache() {
     cid = -1;
     rr = 0;
     plen = 0;
+#ifdef HASTAR_STAMPS
+    n_fill = n_step = 0;
+#endif
   }
   __device__ __forceinline__ int hit(int x) const {
     const uint64_t m = __ballot(cid == x);
@@ -483,6 +489,9 @@ struct CachedAcc3 {
     typedef int v4 __attribute__((ext_vector_type(4)));
     const __attribute__((address_space(1))) v4* q = (const __attribute__((address_space(1))) v4*)&t[x];
     const v4 a = q[0], b = q[1], d = q[2];
+#ifdef HASTAR_STAMPS
+    n_fill++;
+#endif
     Node3 n;
     n.key = rb_uu((uint32_t)a.x);
     n.f = __int_as_float(rb_ui(a.y));
@@ -585,6 +594,9 @@ struct CachedAcc3 {
   // in another lane)
   __device__ __forceinline__ Quad quad_at(int x, int depth) {
     const int h = hit(x);
+#ifdef HASTAR_STAMPS
+    n_step++;
+#endif
     Quad q;
     if (h >= 0) {
       q.key = (uint32_t)__builtin_amdgcn_readlane((int)ck, h);

@@ -45,4 +45,6 @@ for s in args.seeds:
                           outer_per_pop={n: round(cyc[13 + i] / max(st["pops"], 1))
                                          for i, n in enumerate(["find3", "insert3", "unlink3", "succ_gen", "apf",
                                                                 "dubins", "insert_walk", "insert_link",
-                                                                "probe_wait"])})))
+                                                                "probe_wait"])},
+                          outer_tree={"fills_per_pop": cyc[22] / max(st["pops"], 1),
+                                      "walk_steps_per_pop": cyc[23] / max(st["pops"], 1)})))
