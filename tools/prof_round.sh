@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round profile (run on the GPU box):  tools/prof_round.sh <tag>
+#   1. bench.py under rocprofv3 --kernel-trace --stats  -> gpurun_out/<tag>/bench.json,
+#      kernel_stats.csv, trace_summary.json (search-kernel dispatch durations)
+#   2. two PMC passes (FETCH_SIZE, WRITE_SIZE) over the search kernel of a 1-step bench
+#      -> gpurun_out/<tag>/pmc_search_summary.json
+# Big raw traces stay in /tmp on the box.
+set -o pipefail
+TAG=${1:-prof}
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+R=/tmp/rp_$TAG
+rm -rf $R && mkdir -p $R
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/trace -o run -- python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+python3 tools/prof_summary.py trace $R/trace $OUT/trace_summary.json --warmup 1 --steps 3 || exit 1
+find $R/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+B=$(python3 -c "import json;print(json.load(open('$OUT/bench.json'))['config']['queries_per_gpu'])")
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 400 rocprofv3 --pmc $C --output-format csv --kernel-include-regex hastar_search_kernel -d $R/$C -o pmc -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --latency-queries 0 > $OUT/pmc_$C.log 2>&1 || { tail -5 $OUT/pmc_$C.log; exit 1; }
+done
+python3 tools/prof_summary.py pmc $R/FETCH_SIZE $R/WRITE_SIZE $OUT/pmc_search_summary.json --batch $B --grid 1024 || exit 1
+cat $OUT/pmc_search_summary.json
