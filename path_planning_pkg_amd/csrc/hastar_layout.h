@@ -86,7 +86,7 @@ constexpr uint32_t SLOT3_IDX_MASK = (1u << SLOT3_IDX_BITS) - 1;
 constexpr uint32_t SLOT3_GEN_MASK = 0xfffu;
 
 // diagnostic phase counters of the search kernel (-DHASTAR_STAMPS)
-constexpr int NSTAMP = 24;
+constexpr int NSTAMP = 32;
 
 // Per-search result block (written by the search kernel, read by the host).
 struct SearchResult {
