@@ -82,20 +82,20 @@ GM_HD uint32_t abstop12(float x) { return (fbits(x) >> 20) & 0x7ffu; }
 // sinf_poly() with the FMA grouping of the -mfma build: odd (n even: sine) or even
 // (n odd: cosine) polynomial; tab1 selects copy 1 of the table.
 GM_HD float sincos_poly_t(double x, double x2, bool tab1, int n) {
-  if ((n & 1) == 0) {
-    double x3 = x * x2;
-    double s1 = fma(x2, -0x1.994eb3774cf24p-13, 0x1.1107605230bc4p-7);
-    double x7 = x3 * x2;
-    double s = fma(x3, -0x1.555545995a603p-3, x);
-    return (float)fma(s1, x7, s);
-  }
-  double x4 = x2 * x2;
-  double c1 = fma(x2, -0x1.ffffffd0c621cp-2, 0x1.0p+0);
-  double c2 = fma(x2, 0x1.99343027bf8c3p-16, -0x1.6c087e89a359dp-10);
-  double x6 = x4 * x2;
-  double c = fma(x4, 0x1.55553e1068f19p-5, c1);
-  const float v = (float)fma(c2, x6, c);
-  return tab1 ? -v : v;
+  // both polynomials, selected (lanes of a wave may need different ones)
+  const double x3 = x * x2;
+  const double s1 = fma(x2, -0x1.994eb3774cf24p-13, 0x1.1107605230bc4p-7);
+  const double x7 = x3 * x2;
+  const double sp = fma(x3, -0x1.555545995a603p-3, x);
+  const float vs = (float)fma(s1, x7, sp);
+  const double x4 = x2 * x2;
+  const double c1 = fma(x2, -0x1.ffffffd0c621cp-2, 0x1.0p+0);
+  const double c2 = fma(x2, 0x1.99343027bf8c3p-16, -0x1.6c087e89a359dp-10);
+  const double x6 = x4 * x2;
+  const double c = fma(x4, 0x1.55553e1068f19p-5, c1);
+  const float vc = (float)fma(c2, x6, c);
+  if ((n & 1) == 0) return vs;
+  return tab1 ? -vc : vc;
 }
 
 // reduce_large(): Payne-Hanek style reduction for |y| >= 120, 64-bit integer exact.
@@ -121,36 +121,37 @@ GM_HD float nan_of(float y) { return (y - y) / (y - y); }
 // sinf and cosf differ only in the |y| < 2^-12 result and in which polynomial an odd
 // quadrant takes.
 GM_HD float g_sincosf_sel(float y, bool cosine) {
-  double x = y;
-  uint32_t t = abstop12(y);
-  if (t < 0x3f4u) {                      // |y| < pi/4
-    double s = x * x;
-    if (t < 0x398u) return cosine ? 1.0f : y;  // |y| < 2^-12
-    return sincos_poly_t(x, s, false, cosine ? 1 : 0);
+  // |y| < 0.75 (glibc's small-argument path) is the |y| < 120 path with n = 0: the
+  // reduction x - 0 * hpi is exact and the quadrant logic picks the same polynomial, so
+  // both run as one branch-free sequence (no divergence between the lanes of a wave).
+  const double x = y;
+  const uint32_t t = abstop12(y);
+  if (t >= 0x42fu) {  // |y| >= 120, inf, nan (the planner never gets here)
+    if (t >= 0x7f8u) return nan_of(y);
+    const uint32_t xi = fbits(y);
+    int n;
+    const double xr = reduce_large(xi, &n);
+    const int ns = n + (int)(xi >> 31);
+    const double x2 = xr * xr;
+    const bool tab1 = (ns & 2) != 0;
+    if (cosine ? ((n ^ 1) & 1) : (n & 1)) return sincos_poly_t(xr, x2, tab1, 1);
+    return sincos_poly_t(((ns + 1) & 2) ? -xr : xr, x2, tab1, 0);
   }
-  int n, ns;
-  double xr;
-  if (t < 0x42fu) {                      // |y| < 120
-    double r = x * 0x1.45f306dc9c883p+23;
-    n = (((int32_t)r) + 0x800000) >> 24;
-    xr = fma(-(double)n, 0x1.921fb54442d18p+0, x);  // vfnmadd: x - n*hpi, one rounding
-    ns = n;
-  } else if (t < 0x7f8u) {
-    uint32_t xi = fbits(y);
-    xr = reduce_large(xi, &n);
-    ns = n + (int)(xi >> 31);
-  } else {
-    return nan_of(y);
-  }
-  double x2 = xr * xr;
-  const bool tab1 = (ns & 2) != 0;
-  if (cosine ? ((n ^ 1) & 1) : (n & 1)) return sincos_poly_t(xr, x2, tab1, 1);
-  return sincos_poly_t(((ns + 1) & 2) ? -xr : xr, x2, tab1, 0);  // xr * sign[ns & 3]
+  const double r = x * 0x1.45f306dc9c883p+23;
+  const int n = (((int32_t)r) + 0x800000) >> 24;
+  const double xr = fma(-(double)n, 0x1.921fb54442d18p+0, x);  // vfnmadd: x - n*hpi, one rounding
+  const double x2 = xr * xr;
+  const bool odd = cosine ? ((n ^ 1) & 1) : (n & 1);
+  const float v = sincos_poly_t(odd ? xr : (((n + 1) & 2) ? -xr : xr), x2, (n & 2) != 0, odd ? 1 : 0);
+  if (t < 0x398u) return cosine ? 1.0f : y;  // |y| < 2^-12
+  return v;
 }
 GM_HD float g_sinf(float y) { return g_sincosf_sel(y, false); }
 GM_HD float g_cosf(float y) { return g_sincosf_sel(y, true); }
 
 // ---------------------------------------------------------------- atanf -------
+// The argument-reduction cases are selected, not branched, so lanes in different ranges
+// share one instruction stream; each case computes exactly the fdlibm expression.
 GM_HD float g_atanf(float x) {
   const int32_t hx = (int32_t)fbits(x);
   const int32_t ix = hx & 0x7fffffff;
@@ -159,31 +160,17 @@ GM_HD float g_atanf(float x) {
     if (hx > 0) return bitsf(0x33a22168u) + bitsf(0x3fc90fdau);
     return bitsf(0xbfc90fdau) - bitsf(0x33a22168u);
   }
-  int id;
-  float hi = 0.0f, lo = 0.0f;
-  if (ix < 0x3ee00000) {                          // |x| < 0.4375
-    if (ix < 0x31000000) return x;                // |x| < 2^-29 (huge + x > 1 always)
-    id = -1;
-  } else {
-    x = fabsf(x);
-    if (ix < 0x3f980000) {
-      if (ix < 0x3f300000) {                      // 7/16 <= |x| < 11/16
-        id = 0; hi = bitsf(0x3eed6338u); lo = bitsf(0x31ac3769u);
-        x = (x + x - 1.0f) / (x + 2.0f);
-      } else {                                    // 11/16 <= |x| < 19/16
-        id = 1; hi = bitsf(0x3f490fdau); lo = bitsf(0x33222168u);
-        x = (x - 1.0f) / (x + 1.0f);
-      }
-    } else if (ix < 0x401c0000) {                 // |x| < 2.4375
-      id = 2; hi = bitsf(0x3f7b985eu); lo = bitsf(0x33140fb4u);
-      x = (x - 1.5f) / (x * 1.5f + 1.0f);
-    } else {                                      // 2.4375 <= |x| < 2^25
-      id = 3; hi = bitsf(0x3fc90fdau); lo = bitsf(0x33a22168u);
-      x = -1.0f / x;
-    }
-  }
-  float z = x * x;
-  float w = z * z;
+  const bool small = ix < 0x3ee00000;             // |x| < 0.4375: id = -1
+  const float ax = fabsf(x);
+  // id 0: 7/16 <= |x| < 11/16, 1: < 19/16, 2: < 2.4375, 3: >= 2.4375
+  const int id = ix < 0x3f300000 ? 0 : (ix < 0x3f980000 ? 1 : (ix < 0x401c0000 ? 2 : 3));
+  const float num = id == 0 ? ax + ax - 1.0f : (id == 1 ? ax - 1.0f : (id == 2 ? ax - 1.5f : -1.0f));
+  const float den = id == 0 ? ax + 2.0f : (id == 1 ? ax + 1.0f : (id == 2 ? ax * 1.5f + 1.0f : ax));
+  const float hi = bitsf(id == 0 ? 0x3eed6338u : (id == 1 ? 0x3f490fdau : (id == 2 ? 0x3f7b985eu : 0x3fc90fdau)));
+  const float lo = bitsf(id == 0 ? 0x31ac3769u : (id == 1 ? 0x33222168u : (id == 2 ? 0x33140fb4u : 0x33a22168u)));
+  const float xr = small ? x : num / den;
+  const float z = xr * xr;
+  const float w = z * z;
   float s1 = bitsf(0x3c8569d7u) * w + bitsf(0x3d4bda59u);
   s1 = s1 * w + bitsf(0x3d886b35u);
   s1 = s1 * w + bitsf(0x3dba2e6eu);
@@ -195,9 +182,10 @@ GM_HD float g_atanf(float x) {
   s2 = s2 * w - bitsf(0x3de38e38u);
   s2 = s2 * w - bitsf(0x3e4ccccdu);
   s2 = s2 * w;
-  float t = (s1 + s2) * x;
-  if (id < 0) return x - t;
-  float r = hi - ((t - lo) - x);
+  const float t = (s1 + s2) * xr;
+  const float r = hi - ((t - lo) - xr);
+  if (ix < 0x31000000) return x;                  // |x| < 2^-29 (huge + x > 1 always)
+  if (small) return xr - t;
   return (hx < 0) ? -r : r;
 }
 
@@ -234,19 +222,18 @@ GM_HD float g_atan2f(float y, float x) {
   if (iy == 0x7f800000u) return ((int32_t)hy < 0) ? npio2 - tiny : tiny + pio2;
   const int32_t dk = (int32_t)iy - (int32_t)ix;
   const int32_t k = dk >> 23;
-  float z;
-  if (dk > 0x1e7fffff) z = pio2 - bitsf(0x333bbd2eu);       // pi_o_2 + 0.5*pi_lo
-  else if ((int32_t)hx < 0 && k < -60) z = 0.0f;
-  else z = g_atanf(fabsf(y / x));
-  switch (m) {
-    case 0: return z;
-    case 1: return bitsf(fbits(z) ^ 0x80000000u);
-    case 2: return pi - (mpi_lo + z);
-    default: return (z + mpi_lo) - pi;
-  }
+  const float za = g_atanf(fabsf(y / x));
+  const float z = dk > 0x1e7fffff ? pio2 - bitsf(0x333bbd2eu)       // pi_o_2 + 0.5*pi_lo
+                  : (((int32_t)hx < 0 && k < -60) ? 0.0f : za);
+  const float r1 = bitsf(fbits(z) ^ 0x80000000u);
+  const float r2 = pi - (mpi_lo + z);
+  const float r3 = (z + mpi_lo) - pi;
+  return m == 0 ? z : (m == 1 ? r1 : (m == 2 ? r2 : r3));
 }
 
 // ---------------------------------------------------------------- acosf -------
+// The three argument ranges share one instruction stream (one rational approximation,
+// one sqrt, the final expression selected); each range computes exactly fdlibm's value.
 GM_HD float g_acosf(float x) {
   const float pio2_hi = bitsf(0x3fc90fdau), pio2_lo = bitsf(0x33a22168u);
   const float pi = bitsf(0x40490fdau);
@@ -257,38 +244,28 @@ GM_HD float g_acosf(float x) {
     return bitsf(0x34222168u) + pi;                // pi + 2*pio2_lo
   }
   if (ix > 0x3f800000) return (x - x) / (x - x);
-  auto pq = [](float z) -> float {
-    float p = bitsf(0x3811ef08u) * z + bitsf(0x3a4f7f04u);
-    p = p * z - bitsf(0x3d241146u);
-    p = p * z + bitsf(0x3e4e0aa8u);
-    p = p * z - bitsf(0x3ea6b090u);
-    p = p * z + bitsf(0x3e2aaaabu);
-    p = p * z;
-    float q = bitsf(0x3d9dc62eu) * z - bitsf(0x3f303361u);
-    q = q * z + bitsf(0x4001572du);
-    q = q * z - bitsf(0x4019d139u);
-    q = q * z + 1.0f;
-    return p / q;
-  };
-  if (ix < 0x3f000000) {                           // |x| < 0.5
-    if (ix <= 0x32800000) return pio2_lo + pio2_hi;
-    float r = pq(x * x);
-    return pio2_hi - (x - (pio2_lo - r * x));
-  }
-  if (hx < 0) {                                    // x <= -0.5
-    float z = (x + 1.0f) * 0.5f;
-    float s = sqrtf(z);
-    float r = pq(z);
-    float w = r * s - pio2_lo;
-    return pi - (s + w) * 2.0f;
-  }
-  float z = (1.0f - x) * 0.5f;                     // x >= 0.5
-  float s = sqrtf(z);
-  float df = bitsf(fbits(s) & 0xfffff000u);
-  float c = (z - df * df) / (s + df);
-  float r = pq(z);
-  float w = r * s + c;
-  return (df + w) * 2.0f;
+  const bool mid = ix < 0x3f000000;                // |x| < 0.5
+  const bool neg = hx < 0;                         // x <= -0.5 (when !mid)
+  const float z = mid ? x * x : (neg ? (x + 1.0f) * 0.5f : (1.0f - x) * 0.5f);
+  float p = bitsf(0x3811ef08u) * z + bitsf(0x3a4f7f04u);
+  p = p * z - bitsf(0x3d241146u);
+  p = p * z + bitsf(0x3e4e0aa8u);
+  p = p * z - bitsf(0x3ea6b090u);
+  p = p * z + bitsf(0x3e2aaaabu);
+  p = p * z;
+  float q = bitsf(0x3d9dc62eu) * z - bitsf(0x3f303361u);
+  q = q * z + bitsf(0x4001572du);
+  q = q * z - bitsf(0x4019d139u);
+  q = q * z + 1.0f;
+  const float r = p / q;
+  const float s = sqrtf(z);
+  const float df = bitsf(fbits(s) & 0xfffff000u);
+  const float c = (z - df * df) / (s + df);
+  const float v_mid = pio2_hi - (x - (pio2_lo - r * x));
+  const float v_neg = pi - (s + (r * s - pio2_lo)) * 2.0f;
+  const float v_pos = (df + (r * s + c)) * 2.0f;
+  if (mid && ix <= 0x32800000) return pio2_lo + pio2_hi;
+  return mid ? v_mid : (neg ? v_neg : v_pos);
 }
 
 // ---------------------------------------------------------------- hypotf ------
