@@ -1192,6 +1192,10 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
 #ifdef HASTAR_STAMPS
     c.cyc[22] = c.o3.n_fill;
     c.cyc[23] = c.o3.n_step;
+    c.cyc[26] = c.o3.fill_cyc;
+    c.cyc[27] = c.o3.pre_wait_cyc;
+    c.cyc[28] = c.o3.pw_cyc;
+    c.cyc[29] = c.o3.pw_ins_cyc;
     for (int q = 0; q < NSTAMP; ++q) R->cycles[q] = c.cyc[q];
 #else
     for (int q = 0; q < NSTAMP; ++q) R->cycles[q] = 0;

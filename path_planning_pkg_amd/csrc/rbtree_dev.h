@@ -433,7 +433,7 @@ struct CachedAcc3 {
   int rr;       // round-robin victim counter (wave-uniform)
   int plen;     // lanes [0, plen) hold the last walk's path (wave-uniform)
 #ifdef HASTAR_STAMPS
-  unsigned long long n_fill, n_step;  // diagnostic: round trips (misses) and walk steps
+  unsigned long long n_fill, n_step, fill_cyc, pre_wait_cyc, pw_cyc, pw_ins_cyc;  // diagnostics
 #endif
 
   __device__ __forceinline__ void reset_cache() {
@@ -441,7 +441,7 @@ struct CachedAcc3 {
     rr = 0;
     plen = 0;
 #ifdef HASTAR_STAMPS
-    n_fill = n_step = 0;
+    n_fill = n_step = fill_cyc = pre_wait_cyc = pw_cyc = pw_ins_cyc = 0;
 #endif
   }
   __device__ __forceinline__ int hit(int x) const {
@@ -487,13 +487,23 @@ struct CachedAcc3 {
   // record as wave-uniform values
   __device__ __forceinline__ Node3 fill(int x, int slot) {
     typedef int v4 __attribute__((ext_vector_type(4)));
+#ifdef HASTAR_STAMPS
+    const unsigned long long ta = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    pre_wait_cyc += t0 - ta;
+#endif
     const __attribute__((address_space(1))) v4* q = (const __attribute__((address_space(1))) v4*)&t[x];
     const v4 a = q[0], b = q[1], d = q[2];
 #ifdef HASTAR_STAMPS
     n_fill++;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     Node3 n;
     n.key = rb_uu((uint32_t)a.x);
+#ifdef HASTAR_STAMPS
+    fill_cyc += __builtin_amdgcn_s_memtime() - t0;
+#endif
     n.f = __int_as_float(rb_ui(a.y));
     n.l = rb_ui(a.z);
     n.r = rb_ui(a.w);
@@ -620,6 +630,9 @@ struct CachedAcc3 {
   // (ka != kb) && (fa < fb).  Outputs as RBT::find / RBT::insert_pos expect them.
   __device__ __forceinline__ void path_walk(uint32_t k, float f, bool ins, int* y_, uint32_t* yk_, float* yf_,
                                             bool* comp_) {
+#ifdef HASTAR_STAMPS
+    const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
+#endif
     int y = 0, depth = 0;
     uint32_t yk = 0;
     float yf = 0.0f;
@@ -666,6 +679,10 @@ struct CachedAcc3 {
       }
     }
     plen = depth < PATH ? depth : PATH;
+#ifdef HASTAR_STAMPS
+    pw_cyc += __builtin_amdgcn_s_memtime() - tw0;
+    if (ins) pw_ins_cyc += __builtin_amdgcn_s_memtime() - tw0;
+#endif
     *y_ = y;
     *yk_ = yk;
     *yf_ = yf;

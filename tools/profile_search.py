@@ -47,4 +47,8 @@ for s in args.seeds:
                                                                 "dubins", "insert_walk", "insert_link",
                                                                 "probe_wait"])},
                           outer_tree={"fills_per_pop": cyc[22] / max(st["pops"], 1),
-                                      "walk_steps_per_pop": cyc[23] / max(st["pops"], 1)})))
+                                      "walk_steps_per_pop": cyc[23] / max(st["pops"], 1),
+                                      "cycles_per_fill": cyc[26] / max(cyc[22], 1),
+                                      "prior_ops_wait_per_fill": cyc[27] / max(cyc[22], 1),
+                                      "path_walk_per_pop": cyc[28] / max(st["pops"], 1),
+                                      "path_walk_ins_per_pop": cyc[29] / max(st["pops"], 1)})))
