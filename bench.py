@@ -78,6 +78,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-queries", type=int, default=3)
+    ap.add_argument("--workload", choices=("cfg3", "cfg5"), default="cfg3",
+                    help="cfg3: batch of independent queries (default, the headline line); "
+                         "cfg5: 20 Hz replan loop of start/goal pairs (BASELINE.json configs[4])")
+    ap.add_argument("--pairs", type=int, default=64, help="cfg5: start/goal pairs per GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -96,6 +100,8 @@ def main():
     from path_planning_pkg_amd.capi import PlannerConfig
     from tests.scenarios import synthetic
 
+    if args.workload == "cfg5":
+        return run_cfg5(args, gpu, dist, torch, rank, world, device)
     B = args.batch
     def cfg_for(q):
         cfg, proto = synthetic(args.grid, args.bins, args.obstacles, seed=q + 1)
@@ -111,10 +117,12 @@ def main():
     vels = [c[1]["vel"] for c in cfgs]
     starts = [c[1]["start"] for c in cfgs]
 
+    # host-side batch arguments and output arrays are allocated once and reused every step
+    bufs = gpu.BatchBuffers(planners, cap=8192)
+
     def step():
-        for p in planners:
-            p.reset()
-        br = gpu.find_path_batch_arrays(planners, vels, starts, cap=8192)
+        gpu.reset_batch(bufs)  # HybridAStar::reset() of every planner
+        br = gpu.find_path_batch_arrays(planners, vels, starts, buffers=bufs)
         return br, br.kernel_ms
 
     for _ in range(args.warmup):
@@ -197,6 +205,108 @@ def main():
         dist.destroy_process_group()
     if out is not None:
         print(json.dumps(out))
+
+
+def run_cfg5(args, gpu, dist, torch, rank, world, device):
+    """BASELINE.json configs[4] / SURVEY.md §8d cfg5: the local planner's replan loop for
+    `pairs` start/goal pairs per GPU (pair ids rank*pairs ...; weak scaling, no exchange).
+    One step = one 20 Hz tick of every pair: a batched find_path WITHOUT reset (memo and
+    stale node-map values carry over, local_planner.cpp:316), then free-space decay and the
+    boxes moved by their velocity (local_planner.cpp:241,288).  value = pops / tick wall
+    (max over ranks); the tick wall includes the map upkeep."""
+    from tests.scenarios import drive, replan_pairs, replan_tick, replan_tick_inputs
+    P = args.pairs
+    pairs = []
+    for q in shard_query_ids(rank, world, P):  # one generator draw per pair id
+        pairs += replan_pairs(args.grid, args.bins, args.obstacles, 1, seed=1000 + q)
+    t_setup = time.perf_counter()
+    planners = []
+    for cfg, proto, _ in pairs:
+        cfg.values["max_pops"] = args.max_pops
+        cfg.values["max_astar_nodes"] = args.max_astar_nodes
+        p = gpu.HybridAStar(cfg, device=device)
+        drive(p, proto)
+        planners.append(p)
+    t_setup = time.perf_counter() - t_setup
+    bufs = gpu.BatchBuffers(planners, cap=8192)
+    vels = [proto["vel"] for _, proto, _ in pairs]
+    tick = [0]
+
+    def step():
+        t = tick[0]
+        starts = [replan_tick_inputs(proto, v, t)[0] for _, proto, v in pairs]
+        br = gpu.find_path_batch_arrays(planners, vels, starts, buffers=bufs)
+        st = br.stats.copy()
+        for p, (_, proto, v) in zip(planners, pairs):
+            replan_tick(p, proto, v, t)
+        tick[0] += 1
+        return st, br.kernel_ms, int(br.ok.sum())
+
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    pops, kms, oks, alg = 0, [], 0, []
+    for _ in range(args.steps):
+        st, k, ok = step()
+        pops += int(st["pops"].sum())
+        kms.append(k)
+        oks += ok
+        alg.append(algorithmic_bytes(st, args.obstacles))
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    elapsed, pops_all = reduce_over_ranks(dist, elapsed, pops, f"cuda:{device}")
+    out = None
+    if rank == 0:
+        avg_k = float(np.mean(kms))
+        achieved = float(np.mean(alg)) / (avg_k * 1e-3) / 1e9
+        out = {
+            "metric": "Hybrid A* node expansions/sec + plan latency, 1024x1024x72 grid",
+            "value": pops_all / elapsed, "unit": "expansions/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (SURVEY.md §8d cfg5 generator; pair ids seed the boxes, goals and box velocities)",
+            "config": {"workload": f"cfg5: {args.grid}x{args.grid}x{args.bins} grid, {args.obstacles} moving boxes, "
+                                   f"{P} start/goal pairs per GPU replanned every 50 ms tick without reset",
+                       "grid": args.grid, "angle_bins": args.bins, "obstacles": args.obstacles, "pairs_per_gpu": P,
+                       "global_batch": P * world, "parallelism": f"pair-sharded x{world}"},
+            "replan_latency_ms": avg_k, "tick_ms": elapsed / args.steps * 1e3,
+            "tick_budget_ms": 50.0, "success_rate": oks / (P * args.steps), "setup_s_per_gpu": t_setup,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": "hastar_search_kernel",
+                         "kernel_ms": avg_k, "alg_bytes_per_launch": float(np.mean(alg))},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_cfg5(pairs, args.cpu_seconds, args.warmup + args.steps)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    if out is not None:
+        print(json.dumps(out))
+
+
+def cpu_baseline_cfg5(pairs, budget_s, ticks):
+    """The oracle replaying the same pairs' replan loops (1 thread, find_path timed only)."""
+    from oracle.pyoracle import OraclePlanner
+    from tests.scenarios import drive, replan_tick, replan_tick_inputs
+    pops, wall, n = 0, 0.0, 0
+    for cfg, proto, v in pairs:
+        o = OraclePlanner(cfg)
+        drive(o, proto)
+        for t in range(ticks):
+            r = o.find_path(proto["vel"], replan_tick_inputs(proto, v, t)[0])
+            pops += r["stats"]["pops"]
+            wall += r["wall_ms"] * 1e-3
+            replan_tick(o, proto, v, t)
+        o.close()
+        n += 1
+        if wall >= budget_s:
+            break
+    return {"value": pops / wall if wall > 0 else None, "unit": "expansions/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} pairs x {ticks} ticks (same call sequence as the GPU run), find_path only, "
+                      f"1 thread (oracle/hastar_oracle.cpp)"}
 
 
 def cpu_baseline(cfgs, gpu_results, budget_s, replans):

@@ -86,6 +86,9 @@ int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3
 /* reset() (HybridAStar.cpp:49-52): clears the holonomic A* memo. */
 int hastar_reset(hastar_handle h);
 
+/* reset() of n planners in one call (batch drivers; same effect as n hastar_reset calls). */
+int hastar_reset_batch(const hastar_handle* hs, int n);
+
 /* update_obstacles(obstacles, confidence, apf_added_radius) (HybridAStar.cpp:29-33):
  * boxes = n x {center_x, center_y, dimension_x, dimension_y} (Obstacle.h:16-21). */
 int hastar_update_boxes(hastar_handle h, const float* boxes, const float* confidence, int n,

@@ -532,6 +532,14 @@ int hastar_reset(hastar_handle h) {
   return HASTAR_OK;
 }
 
+// reset() of n planners (one call instead of n, for batch drivers)
+int hastar_reset_batch(const hastar_handle* hs, int n) {
+  if (!hs || n < 0) return fail(HASTAR_EINVAL, "bad argument");
+  for (int i = 0; i < n; ++i)
+    if (int rc = hastar_reset(hs[i])) return rc;
+  return HASTAR_OK;
+}
+
 // Grid2D::update_obstacles() (Grid2D.cpp:197-208)
 int hastar_decay(hastar_handle h) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");

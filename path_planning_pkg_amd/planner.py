@@ -43,6 +43,7 @@ def load_library():
     L.hastar_destroy.argtypes = [vp]
     L.hastar_update_goal.argtypes = [vp, fp, fp]
     L.hastar_reset.argtypes = [vp]
+    L.hastar_reset_batch.argtypes = [C.POINTER(C.c_void_p), C.c_int]
     L.hastar_update_boxes.argtypes = [vp, fp, fp, C.c_int, C.c_float]
     L.hastar_update_lines.argtypes = [vp, fp, fp, C.c_int, C.c_float]
     L.hastar_decay.argtypes = [vp]
@@ -241,25 +242,49 @@ class BatchResult:
                     curvature=self.curv[i, :k].copy(), stats=st)
 
 
-def find_path_batch_arrays(planners, vels, starts, cap=4096):
-    """hastar_find_path_batch with array outputs (BatchResult)."""
+class BatchBuffers:
+    """Reusable host-side arguments/outputs of hastar_find_path_batch for a fixed list of
+    planners (a replan loop calls the batch every tick: no per-call allocation, no page
+    faults on fresh output arrays)."""
+
+    def __init__(self, planners, cap=4096):
+        n = len(planners)
+        self.n, self.cap = n, cap
+        self.hs = (C.c_void_p * n)(*[p.h.value for p in planners])
+        self.xyh = np.empty((n, cap, 3), np.float32)
+        self.curv = np.empty((n, cap), np.float32)
+        self.ln = np.zeros(n, np.int32)
+        self.ok = np.zeros(n, np.int32)
+        self.cost = np.zeros(n, np.float32)
+        self.stats = (HastarStats * n)()
+        self.st = np.ctypeslib.as_array(self.stats)
+
+
+def reset_batch(planners_or_buffers):
+    """reset() of every planner in one C call (hastar_reset_batch)."""
+    b = planners_or_buffers
+    if isinstance(b, BatchBuffers):
+        hs, n = b.hs, b.n
+    else:
+        n = len(b)
+        hs = (C.c_void_p * n)(*[p.h.value for p in b])
+    _check(load_library().hastar_reset_batch(hs, n))
+
+
+def find_path_batch_arrays(planners, vels, starts, cap=4096, buffers=None):
+    """hastar_find_path_batch with array outputs (BatchResult).  With `buffers` (a
+    BatchBuffers of the same planners) the outputs are written into its arrays, which the
+    returned BatchResult then views (valid until the next call with those buffers)."""
     L = load_library()
-    n = len(planners)
-    hs = (C.c_void_p * n)(*[p.h.value for p in planners])
+    b = buffers if buffers is not None else BatchBuffers(planners, cap)
+    assert b.n == len(planners)
     v = _f32(vels)
-    s = _f32(starts, (n, 3))
-    xyh = np.empty((n, cap, 3), np.float32)
-    curv = np.empty((n, cap), np.float32)
-    ln = np.zeros(n, np.int32)
-    ok = np.zeros(n, np.int32)
-    cost = np.zeros(n, np.float32)
-    stats = (HastarStats * n)()
-    rc = L.hastar_find_path_batch(hs, n, fptr(v), fptr(s), fptr(xyh), fptr(curv), cap, iptr(ln), fptr(cost),
-                                  iptr(ok), stats)
+    s = _f32(starts, (b.n, 3))
+    rc = L.hastar_find_path_batch(b.hs, b.n, fptr(v), fptr(s), fptr(b.xyh), fptr(b.curv), b.cap, iptr(b.ln),
+                                  fptr(b.cost), iptr(b.ok), b.stats)
     if rc != HASTAR_EOVERFLOW:  # per-planner arena overflows are reported in stats["status"]
         _check(rc)
-    st = np.ctypeslib.as_array(stats)
-    return BatchResult(cost, ok, ln, xyh, curv, st, float(L.hastar_last_search_ms()))
+    return BatchResult(b.cost, b.ok, b.ln, b.xyh, b.curv, b.st, float(L.hastar_last_search_ms()))
 
 
 def find_path_batch(planners, vels, starts, cap=4096):

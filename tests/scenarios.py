@@ -63,3 +63,57 @@ def drive(planner, proto):
         if len(proto["boxes"]):
             planner.update_boxes(proto["boxes"], [proto["box_conf"]] * len(proto["boxes"]), proto["apf_r"])
     planner.reset()
+
+
+def replan_pairs(N, bins, K, n_pairs, seed, res=0.5, clear=8.0):
+    """n_pairs start/goal pairs on an N x N grid.  Each goal is uniform in
+    +-0.15 W with a uniform heading; the start lies U(0.3, 0.6) W behind it along that
+    heading (same heading).  K boxes per pair (sides U(1, 6) m, centres uniform over the
+    square spanned by the pair, rejected within `clear` m of start/goal) with per-box
+    velocities U(-2, 2) m/s per axis.  Returns [(cfg, proto, box_vel)]."""
+    W = N * res
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n_pairs):
+        g = rng.uniform(-0.15 * W, 0.15 * W, 2)
+        th = float(rng.uniform(-math.pi, math.pi))
+        d = float(rng.uniform(0.3, 0.6)) * W
+        s = g - d * np.array([math.cos(th), math.sin(th)])
+        lo, hi = np.minimum(s, g) - 0.2 * W, np.maximum(s, g) + 0.2 * W
+        boxes = []
+        while len(boxes) < K:
+            sx, sy = rng.uniform(1.0, 6.0, 2)
+            cx, cy = rng.uniform(lo, hi)
+            r = math.hypot(sx, sy) / 2
+            if math.hypot(cx - s[0], cy - s[1]) < clear + r or math.hypot(cx - g[0], cy - g[1]) < clear + r:
+                continue
+            boxes.append([cx, cy, sx, sy])
+        vel = rng.uniform(-2.0, 2.0, (K, 2)).astype(np.float32)
+        cfg = PlannerConfig(grid_size=N, num_angle_bins=bins, steering=steering_from_degrees([-30, -15, 0, 15, 30]))
+        proto = dict(goal=[f32(g[0]), f32(g[1]), f32(th)], start=[f32(s[0]), f32(s[1]), f32(th)], vel=2.0, cycles=5,
+                     lines=np.zeros((0, 4), np.float32), line_conf=0.6, line_width=1.25,
+                     boxes=np.array(boxes, np.float32), box_conf=0.75, apf_r=2.5)
+        out.append((cfg, proto, vel))
+    return out
+
+
+def replan_tick_inputs(proto, box_vel, tick, dt=0.05):
+    """Inputs of replan tick `tick` (0-based) of a cfg5 pair: the start pose advanced by
+    vel * dt per tick along its heading, and the boxes moved by box_vel * dt per tick.
+    Both are computed from tick 0 in float64 and rounded once, so every caller sees the
+    same float32 values."""
+    sx, sy, sh = proto["start"]
+    step = proto["vel"] * dt * tick
+    start = [f32(sx + step * math.cos(sh)), f32(sy + step * math.sin(sh)), f32(sh)]
+    boxes = proto["boxes"].astype(np.float64)
+    boxes[:, :2] += box_vel.astype(np.float64) * (dt * tick)
+    return start, boxes.astype(np.float32)
+
+
+def replan_tick(planner, proto, box_vel, tick):
+    """One tick of the L3 loop after its find_path (local_planner.cpp:241, 288): free-space
+    decay, then the moved boxes.  No reset: memo and stale node-map values carry over."""
+    _, boxes = replan_tick_inputs(proto, box_vel, tick + 1)
+    planner.decay()
+    planner.update_boxes(boxes, [proto["box_conf"]] * len(boxes), proto["apf_r"])
+

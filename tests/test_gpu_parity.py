@@ -213,6 +213,29 @@ def test_replans_without_reset(gpu, oracle_lib):
             p.update_boxes(boxes, [0.75] * len(boxes), 2.5)
 
 
+def test_replan_loop_batched(gpu, oracle_lib):
+    """cfg5 semantics at test size: several start/goal pairs replanned
+    together each tick (one batched launch), with decay + moved boxes between ticks and
+    no reset (local_planner.cpp:241,288,316).  Every pair, every tick, bit-exact."""
+    from tests.scenarios import replan_pairs, replan_tick, replan_tick_inputs
+    pairs = replan_pairs(256, 36, 12, 6, seed=21)
+    gs, os_ = [], []
+    for cfg, proto, _ in pairs:
+        g, o = both(cfg, gpu, oracle_lib)
+        drive(g, proto)
+        drive(o, proto)
+        gs.append(g)
+        os_.append(o)
+    bufs = gpu.BatchBuffers(gs, cap=4096)
+    for tick in range(4):
+        starts = [replan_tick_inputs(proto, v, tick)[0] for _, proto, v in pairs]
+        br = gpu.find_path_batch_arrays(gs, [proto["vel"] for _, proto, _ in pairs], starts, buffers=bufs)
+        for i, (o, (_, proto, v)) in enumerate(zip(os_, pairs)):
+            compare_results(br.result(i), o.find_path(proto["vel"], starts[i]), f"tick {tick} pair {i}")
+            replan_tick(gs[i], proto, v, tick)
+            replan_tick(o, proto, v, tick)
+
+
 def test_batch_equals_single(gpu, oracle_lib):
     cases = [synthetic(256, 36, 10, s) for s in (6, 7, 8)] + [harness()[:2]]
     planners, oracles = [], []
