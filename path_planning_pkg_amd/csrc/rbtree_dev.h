@@ -175,7 +175,10 @@ struct RBT : Acc {
     float yf = 0.0f;
     if constexpr (Acc::kPathWalk) {
       bool unused;
-      this->path_walk(k, f, false, &y, &yk, &yf, &unused);
+      int rj;
+      uint32_t rk;
+      float rf;
+      this->path_walk(k, f, false, &y, &yk, &yf, &unused, &rj, &rk, &rf);
       x = NIL;
     }
     while (x != NIL) {
@@ -201,8 +204,30 @@ struct RBT : Acc {
     uint32_t yk = 0;
     float yf = 0.0f;
     if constexpr (Acc::kPathWalk) {
-      this->path_walk(k, f, true, &y, &yk, &yf, &comp);
-      x = NIL;
+      // The walk also reports the deepest node where it turned right (rj; -1 if none).
+      // That node is decrement(y) when the walk ended by going left, and y is the
+      // leftmost node when it never turned right, so _M_get_insert_unique_pos needs no
+      // further tree access.
+      int rj;
+      uint32_t rk;
+      float rf;
+      this->path_walk(k, f, true, &y, &yk, &yf, &comp, &rj, &rk, &rf);
+      if (comp) {
+        if (rj < 0) {
+          *left = true;  // y == L(0)
+          return y;
+        }
+        if (rb_less(rk, rf, k, f)) {
+          *left = (y == 0) || rb_less(k, f, yk, yf);
+          return y;
+        }
+        return -2;
+      }
+      if (rb_less(yk, yf, k, f)) {
+        *left = (y == 0) || rb_less(k, f, yk, yf);
+        return y;
+      }
+      return -2;
     }
     while (x != NIL) {
       const Quad q = this->quad_at(x, depth++);
@@ -628,8 +653,10 @@ struct CachedAcc3 {
   // last node where it went left) and _M_get_insert_unique_pos (ins = true: go left iff
   // probe < node, remember the last node and the last decision), comparator
   // (ka != kb) && (fa < fb).  Outputs as RBT::find / RBT::insert_pos expect them.
+  // For insert walks, *rj_ / *rk_ / *rf_ = the deepest node where the walk turned right
+  // (rj = -1 if it never did).
   __device__ __forceinline__ void path_walk(uint32_t k, float f, bool ins, int* y_, uint32_t* yk_, float* yf_,
-                                            bool* comp_) {
+                                            bool* comp_, int* rj_, uint32_t* rk_, float* rf_) {
 #ifdef HASTAR_STAMPS
     const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -637,6 +664,9 @@ struct CachedAcc3 {
     uint32_t yk = 0;
     float yf = 0.0f;
     bool comp = true;
+    int rj = -1;
+    uint32_t rk = 0;
+    float rf = 0.0f;
     int x = P(0);
     if (x != NIL && plen > 0 && __builtin_amdgcn_readlane(cid, 0) == x) {
       const bool inpath = lane < plen;
@@ -652,6 +682,13 @@ struct CachedAcc3 {
         yk = (uint32_t)__builtin_amdgcn_readlane((int)ck, D);
         yf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), D));
         comp = (lmask >> D) & 1ull;
+        const uint64_t rmask = __ballot(inpath && !left) & (D >= 63 ? ~0ull : ((2ull << D) - 1));
+        if (rmask) {
+          const int h = 63 - __builtin_clzll(rmask);
+          rj = __builtin_amdgcn_readlane(cid, h);
+          rk = (uint32_t)__builtin_amdgcn_readlane((int)ck, h);
+          rf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), h));
+        }
       } else if (lmask) {
         const int h = 63 - __builtin_clzll(lmask);
         y = __builtin_amdgcn_readlane(cid, h);
@@ -668,6 +705,11 @@ struct CachedAcc3 {
         yk = q.key;
         yf = q.f;
         comp = rb_less(k, f, q.key, q.f);
+        if (!comp) {
+          rj = y;
+          rk = yk;
+          rf = yf;
+        }
         x = comp ? q.l : q.r;
       } else if (!rb_less(q.key, q.f, k, f)) {
         y = x;
@@ -687,6 +729,9 @@ struct CachedAcc3 {
     *yk_ = yk;
     *yf_ = yf;
     *comp_ = comp;
+    *rj_ = rj;
+    *rk_ = rk;
+    *rf_ = rf;
   }
   // a node just written in full by the caller (pool allocation): drop stale copies of
   // the index and cache the new contents (no HBM traffic)
