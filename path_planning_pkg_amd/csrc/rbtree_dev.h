@@ -524,6 +524,24 @@ struct CachedAcc3 {
     n_fill++;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+    // every lane loaded the same record: the cache lane takes the loaded vector registers
+    // as they are; the wave-uniform copies below are only materialised (readfirstlane)
+    // for the fields a caller actually uses (the rest is dead code after inlining)
+    if (lane == slot) {
+      cid = x;
+      ck = (uint32_t)a.x;
+      cf = __int_as_float(a.y);
+      cl = a.z;
+      cr = a.w;
+      cp = b.x;
+      cc = (uint32_t)b.y;
+      cg = __int_as_float(b.z);
+      cvm = __int_as_float(b.w);
+      cx = __int_as_float(d.x);
+      cy = __int_as_float(d.y);
+      ch = __int_as_float(d.z);
+      cpv = d.w;
+    }
     Node3 n;
     n.key = rb_uu((uint32_t)a.x);
 #ifdef HASTAR_STAMPS
@@ -540,7 +558,6 @@ struct CachedAcc3 {
     n.y = __int_as_float(rb_ui(d.y));
     n.h = __int_as_float(rb_ui(d.z));
     n.prev = rb_ui(d.w);
-    if (lane == slot) set_lane(x, n);
     return n;
   }
   __device__ __forceinline__ void set_lane(int x, const Node3& n) {
