@@ -68,7 +68,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("HASTAR_BENCH_BATCH", "16384")),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("HASTAR_BENCH_BATCH", "18432")),
                     help="planners (queries) per GPU")
     ap.add_argument("--grid", type=int, default=1024)
     ap.add_argument("--bins", type=int, default=72)
@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--pairs", type=int, default=64, help="cfg5: start/goal pairs per GPU")
     args = ap.parse_args()
 
+    # search arenas may take 92% of the HBM left after the planners' maps (library default 80%)
+    os.environ.setdefault("HASTAR_ARENA_FRAC", "0.92")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

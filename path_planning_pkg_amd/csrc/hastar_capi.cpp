@@ -196,13 +196,16 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
   const size_t b_prevl = align256((size_t)ASTAR_LDS_CAP * sizeof(int));
   const size_t per =
       b_open3 + b_closed3 + b_slots + b_open2 + b_closed2 + b_cell + b_gens + b_dub + b_dubc + b_chain + b_prevl;
-  // memory budget of the pool: HASTAR_ARENA_MB, else 80% of the free HBM
+  // memory budget of the pool: HASTAR_ARENA_MB, else HASTAR_ARENA_FRAC (default 0.8) of
+  // the free HBM
   size_t budget = 0;
   if (const char* e = std::getenv("HASTAR_ARENA_MB")) budget = (size_t)std::strtoull(e, nullptr, 10) << 20;
   if (budget == 0) {
     size_t fr = 0, tot = 0;
     HIPCHK(hipMemGetInfo(&fr, &tot));
-    budget = fr / 10 * 8;
+    double frac = 0.8;
+    if (const char* e = std::getenv("HASTAR_ARENA_FRAC")) frac = std::min(0.97, std::max(0.05, std::atof(e)));
+    budget = (size_t)((double)fr * frac);
   }
   const int n_want = n;
   n = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, budget / per));

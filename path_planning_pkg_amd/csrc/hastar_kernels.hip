@@ -73,13 +73,17 @@ __device__ __forceinline__ uint32_t slot_hash(uint32_t k) {
 
 // unordered_set<Node3D>::insert(*it).first (HybridAStar.cpp:110): the existing record of
 // the popped node's key, or a new copy of the popped open node.  *fresh tells which.
-__device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n, bool* fresh) {
+// The caller may issue the first probe early (closed3_probe) and pass it in.
+__device__ __forceinline__ v2u closed3_probe(const SearchCtx& c, uint32_t key, uint32_t* h) {
+  *h = slot_hash(key) & c.A->slots3_mask;
+  return *(const GAS v2u*)&gp(c.A->slots3)[*h];
+}
+__device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n, bool* fresh, uint32_t h, v2u first) {
   const SlotArena& A = *c.A;
-  uint32_t h = slot_hash(n.key) & A.slots3_mask;
   const uint32_t gbits = (c.gen3 & SLOT3_GEN_MASK) << SLOT3_IDX_BITS;
-  for (;;) {
+  for (bool at_first = true;; at_first = false) {
     GAS v2u* s = (GAS v2u*)&gp(A.slots3)[h];
-    const v2u sv = *s;  // {key, gi}
+    const v2u sv = at_first ? first : *s;  // {key, gi}
     if ((sv.y & ~SLOT3_IDX_MASK) != gbits) {
       *fresh = true;
       if (c.n_closed3 >= A.closed3_cap) return NIL;
@@ -902,8 +906,15 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     STAMP_T tp = STAMP_NOW();
     const int b = c.o3.begin();
     const Node3 top = c.o3.node(b);  // usually cached: the leftmost node was touched by the last walks
+    // the closed-set probe is issued first; its HBM latency overlaps the erase, which
+    // does not depend on it (HybridAStar.cpp:109-111 order is kept: the insert itself
+    // reads the popped node's fields, captured in `top`)
+    uint32_t ph;
+    const v2u p0 = closed3_probe(c, top.key, &ph);
+    c.o3.unlink(b);
+    tpool_free(c.o3, c.ps3, b);
     bool fresh;
-    const int ci = closed3_insert(c, top, &fresh);
+    const int ci = closed3_insert(c, top, &fresh, ph, p0);
     if (ci == NIL) { c.status = -75; break; }
     // a duplicate key expands the OLD record; a new record is the popped node itself
     Closed3 cur;
@@ -919,8 +930,6 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     } else {
       cur = gload(&gp(A.closed3)[ci]);
     }
-    c.o3.unlink(b);
-    tpool_free(c.o3, c.ps3, b);
     c.pops++;
     const int cx = key3_x(cur.key), cy = key3_y(cur.key), cbin = key3_bin(cur.key);
     dig = mix64(dig ^ digest_key(cur.key)) + (uint64_t)fbits(cur.g);
