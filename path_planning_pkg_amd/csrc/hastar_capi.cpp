@@ -81,18 +81,17 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // Arena requirements of one planner (the pool is sized for the maximum over a batch).
 struct ArenaReq {
-  int open3 = 0, closed3 = 0, open2 = 0, closed2 = 0, dub = 0, chain = 0;
+  int open3 = 0, closed3 = 0, open2 = 0, dub = 0, chain = 0;
   uint32_t slots = 1;
   size_t cells = 0;
   bool covers(const ArenaReq& o) const {
-    return open3 >= o.open3 && closed3 >= o.closed3 && open2 >= o.open2 && closed2 >= o.closed2 && dub >= o.dub &&
+    return open3 >= o.open3 && closed3 >= o.closed3 && open2 >= o.open2 && dub >= o.dub &&
            chain >= o.chain && slots >= o.slots && cells >= o.cells;
   }
   void merge(const ArenaReq& o) {
     open3 = std::max(open3, o.open3);
     closed3 = std::max(closed3, o.closed3);
     open2 = std::max(open2, o.open2);
-    closed2 = std::max(closed2, o.closed2);
     dub = std::max(dub, o.dub);
     chain = std::max(chain, o.chain);
     slots = std::max(slots, o.slots);
@@ -190,12 +189,12 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
   D.n_arenas = 0;
   const size_t b_open3 = align256((size_t)r.open3 * sizeof(Node3)), b_closed3 = align256((size_t)r.closed3 * sizeof(Closed3));
   const size_t b_slots = align256((size_t)r.slots * sizeof(Slot3)), b_open2 = align256((size_t)r.open2 * sizeof(Node2));
-  const size_t b_closed2 = align256((size_t)r.closed2 * sizeof(Closed2)), b_cell = align256(r.cells * sizeof(Cell2));
+  const size_t b_cell = align256(r.cells * sizeof(Cell2));
   const size_t b_gens = 256, b_dub = align256((size_t)r.dub * 3 * sizeof(float));
   const size_t b_dubc = align256((size_t)r.dub * sizeof(float)), b_chain = align256((size_t)r.chain * sizeof(int));
   const size_t b_prevl = align256((size_t)ASTAR_LDS_CAP * sizeof(int));
   const size_t per =
-      b_open3 + b_closed3 + b_slots + b_open2 + b_closed2 + b_cell + b_gens + b_dub + b_dubc + b_chain + b_prevl;
+      b_open3 + b_closed3 + b_slots + b_open2 + b_cell + b_gens + b_dub + b_dubc + b_chain + b_prevl;
   // memory budget of the pool: HASTAR_ARENA_MB, else HASTAR_ARENA_FRAC (default 0.8) of
   // the free HBM
   size_t budget = 0;
@@ -224,7 +223,6 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
     A.closed3 = reinterpret_cast<Closed3*>(q); q += b_closed3;
     A.slots3 = reinterpret_cast<Slot3*>(q); q += b_slots;
     A.open2 = reinterpret_cast<Node2*>(q); q += b_open2;
-    A.closed2 = reinterpret_cast<Closed2*>(q); q += b_closed2;
     A.cell2 = reinterpret_cast<Cell2*>(q); q += b_cell;
     A.gens = reinterpret_cast<uint32_t*>(q); q += b_gens;
     A.dub_xyh = reinterpret_cast<float*>(q); q += b_dub;
@@ -235,7 +233,6 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
     A.closed3_cap = r.closed3;
     A.slots3_mask = r.slots - 1;
     A.open2_cap = r.open2;
-    A.closed2_cap = r.closed2;
     A.cells = r.cells;
     A.dub_cap = r.dub;
     A.chain_cap = r.chain;
@@ -412,7 +409,6 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   const int astar_cap =
       p->max_astar_nodes > 0 ? p->max_astar_nodes : (int)std::min<size_t>(NN + 16, (size_t)65536);
   R.open2 = astar_cap + 1;
-  R.closed2 = (int)std::min<size_t>(NN, (size_t)1 << 30);
   R.cells = NN;
   int dub_cap = p->max_dubins_samples;
   if (dub_cap <= 0) {

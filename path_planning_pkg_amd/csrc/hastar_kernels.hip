@@ -51,7 +51,7 @@ struct SearchCtx {
   int lane;
   RBT<CachedAcc3> o3;        // outer open tree: HBM nodes behind a register node cache
   PoolState ps3, ps2;
-  int n_closed3, n_closed2;
+  int n_closed3;
   uint32_t gen3, gen2;
   long long pops, succ, apops, asearch, shots, amigr, apops_g;
   int status;
@@ -387,15 +387,15 @@ struct HbmAcc : AosAcc<Node2, GAS Node2*> {
   }
 };
 
-// AStar::update_visted + Grid2D::update_costs (AStar.cpp:209-218, Grid2D.cpp:219-227)
+// AStar::update_visted + Grid2D::update_costs (AStar.cpp:209-218, Grid2D.cpp:219-227):
+// the prev chain of closed records, which are the cells' own records
 __device__ __forceinline__ void memoise(SearchCtx& c, float total, int from) {
   const PlannerDev& P = *c.P;
-  const GAS Closed2* cl = gp(c.A->closed2);
+  const GAS Cell2* cells = gp(c.A->cell2);
   for (int i = from; i != NIL;) {
-    const Closed2 r = gload(&cl[i]);
-    const size_t cell = (size_t)(r.key >> 16) * P.N + (r.key & 0xffffu);
-    gp(P.visited)[cell] = (uint8_t)P.vgen;
-    gp(P.nm_f)[cell] = total - r.g;
+    const Cell2 r = gload(&cells[i]);
+    gp(P.visited)[i] = (uint8_t)P.vgen;
+    gp(P.nm_f)[i] = total - r.g;
     i = r.prev;
   }
 }
@@ -421,7 +421,6 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
   const SlotArena& A = *c.A;
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
-  GAS Closed2* cl = gp(A.closed2);
   GAS Cell2* cells = gp(A.cell2);
   const int cap = G ? A.open2_cap : A_CAP;
   while (!tr.empty()) {
@@ -435,8 +434,7 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     // one HBM round trip: the popped cell's closed state and prev link, and the
     // neighbour probes (bounds, occupancy, memo flag, node-map f, closed membership —
     // loop-invariant during this expansion; Grid2D::get_neighbors, Grid2D.cpp:72-96)
-    const uint32_t tgen = ufu(cells[tcell].cgen);
-    const int tcidx = ufi(cells[tcell].cidx);
+    const Cell2 tc = gload(&cells[tcell]);
     const int tprev = ufi(tr.PV(b));
     const int ni = tx + adx, nj = ty + ady;
     bool valid = false, vis = false, closed = false;
@@ -454,34 +452,28 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     tr.unlink(b);
     tpool_free(tr, c.ps2, b);
     // unordered_set::insert(*it).first (AStar.cpp:130): a duplicate expands the OLD record
-    int ci;
-    Closed2 cur;
-    if (tgen == c.gen2) {
-      ci = tcidx;
-      cur = gload(&cl[ci]);
-      cur.key = ufu(cur.key);
-      cur.g = uff(cur.g);
-      cur.f = uff(cur.f);
+    // (the cell's record; the popped node is of the same cell)
+    const int ci = (int)tcell;
+    float g0;
+    if (ufu(tc.cgen) == c.gen2) {
+      g0 = uff(tc.g);
     } else {
-      if (c.n_closed2 >= A.closed2_cap) { c.status = -75; *result = FLT_MAX; return true; }
-      ci = c.n_closed2++;
-      cur.key = top.key;
-      cur.g = top_g;
-      cur.f = top.f;
-      cur.prev = tprev;
-      gstore(&cl[ci], cur);
-      cells[tcell].cgen = c.gen2;
-      cells[tcell].cidx = ci;
+      g0 = top_g;
+      Cell2 rec;
+      rec.cgen = c.gen2;
+      rec.g = top_g;
+      rec.prev = tprev;
+      rec.oinfo = tc.oinfo;
+      gstore(&cells[tcell], rec);
     }
     c.apops++;
     if (G) c.apops_g++;
-    const int cx = (int)(cur.key >> 16), cy = (int)(cur.key & 0xffffu);
-    if (cx == P.goal_cx && cy == P.goal_cy) {
-      memoise(c, cur.f, ci);
-      *result = cur.f;
+    if (tx == P.goal_cx && ty == P.goal_cy) {
+      const float fgoal = g0 + euclid_h(P, tx, ty);  // the record's f (Node2D: f = g + h)
+      memoise(c, fgoal, ci);
+      *result = fgoal;
       return true;
     }
-    const float g0 = cur.g;
     const uint64_t vmask = __ballot(valid), vismask = __ballot(vis), cmask = __ballot(closed);
     if (!G) STAMP_ADD(8, t_pop);
     for (int k = 0; k < nact; ++k) {
@@ -574,7 +566,6 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
   const SlotArena& A = *c.A;
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
-  GAS Closed2* cl = gp(A.closed2);
   GAS Cell2* cells = gp(A.cell2);
   while (rg.n > 0) {
     if (c.ps2.next + 8 > A_CAP) return false;
@@ -584,8 +575,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     const float top_g = uff(tr.G(b));
     const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
     const uint32_t tcell = (uint32_t)tx * (uint32_t)P.N + (uint32_t)ty;
-    const uint32_t tgen = ufu(cells[tcell].cgen);
-    const int tcidx = ufi(cells[tcell].cidx);
+    const Cell2 tc = gload(&cells[tcell]);
     const int tprev = ufi(tr.PV(b));
     const int ni = tx + adx, nj = ty + ady;
     bool valid = false, vis = false, closed = false;
@@ -600,7 +590,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
       valid = occv < P.thr;
       vis = valid && visv == (uint8_t)P.vgen;
       closed = valid && cr.cgen == c.gen2;
-      if (cr.ogen == c.gen2) ohint = cr.oinfo;
+      if ((cr.oinfo >> CELL2_OGEN_SHIFT) == (c.gen2 & CELL2_OGEN_MASK)) ohint = cr.oinfo & CELL2_HINT_MASK;
     }
     // consume every probe before the first store of this pop, so that no later register
     // reuse has to wait on a store (vmcnt counts loads and stores in issue order)
@@ -609,33 +599,26 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     tr.unlink(b);
     free_lds(c, tr, b);
     ring_erase(L, rg, 0, lane);
-    int ci;
-    Closed2 cur;
-    if (tgen == c.gen2) {
-      ci = tcidx;
-      cur = gload(&cl[ci]);
-      cur.key = ufu(cur.key);
-      cur.g = uff(cur.g);
-      cur.f = uff(cur.f);
+    const int ci = (int)tcell;  // closed record = the cell's record
+    float g0;
+    if (ufu(tc.cgen) == c.gen2) {
+      g0 = uff(tc.g);
     } else {
-      if (c.n_closed2 >= A.closed2_cap) { c.status = -75; *result = FLT_MAX; return true; }
-      ci = c.n_closed2++;
-      cur.key = top.key;
-      cur.g = top_g;
-      cur.f = top.f;
-      cur.prev = tprev;
-      gstore(&cl[ci], cur);
-      cells[tcell].cgen = c.gen2;
-      cells[tcell].cidx = ci;
+      g0 = top_g;
+      Cell2 rec;
+      rec.cgen = c.gen2;
+      rec.g = top_g;
+      rec.prev = tprev;
+      rec.oinfo = tc.oinfo;
+      gstore(&cells[tcell], rec);
     }
     c.apops++;
-    const int cx = (int)(cur.key >> 16), cy = (int)(cur.key & 0xffffu);
-    if (cx == P.goal_cx && cy == P.goal_cy) {
-      memoise(c, cur.f, ci);
-      *result = cur.f;
+    if (tx == P.goal_cx && ty == P.goal_cy) {
+      const float fgoal = g0 + euclid_h(P, tx, ty);  // the record's f (Node2D: f = g + h)
+      memoise(c, fgoal, ci);
+      *result = fgoal;
       return true;
     }
-    const float g0 = cur.g;
     STAMP_ADD(8, t_pop);
     // The expansion's HBM stores (node-map f of inserted cells, prev links of new nodes) are
     // collected in lane k and issued together after the loop: a global store inside the
@@ -653,8 +636,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
           gp(P.nm_f)[st_cell] = st_f;
           if (st_node != NIL) {
             gp(A.prevl)[st_node] = ci;
-            cells[st_cell].ogen = c.gen2;
-            cells[st_cell].oinfo = st_hint;
+            cells[st_cell].oinfo = ((c.gen2 & CELL2_OGEN_MASK) << CELL2_OGEN_SHIFT) | st_hint;
           }
         }
         STAMP_T t_m = STAMP_NOW();
@@ -737,8 +719,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
       gp(P.nm_f)[st_cell] = st_f;
       if (st_node != NIL) {
         gp(A.prevl)[st_node] = ci;
-        cells[st_cell].ogen = c.gen2;
-        cells[st_cell].oinfo = st_hint;
+        cells[st_cell].oinfo = ((c.gen2 & CELL2_OGEN_MASK) << CELL2_OGEN_SHIFT) | st_hint;
       }
     }
     wave_lds_sync();
@@ -758,7 +739,6 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   gp(P.nm_f)[s_cell] = h0;  // Grid2D::set_start_node_grid -> Node2D::soft_reset
   c.asearch++;
   c.gen2++;
-  c.n_closed2 = 0;
   c.ps2.next = 1;
   c.ps2.free = NIL;
   RBT<LdsAcc> tl;
@@ -774,8 +754,7 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
     int n0;
     insert_lds(c, tl, L, rg, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL, none, at0, &n0);
     gp(A.prevl)[n0] = NIL;
-    gp(A.cell2)[s_cell].ogen = c.gen2;
-    gp(A.cell2)[s_cell].oinfo = (uint32_t)n0;
+    gp(A.cell2)[s_cell].oinfo = ((c.gen2 & CELL2_OGEN_MASK) << CELL2_OGEN_SHIFT) | (uint32_t)n0;
   }
   wave_lds_sync();
   const int nact = P.diag ? 8 : 4;
@@ -861,7 +840,6 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
   c.o3.reset_cache();
   closed3_next_gen(c);
   c.n_closed3 = 0;
-  c.n_closed2 = 0;
   c.pops = c.succ = c.apops = c.asearch = c.shots = c.amigr = c.apops_g = 0;
   c.status = 0;
   c.o3.clear();

@@ -55,24 +55,25 @@ struct alignas(16) Node2 {
   int prev;               // index into the A* closed records of the current search
 };
 
-// Holonomic A* closed record (unordered_set<Node2D>, AStar.h:71-72).
-struct alignas(16) Closed2 {
-  uint32_t key;
-  float g, f;
-  int prev;
-};
-
 // Per-cell record of the inner A* (slot arena, N*N, generation-stamped so a new search
-// needs no clearing): closed membership (cgen == search generation -> closed record cidx)
-// and a hint for the open tree (ogen == generation -> the cell's last inserted open node
-// is onode = oinfo & 0xffff; bit 16 set once a second node of the cell was inserted while
-// another was still open).
+// needs no clearing).  It is also the search's closed record of the cell
+// (unordered_set<Node2D>, AStar.h:71-72): a cell is closed at most once per search, so
+// the record lives at the cell's index and `prev` links are cell indices.
+//   cgen == search generation  -> closed, with the popped node's g and prev cell;
+//   oinfo = (generation & 0x7fff) << 17 | hint: the cell's last inserted open node of the
+//   LDS tree (bits 0-15) and bit 16, set once a second node of the cell was inserted while
+//   another was still open.  A hint whose 15-bit generation matches a stale search is
+//   harmless: it is only used after checking the node's key (and `dup` only forces the
+//   exact scan).
 struct alignas(16) Cell2 {
   uint32_t cgen;
-  int cidx;
-  uint32_t ogen;
+  float g;
+  int prev;
   uint32_t oinfo;
 };
+constexpr int CELL2_OGEN_SHIFT = 17;
+constexpr uint32_t CELL2_OGEN_MASK = 0x7fffu;
+constexpr uint32_t CELL2_HINT_MASK = 0x1ffffu;
 
 // Closed-set hash slot (open addressing).  gi = generation (12 bits) << 20 | record
 // index; a slot is live iff its generation is the search's, so clear() is O(1).  The
@@ -149,8 +150,7 @@ struct SlotArena {
   Closed3* closed3; int closed3_cap; int pad1;
   Slot3* slots3;    uint32_t slots3_mask; int pad2;
   Node2* open2;     int open2_cap;   int pad3;
-  Closed2* closed2; int closed2_cap; int pad4;
-  Cell2* cell2;     // N*N per-cell records of the current inner A* search
+  Cell2* cell2;     // N*N per-cell records (closed state + open hint) of the current inner A* search
   size_t cells;     // capacity of cell2 (max N*N served)
   uint32_t* gens;   // [0] closed-set generation, [1] A* closed generation
   float* dub_xyh; float* dub_curv; int dub_cap; int pad5;
