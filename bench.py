@@ -68,7 +68,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("HASTAR_BENCH_BATCH", "20480")),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("HASTAR_BENCH_BATCH", "23552")),
                     help="planners (queries) per GPU")
     ap.add_argument("--grid", type=int, default=1024)
     ap.add_argument("--bins", type=int, default=72)

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -78,6 +79,13 @@ hipError_t dalloc(T** p, size_t n) {
   return hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(n, 1) * sizeof(T));
 }
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+struct DeviceCtx;
+template <class T>
+hipError_t side_alloc(DeviceCtx& D, T** p, size_t n);
+template <class T>
+void side_free(DeviceCtx& D, T* p, size_t n);
+// 32-bit words of a visited bitmap of NN cells, rounded up to 16-byte stores
+size_t bitmap_words(size_t NN) { return ((NN + 31) / 32 + 3) & ~(size_t)3; }
 
 // Arena requirements of one planner (the pool is sized for the maximum over a batch).
 struct ArenaReq {
@@ -99,9 +107,53 @@ struct ArenaReq {
   }
 };
 
+// Sub-allocator for the planners' small device buffers (visited bitmap, motion tables, path
+// output, obstacle lists).  hipMalloc hands out 2-MiB granules, so a planner whose maps
+// (2 x 4 MiB at N = 1024) shared one allocation with these few hundred KiB used 10 MiB;
+// here the maps are one exact allocation and the rest is carved from 64-MiB chunks.
+// Freed blocks are kept per size and reused (planners of one configuration all ask for
+// the same sizes).
+struct SidePool {
+  std::mutex mu;
+  std::vector<void*> chunks;
+  char* cur = nullptr;
+  size_t left = 0;
+  std::unordered_map<size_t, std::vector<void*>> freed;
+  static size_t round(size_t b) { return (std::max<size_t>(b, 1) + 255) & ~(size_t)255; }
+  hipError_t alloc(void** p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu);
+    bytes = round(bytes);
+    auto it = freed.find(bytes);
+    if (it != freed.end() && !it->second.empty()) {
+      *p = it->second.back();
+      it->second.pop_back();
+      return hipSuccess;
+    }
+    if (left < bytes) {
+      const size_t sz = std::max<size_t>(bytes, (size_t)64 << 20);
+      void* c = nullptr;
+      const hipError_t e = hipMalloc(&c, sz);
+      if (e != hipSuccess) return e;
+      chunks.push_back(c);
+      cur = static_cast<char*>(c);
+      left = sz;
+    }
+    *p = cur;
+    cur += bytes;
+    left -= bytes;
+    return hipSuccess;
+  }
+  void release(void* p, size_t bytes) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(mu);
+    freed[round(bytes)].push_back(p);
+  }
+};
+
 // Everything a device shares among its planners.
 struct DeviceCtx {
   std::mutex mu;
+  SidePool side;
   bool init = false;
   int device = -1;
   hipStream_t stream = nullptr;
@@ -135,8 +187,19 @@ struct DeviceCtx {
   float* h_pxyh = nullptr;
   float* h_pcurv = nullptr;
   size_t pts_cap = 0;
+  uint32_t** d_ptrs = nullptr;  // bitmap pointers of a batched reset
+  size_t ptrs_cap = 0;
 };
 DeviceCtx g_dev[64];
+
+template <class T>
+hipError_t side_alloc(DeviceCtx& D, T** p, size_t n) {
+  return D.side.alloc(reinterpret_cast<void**>(p), std::max<size_t>(n, 1) * sizeof(T));
+}
+template <class T>
+void side_free(DeviceCtx& D, T* p, size_t n) {
+  D.side.release(p, std::max<size_t>(n, 1) * sizeof(T));
+}
 
 int device_ctx(int dev, DeviceCtx** out) {
   DeviceCtx& D = g_dev[dev & 63];
@@ -275,7 +338,9 @@ struct hastar_handle_s {
   float* d_seq = nullptr;
   float* d_wid = nullptr;
   int lp_cap = 0, wid_cap = 0;
-  void* slab = nullptr;         // the planner's persistent state, one allocation
+  void* slab = nullptr;         // the planner's maps (log-odds + node-map f), one exact allocation
+  void* side = nullptr;         // bitmap, motion tables, path output: from the device's SidePool
+  size_t side_bytes = 0;
   SearchResult last{};
   bool have_last = false;
   long long last_pops = 0;      // work estimate for longest-first scheduling
@@ -286,13 +351,17 @@ static void free_handle(hastar_handle h) {
   hipSetDevice(h->device);
   if (h->dc) hipStreamSynchronize(h->dc->stream);
   if (h->slab) hipFree(h->slab);
-  if (h->d_rp) hipFree(h->d_rp);
-  if (h->d_dl) hipFree(h->d_dl);
-  if (h->d_ids) hipFree(h->d_ids);
-  if (h->d_lp) hipFree(h->d_lp);
-  if (h->d_seq) hipFree(h->d_seq);
-  if (h->d_wid) hipFree(h->d_wid);
-  if (h->desc.apf) hipFree(h->desc.apf);
+  if (h->dc) {
+    DeviceCtx& DC = *h->dc;
+    DC.side.release(h->side, h->side_bytes);
+    side_free(DC, h->d_rp, (size_t)h->rp_cap * 4);
+    side_free(DC, h->d_dl, (size_t)h->rp_cap);
+    side_free(DC, h->d_ids, (size_t)h->ids_cap);
+    side_free(DC, h->d_lp, (size_t)h->lp_cap * 9);
+    side_free(DC, h->d_seq, (size_t)h->lp_cap * 100);
+    side_free(DC, h->d_wid, (size_t)h->wid_cap);
+    side_free(DC, h->desc.apf, (size_t)h->apf_cap * 3);
+  }
   delete h;
 }
 
@@ -423,20 +492,28 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   // truncated).
   D.out_cap = dub_cap + std::min(h->max_pops + 2, 8 * N + 64);
 
-  // the planner's persistent state: one allocation
-  const size_t b_occ = align256(NN * sizeof(float)), b_nm = align256(NN * sizeof(float)), b_vis = align256(NN);
+  // the planner's persistent state: the two N x N maps in one exact allocation (8 MiB at
+  // N = 1024, a whole number of 2-MiB granules), everything else from the device's pool
+  const size_t b_occ = align256(NN * sizeof(float)), b_nm = align256(NN * sizeof(float));
+  const size_t b_vis = align256(bitmap_words(NN) * sizeof(uint32_t));
   const size_t b_off = align256(off.size() * sizeof(float)), b_s = align256((size_t)ns * sizeof(float));
   const size_t b_ox = align256((size_t)D.out_cap * 3 * sizeof(float)), b_oc = align256((size_t)D.out_cap * sizeof(float));
-  const size_t total = b_occ + b_nm + b_vis + b_off + 3 * b_s + b_ox + b_oc;
-  if (hipMalloc(&h->slab, total) != hipSuccess) {
+  h->side_bytes = b_vis + b_off + 3 * b_s + b_ox + b_oc;
+  if (hipMalloc(&h->slab, b_occ + b_nm) != hipSuccess) {
     h->slab = nullptr;
     free_handle(h);
     return fail(HASTAR_ENOMEM, "planner state allocation failed");
   }
+  if (dc->side.alloc(&h->side, h->side_bytes) != hipSuccess) {
+    h->side = nullptr;
+    free_handle(h);
+    return fail(HASTAR_ENOMEM, "planner side-buffer allocation failed");
+  }
   char* q = static_cast<char*>(h->slab);
   D.occ = reinterpret_cast<float*>(q); q += b_occ;
   D.nm_f = reinterpret_cast<float*>(q); q += b_nm;
-  D.visited = reinterpret_cast<uint8_t*>(q); q += b_vis;
+  q = static_cast<char*>(h->side);
+  D.visited = reinterpret_cast<uint32_t*>(q); q += b_vis;
   D.off = reinterpret_cast<float*>(q); q += b_off;
   D.dth = reinterpret_cast<float*>(q); q += b_s;
   D.act_cost = reinterpret_cast<float*>(q); q += b_s;
@@ -448,8 +525,7 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   D.n_apf = 0;
   hipStream_t st = dc->stream;
   hipError_t he = hipMemsetAsync(D.occ, 0, NN * sizeof(float), st);
-  D.vgen = 1;
-  if (he == hipSuccess) he = hipMemsetAsync(D.visited, 0, NN, st);
+  if (he == hipSuccess) he = hipMemsetAsync(D.visited, 0, bitmap_words(NN) * sizeof(uint32_t), st);
   if (he == hipSuccess) he = hipMemcpyAsync(D.off, off.data(), off.size() * sizeof(float), hipMemcpyHostToDevice, st);
   if (he == hipSuccess) he = hipMemcpyAsync(D.dth, dth.data(), ns * sizeof(float), hipMemcpyHostToDevice, st);
   if (he == hipSuccess) he = hipMemcpyAsync(D.act_cost, cost.data(), ns * sizeof(float), hipMemcpyHostToDevice, st);
@@ -519,23 +595,43 @@ int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3
 int hastar_reset(hastar_handle h) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
-  // the memo flags are generation-stamped: reset is a new generation; the map is only
-  // cleared when the 8-bit generation wraps
-  PlannerDev& D = h->desc;
-  if (D.vgen >= 255) {
-    HIPCHK(hipMemsetAsync(D.visited, 0, (size_t)D.N * D.N, h->dc->stream));
-    D.vgen = 1;
-  } else {
-    D.vgen++;
-  }
+  // the memo flags are a bitmap (N*N / 8 bytes): reset clears it
+  const PlannerDev& D = h->desc;
+  HIPCHK(hipMemsetAsync(D.visited, 0, bitmap_words((size_t)D.N * D.N) * sizeof(uint32_t), h->dc->stream));
   return HASTAR_OK;
 }
 
-// reset() of n planners (one call instead of n, for batch drivers)
+// reset() of n planners: one kernel clears every bitmap of a device (planners grouped by
+// device and grid size)
 int hastar_reset_batch(const hastar_handle* hs, int n) {
   if (!hs || n < 0) return fail(HASTAR_EINVAL, "bad argument");
   for (int i = 0; i < n; ++i)
-    if (int rc = hastar_reset(hs[i])) return rc;
+    if (!hs[i]) return fail(HASTAR_EINVAL, "null handle");
+  std::vector<char> done(n, 0);
+  for (int i = 0; i < n; ++i) {
+    if (done[i]) continue;
+    const int dev = hs[i]->device, N = hs[i]->desc.N;
+    std::vector<uint32_t*> ptrs;
+    for (int j = i; j < n; ++j)
+      if (!done[j] && hs[j]->device == dev && hs[j]->desc.N == N) {
+        ptrs.push_back(hs[j]->desc.visited);
+        done[j] = 1;
+      }
+    HIPCHK(hipSetDevice(dev));
+    DeviceCtx& DC = *hs[i]->dc;
+    std::lock_guard<std::mutex> lk(DC.mu);
+    if (ptrs.size() > DC.ptrs_cap) {
+      HIPCHK(hipStreamSynchronize(DC.stream));
+      if (DC.d_ptrs) hipFree(DC.d_ptrs);
+      DC.d_ptrs = nullptr;
+      DC.ptrs_cap = 0;
+      HIPCHK(hipMalloc(reinterpret_cast<void**>(&DC.d_ptrs), ptrs.size() * sizeof(uint32_t*)));
+      DC.ptrs_cap = ptrs.size();
+    }
+    // pageable source: the copy is staged before hipMemcpyAsync returns
+    HIPCHK(hipMemcpyAsync(DC.d_ptrs, ptrs.data(), ptrs.size() * sizeof(uint32_t*), hipMemcpyHostToDevice, DC.stream));
+    HIPCHK(launch_clear_bitmaps(DC.d_ptrs, (int)ptrs.size(), bitmap_words((size_t)N * N), DC.stream));
+  }
   return HASTAR_OK;
 }
 
@@ -576,20 +672,20 @@ int hastar_update_boxes(hastar_handle h, const float* boxes, const float* conf, 
   if (n > h->apf_cap || n > h->rp_cap) {
     HIPCHK(hipStreamSynchronize(DC.stream));  // buffers may still be read by queued work
     if (n > h->apf_cap) {
-      if (D.apf) hipFree(D.apf);
+      side_free(DC, D.apf, (size_t)h->apf_cap * 3);
       D.apf = nullptr;
       h->apf_cap = 0;
-      HIPCHK(dalloc(&D.apf, (size_t)n * 3));
+      HIPCHK(side_alloc(DC, &D.apf, (size_t)n * 3));
       h->apf_cap = n;
     }
     if (n > h->rp_cap) {
-      if (h->d_rp) hipFree(h->d_rp);
-      if (h->d_dl) hipFree(h->d_dl);
+      side_free(DC, h->d_rp, (size_t)h->rp_cap * 4);
+      side_free(DC, h->d_dl, (size_t)h->rp_cap);
       h->d_rp = nullptr;
       h->d_dl = nullptr;
       h->rp_cap = 0;
-      HIPCHK(dalloc(&h->d_rp, (size_t)n * 4));
-      HIPCHK(dalloc(&h->d_dl, (size_t)n));
+      HIPCHK(side_alloc(DC, &h->d_rp, (size_t)n * 4));
+      HIPCHK(side_alloc(DC, &h->d_dl, (size_t)n));
       h->rp_cap = n;
     }
   }
@@ -634,10 +730,10 @@ int hastar_update_boxes(hastar_handle h, const float* boxes, const float* conf, 
     first[n_layers] = n;
     if (n > h->ids_cap) {
       HIPCHK(hipStreamSynchronize(DC.stream));
-      if (h->d_ids) hipFree(h->d_ids);
+      side_free(DC, h->d_ids, (size_t)h->ids_cap);
       h->d_ids = nullptr;
       h->ids_cap = 0;
-      HIPCHK(dalloc(&h->d_ids, (size_t)n));
+      HIPCHK(side_alloc(DC, &h->d_ids, (size_t)n));
       h->ids_cap = n;
     }
     HIPCHK(hipMemcpyAsync(h->d_ids, ids.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice, DC.stream));
@@ -692,20 +788,20 @@ int hastar_update_lines(hastar_handle h, const float* lines, const float* conf, 
   if (n > h->lp_cap || (int)wid.size() > h->wid_cap) {
     HIPCHK(hipStreamSynchronize(DC.stream));
     if (n > h->lp_cap) {
-      if (h->d_lp) hipFree(h->d_lp);
-      if (h->d_seq) hipFree(h->d_seq);
+      side_free(DC, h->d_lp, (size_t)h->lp_cap * 9);
+      side_free(DC, h->d_seq, (size_t)h->lp_cap * stride);
       h->d_lp = nullptr;
       h->d_seq = nullptr;
       h->lp_cap = 0;
-      HIPCHK(dalloc(&h->d_lp, (size_t)n * 9));
-      HIPCHK(dalloc(&h->d_seq, (size_t)n * stride));
+      HIPCHK(side_alloc(DC, &h->d_lp, (size_t)n * 9));
+      HIPCHK(side_alloc(DC, &h->d_seq, (size_t)n * stride));
       h->lp_cap = n;
     }
     if ((int)wid.size() > h->wid_cap) {
-      if (h->d_wid) hipFree(h->d_wid);
+      side_free(DC, h->d_wid, (size_t)h->wid_cap);
       h->d_wid = nullptr;
       h->wid_cap = 0;
-      HIPCHK(dalloc(&h->d_wid, wid.size()));
+      HIPCHK(side_alloc(DC, &h->d_wid, wid.size()));
       h->wid_cap = (int)wid.size();
     }
   }
@@ -1010,8 +1106,9 @@ int hastar_debug_memo(hastar_handle h, float* f_out, unsigned char* visited_out)
   HIPCHK(hipStreamSynchronize(h->dc->stream));
   const size_t NN = (size_t)h->desc.N * h->desc.N;
   HIPCHK(hipMemcpy(f_out, h->desc.nm_f, NN * sizeof(float), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(visited_out, h->desc.visited, NN, hipMemcpyDeviceToHost));
-  for (size_t i = 0; i < NN; ++i) visited_out[i] = visited_out[i] == (unsigned char)h->desc.vgen ? 1 : 0;
+  std::vector<uint32_t> bits(bitmap_words(NN));
+  HIPCHK(hipMemcpy(bits.data(), h->desc.visited, bits.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < NN; ++i) visited_out[i] = (bits[i >> 5] >> (i & 31)) & 1u;
   return HASTAR_OK;
 }
 

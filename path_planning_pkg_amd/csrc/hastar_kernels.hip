@@ -394,7 +394,8 @@ __device__ __forceinline__ void memoise(SearchCtx& c, float total, int from) {
   const GAS Cell2* cells = gp(c.A->cell2);
   for (int i = from; i != NIL;) {
     const Cell2 r = gload(&cells[i]);
-    gp(P.visited)[i] = (uint8_t)P.vgen;
+    GAS uint32_t* vw = &gp(P.visited)[(uint32_t)i >> 5];
+    *vw = *vw | (1u << (i & 31));  // one wave owns the planner: a plain read-modify-write
     gp(P.nm_f)[i] = total - r.g;
     i = r.prev;
   }
@@ -442,11 +443,11 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     if (lane < nact && ni > -1 && ni < P.N && nj > -1 && nj < P.N) {
       const uint32_t cell = (uint32_t)ni * (uint32_t)P.N + (uint32_t)nj;
       const float occv = gp(P.occ)[cell];
-      const uint8_t visv = gp(P.visited)[cell];
+      const uint32_t visw = gp(P.visited)[cell >> 5];
       nf = gp(P.nm_f)[cell];
       const uint32_t cg = cells[cell].cgen;
       valid = occv < P.thr;
-      vis = valid && visv == (uint8_t)P.vgen;
+      vis = valid && ((visw >> (cell & 31)) & 1u);
       closed = valid && cg == c.gen2;
     }
     tr.unlink(b);
@@ -584,11 +585,11 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     if (lane < nact && ni > -1 && ni < P.N && nj > -1 && nj < P.N) {
       const uint32_t cell = (uint32_t)ni * (uint32_t)P.N + (uint32_t)nj;
       const float occv = gp(P.occ)[cell];
-      const uint8_t visv = gp(P.visited)[cell];
+      const uint32_t visw = gp(P.visited)[cell >> 5];
       nf = gp(P.nm_f)[cell];
       const Cell2 cr = gload(&cells[cell]);
       valid = occv < P.thr;
-      vis = valid && visv == (uint8_t)P.vgen;
+      vis = valid && ((visw >> (cell & 31)) & 1u);
       closed = valid && cr.cgen == c.gen2;
       if ((cr.oinfo >> CELL2_OGEN_SHIFT) == (c.gen2 & CELL2_OGEN_MASK)) ohint = cr.oinfo & CELL2_HINT_MASK;
     }
@@ -734,7 +735,7 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   const SlotArena& A = *c.A;
   const int lane = c.lane;
   const size_t s_cell = (size_t)si * P.N + sj;
-  if (gp(P.visited)[s_cell] == (uint8_t)P.vgen) return gp(P.nm_f)[s_cell];
+  if ((gp(P.visited)[s_cell >> 5] >> (s_cell & 31)) & 1u) return gp(P.nm_f)[s_cell];
   const float h0 = euclid_h(P, si, sj);
   gp(P.nm_f)[s_cell] = h0;  // Grid2D::set_start_node_grid -> Node2D::soft_reset
   c.asearch++;
@@ -993,7 +994,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
       occv = gp(P.occ)[cell];
       sh0 = slot_hash(skey) & A.slots3_mask;
       slot0 = *(const GAS v2u*)&gp(A.slots3)[sh0];
-      pvis = gp(P.visited)[cell];
+      pvis = (gp(P.visited)[cell >> 5] >> (cell & 31)) & 1u;
       pnf = gp(P.nm_f)[cell];
     }
     STAMP_ADD(16, tx);
@@ -1025,7 +1026,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
       }
     }
     const uint64_t closed_m = __ballot(isc);
-    const uint64_t vis_m = __ballot(kept && (uint8_t)pvis == (uint8_t)P.vgen);
+    const uint64_t vis_m = __ballot(kept && pvis != 0u);
     STAMP_ADD(21, tw);
     STAMP_ADD(1, tx);
     // ---- HybridAStar.cpp:159-193, successors in action order
@@ -1240,6 +1241,15 @@ __global__ __launch_bounds__(256) void k_gather_paths(const PlannerDev* __restri
   for (int t = threadIdx.x; t < n; t += blockDim.x) curv[o + t] = sc[t];
 }
 
+// AStar::reset (AStar.cpp:56-60) of many planners: clear their visited bitmaps
+// (ptrs: n bitmap pointers, words: 32-bit words per bitmap, a multiple of 4)
+__global__ __launch_bounds__(256) void k_clear_bitmaps(uint32_t* const* __restrict__ ptrs, int n, size_t words) {
+  for (int p = blockIdx.x; p < n; p += gridDim.x) {
+    uint4* w = reinterpret_cast<uint4*>(ptrs[p]);
+    for (size_t t = threadIdx.x; t < words / 4; t += blockDim.x) w[t] = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
 __global__ void k_init_nodemap(PlannerDev P) {
   const size_t NN = (size_t)P.N * P.N;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x) {
@@ -1449,6 +1459,10 @@ hipError_t launch_gather_paths(const PlannerDev* d_descs, const long long* d_off
                                float* curv, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_gather_paths, dim3(n), dim3(256), 0, st, d_descs, d_off, d_len, xyh, curv);
+  return hipGetLastError();
+}
+hipError_t launch_clear_bitmaps(uint32_t* const* ptrs, int n, size_t words, hipStream_t st) {
+  hipLaunchKernelGGL(k_clear_bitmaps, dim3(std::min(n, 8192)), dim3(256), 0, st, ptrs, n, words);
   return hipGetLastError();
 }
 hipError_t launch_init_nodemap(const PlannerDev& P, hipStream_t st) {

@@ -109,7 +109,7 @@ struct PlannerDev {
   // --- grid / vehicle constants (Grid2D.cpp:7-62, VehicleModel.cpp:7-47, HybridAStar.cpp:7-24)
   int N, n2, n45, diag;
   int bins, nsteer, na, shot_interval;
-  int shot_decay, n_apf, vgen, pad_i1;  // vgen: generation that marks visited cells
+  int shot_decay, n_apf, pad_i0, pad_i1;
   float res, thr, apf_rep, apf_ang;
   float ts, a_lat, a_lat2, prec;
   float r_min, step, ang_step, act_cost_diag;   // Dubins radius/step; 2D diagonal move cost
@@ -125,7 +125,7 @@ struct PlannerDev {
   // --- state arrays
   float* occ;            // N*N log-odds (_obstacle_map), row i = x cell
   float* nm_f;           // N*N Node2D::_cost_f of _node_map (A* memo + stale f)
-  uint8_t* visited;      // N*N AStar::_visted: cell is visited iff visited[cell] == vgen
+  uint32_t* visited;     // AStar::_visted as a bitmap: cell c is visited iff bit c & 31 of word c >> 5
   float* apf;            // n_apf x {x, y, r} (Grid3D::_apf_obstacles)
   float* off;            // nsteer x (bins + 1) x {dx, dy} (VehicleModel::_offset_xy + zero row)
   float* dth;            // nsteer  _offset_heading
