@@ -84,8 +84,8 @@ def main():
     ap.add_argument("--pairs", type=int, default=64, help="cfg5: start/goal pairs per GPU")
     args = ap.parse_args()
 
-    # search arenas may take 92% of the HBM left after the planners' maps (library default 80%)
-    os.environ.setdefault("HASTAR_ARENA_FRAC", "0.92")
+    # search arenas may take 95% of the HBM left after the planners' maps (library default 80%)
+    os.environ.setdefault("HASTAR_ARENA_FRAC", "0.95")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
