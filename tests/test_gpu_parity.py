@@ -236,6 +236,33 @@ def test_replan_loop_batched(gpu, oracle_lib):
             replan_tick(o, proto, v, tick)
 
 
+def test_reset_batch_equals_reset(gpu, oracle_lib):
+    """hastar_reset_batch (one kernel clearing every visited bitmap) == reset() per planner:
+    a warm memo is dropped, the stale node-map f values stay (AStar.cpp:56-60)."""
+    cases = [synthetic(256, 36, 10, s) for s in (12, 13, 14)]
+    gs, os_ = [], []
+    for cfg, proto in cases:
+        g, o = both(cfg, gpu, oracle_lib)
+        drive(g, proto)
+        drive(o, proto)
+        gs.append(g)
+        os_.append(o)
+    vels = [c[1]["vel"] for c in cases]
+    starts = [c[1]["start"] for c in cases]
+    gpu.find_path_batch(gs, vels, starts)
+    for (cfg, proto), o in zip(cases, os_):
+        o.find_path(proto["vel"], proto["start"])
+        o.reset()
+    gpu.reset_batch(gs)
+    res, _ = gpu.find_path_batch(gs, vels, starts)
+    for i, ((cfg, proto), o) in enumerate(zip(cases, os_)):
+        compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"after reset_batch {i}")
+        fg, vg = gs[i].memo()
+        fo, vo = o.get_memo()
+        assert_bits_equal(fg, fo, "memo f")
+        assert (vg == vo).all()
+
+
 def test_batch_equals_single(gpu, oracle_lib):
     cases = [synthetic(256, 36, 10, s) for s in (6, 7, 8)] + [harness()[:2]]
     planners, oracles = [], []
