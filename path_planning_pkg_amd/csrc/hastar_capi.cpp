@@ -212,7 +212,7 @@ int device_ctx(int dev, DeviceCtx** out) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, dev));
     D.resident_slots = search_slots_per_cu() * prop.multiProcessorCount;
-    HIPCHK(dalloc(&D.d_next, 1));
+    HIPCHK(dalloc(&D.d_next, 4));  // [0] work counter, [1] head placement, [2] head done
     D.init = true;
   }
   *out = &D;
@@ -946,7 +946,13 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   // raised issue priority for the head of the longest-first queue (HASTAR_PRIO_N overrides)
   int n_prio = std::max(1, slots / 8);
   if (const char* e = std::getenv("HASTAR_PRIO_N")) n_prio = std::atoi(e);
-  HIPCHK(launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, max_pops, st));
+  // Isolation of the queue head (the longest expected search) from the waves sharing its
+  // CU: when the batch outnumbers the slots, the batch time is the head's latency under
+  // load, and a CU of its own cuts that by ~7 % (3.37 -> 3.13 s at B = 23552,
+  // profiles/iso_sweep_r01g.txt) for ~5 of 1536 slots.  HASTAR_ISO = 0 off, 1 SIMD, 2 CU.
+  int iso = n > slots ? 2 : 0;
+  if (const char* e = std::getenv("HASTAR_ISO")) iso = std::atoi(e);
+  HIPCHK(launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, max_pops, iso, st));
   HIPCHK(hipEventRecord(DC.ev1, st));
   HIPCHK(hipMemcpyAsync(DC.h_results, DC.d_results, (size_t)n * sizeof(SearchResult), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));

@@ -1198,7 +1198,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
 __global__ __launch_bounds__(64, HASTAR_WAVES_PER_EU) void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners,
                                                            const SlotArena* __restrict__ arenas,
                                                            const int* __restrict__ order, int* __restrict__ next,
-                                                           int max_pops, int n_prio) {
+                                                           int max_pops, int n_prio, int iso) {
   __shared__ ApfStage apfs;
   __shared__ AStarLds alds;
   SearchCtx c;
@@ -1207,10 +1207,37 @@ __global__ __launch_bounds__(64, HASTAR_WAVES_PER_EU) void hastar_search_kernel(
   c.lane = threadIdx.x;
   c.gen3 = gp(A.gens)[0];
   c.gen2 = gp(A.gens)[1];
+  // Head isolation (iso = 1: SIMD, 2: CU).  Slot 0 runs queue entry 0, the longest expected
+  // search, and publishes its placement (HW_ID bits 4-15: SIMD, CU, SH, SE; XCC_ID); the
+  // other waves wait for that (bounded), and the ones sharing its SIMD / CU take no work,
+  // so the batch's critical search does not share issue slots.
+  bool first = true;
+  if (iso) {
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+    const uint32_t key = (((hw >> 4) & 0xfffu) & (iso == 2 ? ~0x3u : ~0u)) | (xcc << 12);
+    if (blockIdx.x == 0) {
+      if (c.lane == 0) __hip_atomic_store(&next[1], (int)(key + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      int head = 0;
+      for (int spin = 0; spin < 20000; ++spin) {
+        head = __hip_atomic_load(&next[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        head = __builtin_amdgcn_readfirstlane(head);
+        if (head != 0) break;
+        __builtin_amdgcn_s_sleep(8);
+      }
+      if (head == (int)(key + 1)) return;  // shares the head's SIMD / CU: no work
+    }
+  }
   for (;;) {
     int q = 0;
-    if (c.lane == 0) q = atomicAdd(next, 1);
-    q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
+    if (iso && first && blockIdx.x == 0) {
+      q = 0;
+    } else {
+      if (c.lane == 0) q = atomicAdd(next, 1);
+      q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
+    }
+    first = false;
     if (q >= n_planners) break;
     // the queue is ordered longest-expected-first; the head of it runs at raised issue
     // priority so the batch's stragglers are not slowed by the waves sharing their SIMD
@@ -1443,11 +1470,13 @@ __global__ __launch_bounds__(64) void k_test_dubins_path(PlannerDev P, float sx,
 
 // ------------------------------------------------------------- launch wrappers -------
 hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots, const int* d_order, int n_prio,
-                         int* d_next, int max_pops, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(d_next, 0, sizeof(int), st);
+                         int* d_next, int max_pops, int iso, hipStream_t st) {
+  // work counter 0 (1 with isolation: slot 0 takes queue entry 0 itself), no head yet
+  const int init[4] = {iso ? 1 : 0, 0, 0, 0};
+  hipError_t e = hipMemcpyAsync(d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(hastar_search_kernel, dim3(n_slots), dim3(64), 0, st, d_descs, n, d_arenas, d_order, d_next,
-                     max_pops, n_prio);
+                     max_pops, n_prio, iso);
   return hipGetLastError();
 }
 int search_slots_per_cu() {

@@ -263,6 +263,24 @@ def test_reset_batch_equals_reset(gpu, oracle_lib):
         assert (vg == vo).all()
 
 
+def test_batch_with_head_isolation(gpu, oracle_lib, monkeypatch):
+    """HASTAR_ISO=2 (slot 0 runs the queue head; waves sharing its CU take no work) and
+    fewer slots than planners: every result is still the oracle's."""
+    monkeypatch.setenv("HASTAR_ISO", "2")
+    monkeypatch.setenv("HASTAR_SLOTS", "3")
+    cases = [synthetic(128, 36, 6, s) for s in (31, 32, 33, 34, 35, 36, 37)]
+    gs, os_ = [], []
+    for cfg, proto in cases:
+        g, o = both(cfg, gpu, oracle_lib)
+        drive(g, proto)
+        drive(o, proto)
+        gs.append(g)
+        os_.append(o)
+    res, _ = gpu.find_path_batch(gs, [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases])
+    for i, ((cfg, proto), o) in enumerate(zip(cases, os_)):
+        compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"iso batch {i}")
+
+
 def test_batch_equals_single(gpu, oracle_lib):
     cases = [synthetic(256, 36, 10, s) for s in (6, 7, 8)] + [harness()[:2]]
     planners, oracles = [], []

@@ -23,6 +23,7 @@ ap.add_argument("--max-astar-nodes", type=int, default=0)
 ap.add_argument("--repeat", type=int, default=1, help="runs per batch (later runs use the longest-first order)")
 ap.add_argument("--prio", type=int, nargs="*", default=None, help="HASTAR_PRIO_N values to sweep")
 ap.add_argument("--slots", type=int, nargs="*", default=None, help="HASTAR_SLOTS values to sweep")
+ap.add_argument("--iso", type=int, nargs="*", default=None, help="HASTAR_ISO values to sweep (head isolation)")
 args = ap.parse_args()
 import os
 
@@ -55,7 +56,10 @@ for q in range(Bmax):
     cf.append(proto)
 print(json.dumps({"setup_s": time.time() - t, "planners": Bmax}), flush=True)
 for B in args.batches:
-  for prio, slots in [(p_, s_) for p_ in (args.prio or [None]) for s_ in (args.slots or [None])]:
+  for prio, slots, iso in [(p_, s_, i_) for p_ in (args.prio or [None]) for s_ in (args.slots or [None])
+                           for i_ in (args.iso or [None])]:
+   if iso is not None:
+       os.environ["HASTAR_ISO"] = str(iso)
    if prio is not None:
        os.environ["HASTAR_PRIO_N"] = str(prio)
    if slots is not None:
@@ -72,7 +76,7 @@ for B in args.batches:
         modes = [p.astar_modes() for p in ps[:B]]
         hbm = sum(m["astar_pops_hbm"] for m in modes)
         migr = sum(m["migrations"] for m in modes)
-        print(json.dumps({"batch": B, "prio": prio, "slots": slots, "rep": rep, "kernel_ms": kms, "wall_ms": wall * 1e3, "pops": pops, "astar_pops": apops,
+        print(json.dumps({"batch": B, "prio": prio, "slots": slots, "iso": iso, "rep": rep, "kernel_ms": kms, "wall_ms": wall * 1e3, "pops": pops, "astar_pops": apops,
                           "pops_per_s": pops / (kms * 1e-3), "astar_pops_hbm": hbm, "astar_migrations": migr,
                           "astar_searches": sum(r["stats"]["astar_searches"] for r in res), "overflow_seeds": bad[:20], "n_overflow": len(bad),
                           "max_work": max(r["stats"]["pops"] + r["stats"]["astar_pops"] for r in res),
