@@ -343,7 +343,7 @@ struct hastar_handle_s {
   size_t side_bytes = 0;
   SearchResult last{};
   bool have_last = false;
-  long long last_pops = 0;      // work estimate for longest-first scheduling
+  long long last_pops = 0;      // work estimate for longest-first scheduling (last search's duration)
 };
 
 static void free_handle(hastar_handle h) {
@@ -969,7 +969,9 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     hastar_handle h = hs[i];
     h->last = R;
     h->have_last = true;
-    h->last_pops = (long long)R.pops + R.astar_pops;
+    // longest-first key: the search's own duration (s_memrealtime ticks) — it weighs outer
+    // pops, inner A* pops and shots by what they actually cost, unlike a pop count
+    h->last_pops = R.t_end > R.t_start ? (long long)(R.t_end - R.t_start) : (long long)R.pops + R.astar_pops;
     ok[i] = R.ok;
     cost[i] = R.ok ? R.cost : FLT_MAX;
     fill_stats(R, stats ? &stats[i] : nullptr);

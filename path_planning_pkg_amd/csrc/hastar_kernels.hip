@@ -286,28 +286,39 @@ __device__ __forceinline__ void rank2(const AStarLds& L, const Ring& rg, float v
   rank_out(B, bB, cB, SR, n, i1, f1, i2, f2);
 }
 
+// Shift `cnt` consecutive ring entries by one slot (dir = -1: entries at ring offsets
+// [from, from + cnt) move to [from - 1, ...); dir = +1: they move to [from + 1, ...)).  All
+// of a lane's loads (one per 64 entries, at most A_CAP / 2 entries: the shorter side) are
+// issued before its stores, so the shift costs one LDS round trip instead of one per 64
+// entries.  Positions are ring offsets relative to `head` (masked by A_CAP - 1).
+constexpr int RING_CH = A_CAP / 2 / 64;  // chunks of 64 entries in the shorter side
+__device__ __forceinline__ void ring_shift(AStarLds& L, int head, int from, int cnt, int dir, int lane) {
+  constexpr int M = A_CAP - 1;
+  const int nch = (cnt + 63) >> 6;
+  int16_t v[RING_CH];
+#pragma unroll
+  for (int c = 0; c < RING_CH; ++c) {
+    const int i = c * 64 + lane;
+    v[c] = 0;
+    if (c < nch && i < cnt) v[c] = L.ring[(head + from + i) & M];
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int c = 0; c < RING_CH; ++c) {
+    const int i = c * 64 + lane;
+    if (c < nch && i < cnt) L.ring[(head + from + i + dir) & M] = v[c];
+  }
+  wave_lds_sync();
+}
+
 // ring insert of node x at rank r (shifts the shorter side by one)
 __device__ __forceinline__ void ring_insert(AStarLds& L, Ring& rg, int r, int x, int lane) {
   constexpr int M = A_CAP - 1;
   if (r < rg.n - r) {  // ranks [0, r) move one slot down, head - 1
+    if (r > 0) ring_shift(L, rg.head, 0, r, -1, lane);
     rg.head = (rg.head - 1) & M;
-    for (int c0 = 0; c0 < r; c0 += 64) {
-      const int i = c0 + lane;
-      int16_t v = 0;
-      if (i < r) v = L.ring[(rg.head + i + 1) & M];
-      wave_lds_sync();
-      if (i < r) L.ring[(rg.head + i) & M] = v;
-      wave_lds_sync();
-    }
-  } else {  // ranks [r, n) move one slot up, from the top
-    for (int c1 = rg.n; c1 > r; c1 -= 64) {
-      const int i = c1 - 1 - lane;
-      int16_t v = 0;
-      if (i >= r) v = L.ring[(rg.head + i) & M];
-      wave_lds_sync();
-      if (i >= r) L.ring[(rg.head + i + 1) & M] = v;
-      wave_lds_sync();
-    }
+  } else {  // ranks [r, n) move one slot up
+    if (rg.n > r) ring_shift(L, rg.head, r, rg.n - r, +1, lane);
   }
   if (lane == 0) L.ring[(rg.head + r) & M] = (int16_t)x;
   rg.n++;
@@ -318,24 +329,10 @@ __device__ __forceinline__ void ring_insert(AStarLds& L, Ring& rg, int r, int x,
 __device__ __forceinline__ void ring_erase(AStarLds& L, Ring& rg, int r, int lane) {
   constexpr int M = A_CAP - 1;
   if (r < rg.n - 1 - r) {  // ranks [0, r) move one slot up, head + 1
-    for (int c1 = r; c1 > 0; c1 -= 64) {
-      const int i = c1 - 1 - lane;
-      int16_t v = 0;
-      if (i >= 0) v = L.ring[(rg.head + i) & M];
-      wave_lds_sync();
-      if (i >= 0) L.ring[(rg.head + i + 1) & M] = v;
-      wave_lds_sync();
-    }
+    if (r > 0) ring_shift(L, rg.head, 0, r, +1, lane);
     rg.head = (rg.head + 1) & M;
   } else {  // ranks (r, n) move one slot down
-    for (int c0 = r + 1; c0 < rg.n; c0 += 64) {
-      const int i = c0 + lane;
-      int16_t v = 0;
-      if (i < rg.n) v = L.ring[(rg.head + i) & M];
-      wave_lds_sync();
-      if (i < rg.n) L.ring[(rg.head + i - 1) & M] = v;
-      wave_lds_sync();
-    }
+    if (rg.n - 1 > r) ring_shift(L, rg.head, r + 1, rg.n - 1 - r, -1, lane);
   }
   rg.n--;
 }
@@ -479,9 +476,9 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     if (!G) STAMP_ADD(8, t_pop);
     for (int k = 0; k < nact; ++k) {
       if (!((vmask >> k) & 1ull)) continue;
-      const float kcost = uff(shfl_f(acost, k));
+      const float kcost = rl_f(acost, k);
       if ((vismask >> k) & 1ull) {
-        const float tot = uff(shfl_f(nf, k)) + g0 + kcost;
+        const float tot = rl_f(nf, k) + g0 + kcost;
         STAMP_T t_m = STAMP_NOW();
         memoise(c, tot, ci);
         STAMP_ADD(12, t_m);
@@ -489,9 +486,9 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
         return true;
       }
       if ((cmask >> k) & 1ull) continue;
-      const int ki = ufi(shfl_i(ni, k)), kj = ufi(shfl_i(nj, k));
+      const int ki = rl_i(ni, k), kj = rl_i(nj, k);
       const uint32_t key = ((uint32_t)ki << 16) | (uint32_t)kj;
-      const float fprobe = uff(shfl_f(nf, k));  // stale _node_map f, as the reference reads it
+      const float fprobe = rl_f(nf, k);  // stale _node_map f, as the reference reads it
       STAMP_T t_f = STAMP_NOW();
       const int hit = tr.find(key, fprobe);
       if (!G) STAMP_ADD(9, t_f);
@@ -630,9 +627,9 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     bool st_on = false;
     for (int k = 0; k < nact; ++k) {
       if (!((vmask >> k) & 1ull)) continue;
-      const float kcost = uff(shfl_f(acost, k));
+      const float kcost = rl_f(acost, k);
       if ((vismask >> k) & 1ull) {
-        const float tot = uff(shfl_f(nf, k)) + g0 + kcost;
+        const float tot = rl_f(nf, k) + g0 + kcost;
         if (st_on) {  // this expansion's earlier node-map writes happen before the return
           gp(P.nm_f)[st_cell] = st_f;
           if (st_node != NIL) {
@@ -647,9 +644,9 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
         return true;
       }
       if ((cmask >> k) & 1ull) continue;
-      const int ki = ufi(shfl_i(ni, k)), kj = ufi(shfl_i(nj, k));
+      const int ki = rl_i(ni, k), kj = rl_i(nj, k);
       const uint32_t key = ((uint32_t)ki << 16) | (uint32_t)kj;
-      const float fprobe = uff(shfl_f(nf, k));  // stale _node_map f, as the reference reads it
+      const float fprobe = rl_f(nf, k);  // stale _node_map f, as the reference reads it
       const float gn = g0 + kcost;
       const float fn = gn + euclid_h(P, ki, kj);
       STAMP_T t_f = STAMP_NOW();
