@@ -70,7 +70,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("HASTAR_BENCH_BATCH", "23552")),
                     help="planners (queries) per GPU")
-    ap.add_argument("--grid", type=int, default=1024)
+    ap.add_argument("--grid", type=int, default=None, help="default 1024 (cfg3, cfg5) or 2048 (cfg4)")
     ap.add_argument("--bins", type=int, default=72)
     ap.add_argument("--obstacles", type=int, default=200)
     ap.add_argument("--max-pops", type=int, default=0, help="0 = library default (262144)")
@@ -78,11 +78,17 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-queries", type=int, default=3)
-    ap.add_argument("--workload", choices=("cfg3", "cfg5"), default="cfg3",
+    ap.add_argument("--workload", choices=("cfg3", "cfg4", "cfg5"), default="cfg3",
                     help="cfg3: batch of independent queries (default, the headline line); "
-                         "cfg5: 20 Hz replan loop of start/goal pairs (BASELINE.json configs[4])")
+                         "cfg4: 2048^2 queries with the map build row-sharded over the ranks + RCCL all-gather "
+                         "(BASELINE.json configs[3]); cfg5: 20 Hz replan loop of start/goal pairs (configs[4])")
+    ap.add_argument("--map-queries", type=int, default=16, help="cfg4: maps built both locally and row-sharded")
     ap.add_argument("--pairs", type=int, default=64, help="cfg5: start/goal pairs per GPU")
     args = ap.parse_args()
+    if args.grid is None:
+        args.grid = 2048 if args.workload == "cfg4" else 1024
+    if args.workload == "cfg4" and "--batch" not in sys.argv and "HASTAR_BENCH_BATCH" not in os.environ:
+        args.batch = 2048
 
     # search arenas may take 95% of the HBM left after the planners' maps (library default 80%)
     os.environ.setdefault("HASTAR_ARENA_FRAC", "0.95")
@@ -105,6 +111,8 @@ def main():
     if args.workload == "cfg5":
         return run_cfg5(args, gpu, dist, torch, rank, world, device)
     B = args.batch
+    map_build = map_build_phase(args, gpu, dist, torch, rank, world, device) if args.workload == "cfg4" else None
+
     def cfg_for(q):
         cfg, proto = synthetic(args.grid, args.bins, args.obstacles, seed=q + 1)
         cfg.values["max_pops"] = args.max_pops
@@ -186,8 +194,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (SURVEY.md §8d generator; seeds = query ids)",
-            "config": {"workload": f"cfg3: {args.grid}x{args.grid}x{args.bins} grid, {args.obstacles} box obstacles, "
-                                   f"batch of {B} independent queries per GPU, forward Dubins",
+            "config": {"workload": f"{args.workload}: {args.grid}x{args.grid}x{args.bins} grid, {args.obstacles} box "
+                                   f"obstacles, batch of {B} independent queries per GPU, forward Dubins"
+                                   + (", map build row-sharded over the ranks + RCCL all-gather (map_build)"
+                                      if map_build else ""),
                        "grid": args.grid, "angle_bins": args.bins, "obstacles": args.obstacles,
                        "queries_per_gpu": B, "global_batch": B * world, "parallelism": f"query-sharded x{world}"},
             "plan_latency_ms": float(np.median(lat)) if lat else None,
@@ -200,6 +210,8 @@ def main():
                          "kernel": "hastar_search_kernel", "kernel_ms": avg_kernel_ms,
                          "alg_bytes_per_launch": float(np.mean(alg_bytes))},
         }
+        if map_build:
+            out["map_build"] = map_build
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps)
     if dist:
@@ -207,6 +219,55 @@ def main():
         dist.destroy_process_group()
     if out is not None:
         print(json.dumps(out))
+
+
+def map_build_phase(args, gpu, dist, torch, rank, world, device):
+    """cfg4 (BASELINE.json configs[3]): the map build of `map_queries` queries
+    (the same query ids on every rank), timed two ways on the same planners: (a) local — each
+    rank builds the whole map (tests/scenarios.py::drive); (b) row-sharded — each rank builds
+    N/world rows, then one RCCL all-gather per map and an import
+    (path_planning_pkg_amd/shard.py).  Times are per map, max over ranks; `parity` says whether
+    every sharded map equals the local build bit for bit on every rank."""
+    from path_planning_pkg_amd.shard import drive_sharded
+    from tests.scenarios import drive, synthetic
+    M = args.map_queries
+    cases = [synthetic(args.grid, args.bins, args.obstacles, seed=q + 1) for q in range(M)]
+    loc = [gpu.HybridAStar(c, device=device) for c, _ in cases]
+    shd = [gpu.HybridAStar(c, device=device) for c, _ in cases]
+
+    def timed(fn):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize(device)
+        el = time.perf_counter() - t0
+        el, _ = reduce_over_ranks(dist, el, 0, f"cuda:{device}")
+        return el / M * 1e3
+
+    def local():
+        for p, (_, proto) in zip(loc, cases):
+            drive(p, proto)
+
+    def sharded():
+        for p, (_, proto) in zip(shd, cases):
+            drive_sharded(p, proto, rank, world, device)
+
+    t_loc = timed(local)
+    t_shd = timed(sharded)
+    same = all(np.array_equal(a.get_obstacles().view(np.uint32), b.get_obstacles().view(np.uint32))
+               for a, b in zip(loc, shd))
+    if dist:
+        flag = torch.tensor([0 if same else 1], device=f"cuda:{device}")
+        dist.all_reduce(flag)
+        same = int(flag[0]) == 0
+    for p in loc + shd:
+        p.close()
+    N = args.grid
+    return {"maps": M, "grid": N, "ranks": world, "local_ms_per_map": t_loc, "sharded_ms_per_map": t_shd,
+            "allgather_bytes_per_map": N * N * 4, "parity": bool(same),
+            "protocol": "update_goal + 5 x {decay, 200 boxes} per map (tests/scenarios.py::drive)"}
 
 
 def run_cfg5(args, gpu, dist, torch, rank, world, device):

@@ -125,6 +125,19 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel_init
 /* get_obstacles() (HybridAStar.cpp:62-65): copies the N x N log-odds map (row i = x cell). */
 int hastar_get_obstacles(hastar_handle h, float* out);
 
+/* ---- row-block sharding of the map build (no reference
+ * counterpart: the reference builds Grid2D::_grid (Grid2D.cpp:99-208) on one core) ----
+ * hastar_set_row_window limits hastar_decay / hastar_update_boxes / hastar_update_lines to
+ * rows [row0, row1) of the N x N log-odds map (row i = x cell); [0, N) is the default and
+ * the reference's behaviour.  The union of disjoint windows equals the full build bit for
+ * bit.  hastar_update_goal (relocate) ignores the window.  export/import copy rows between
+ * the planner's map and a DEVICE buffer on the planner's device (N floats per row) and
+ * return after the copy completed: a rank exports its block, the blocks are all-gathered
+ * (RCCL), and every rank imports the gathered map with row0 = 0, row1 = N. */
+int hastar_set_row_window(hastar_handle h, int row0, int row1);
+int hastar_export_rows(hastar_handle h, int row0, int row1, float* dst_device);
+int hastar_import_rows(hastar_handle h, int row0, int row1, const float* src_device);
+
 /* Grid size N of the handle. */
 int hastar_grid_size(hastar_handle h);
 

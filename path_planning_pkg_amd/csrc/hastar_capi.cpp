@@ -344,6 +344,7 @@ struct hastar_handle_s {
   SearchResult last{};
   bool have_last = false;
   long long last_pops = 0;      // work estimate for longest-first scheduling (last search's duration)
+  int row0 = 0, row1 = 0;       // map-build row window [row0, row1) (hastar_set_row_window); [0, N) by default
 };
 
 static void free_handle(hastar_handle h) {
@@ -400,6 +401,8 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   PlannerDev& D = h->desc;
   const int N = p->grid_size;
   D.N = N;
+  h->row0 = 0;
+  h->row1 = N;
   D.n2 = (int)std::round(N * 0.5);
   D.n45 = (int)std::round(N * 0.8);
   D.diag = p->grid_2d_allow_diag_moves ? 1 : 0;
@@ -639,7 +642,9 @@ int hastar_reset_batch(const hastar_handle* hs, int n) {
 int hastar_decay(hastar_handle h) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(launch_decay(h->desc.occ, (size_t)h->desc.N * h->desc.N, h->lp_free, h->lp_min, h->lp_max, h->dc->stream));
+  const size_t N = (size_t)h->desc.N;
+  HIPCHK(launch_decay(h->desc.occ + (size_t)h->row0 * N, (size_t)(h->row1 - h->row0) * N, h->lp_free, h->lp_min,
+                      h->lp_max, h->dc->stream));
   return HASTAR_OK;
 }
 
@@ -741,7 +746,7 @@ int hastar_update_boxes(hastar_handle h, const float* boxes, const float* conf, 
     if (int rc = scratch_acquire(DC, (size_t)D.N * D.N)) return rc;
     for (int l = 0; l < n_layers; ++l)
       HIPCHK(launch_raster_boxes(D.occ, DC.cnt, D.N, h->d_rp, h->d_dl, h->d_ids + first[l], first[l + 1] - first[l], cg,
-                                 sg, h->lp_min, h->lp_max, DC.stream));
+                                 sg, h->lp_min, h->lp_max, h->row0, h->row1, DC.stream));
   }
   return HASTAR_OK;
 }
@@ -811,7 +816,48 @@ int hastar_update_lines(hastar_handle h, const float* lines, const float* conf, 
   std::lock_guard<std::mutex> lk(DC.mu);
   if (int rc = scratch_acquire(DC, (size_t)D.N * D.N)) return rc;
   HIPCHK(launch_raster_lines(D.occ, DC.cnt, D.N, D.n45, D.n2, D.res, h->d_lp, h->d_seq, h->d_wid, stride, n, h->lp_min,
-                             h->lp_max, DC.stream));
+                             h->lp_max, h->row0, h->row1, DC.stream));
+  return HASTAR_OK;
+}
+
+// Row-block sharding of the map build.  Grid2D::_grid[i][j] is
+// stored row-major (i * N + j); the window limits decay and the box/line rasters to the rows
+// i in [row0, row1).  Every cell's update sequence is the reference's, restricted to the
+// window, so the union of disjoint windows built by different ranks equals the full build
+// bit for bit.  relocate (hastar_update_goal) stays global: call it before sharding.
+int hastar_set_row_window(hastar_handle h, int row0, int row1) {
+  if (!h) return fail(HASTAR_EINVAL, "null handle");
+  if (row0 < 0 || row1 < row0 || row1 > h->desc.N) return fail(HASTAR_EINVAL, "row window must satisfy 0 <= row0 <= row1 <= N");
+  h->row0 = row0;
+  h->row1 = row1;
+  return HASTAR_OK;
+}
+
+// Device-to-device copy of log-odds rows [row0, row1) into `dst` (N floats per row, a device
+// pointer on the planner's device).  Returns after the copy has completed.
+int hastar_export_rows(hastar_handle h, int row0, int row1, float* dst) {
+  if (!h || (!dst && row1 > row0)) return fail(HASTAR_EINVAL, "bad argument");
+  if (row0 < 0 || row1 < row0 || row1 > h->desc.N) return fail(HASTAR_EINVAL, "rows must satisfy 0 <= row0 <= row1 <= N");
+  HIPCHK(hipSetDevice(h->device));
+  const size_t N = (size_t)h->desc.N;
+  if (row1 > row0)
+    HIPCHK(hipMemcpyAsync(dst, h->desc.occ + (size_t)row0 * N, (size_t)(row1 - row0) * N * sizeof(float),
+                          hipMemcpyDeviceToDevice, h->dc->stream));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
+  return HASTAR_OK;
+}
+
+// Overwrites log-odds rows [row0, row1) from `src` (device pointer, N floats per row; e.g. the
+// all-gathered map).  Returns after the copy has completed, so `src` may be reused at once.
+int hastar_import_rows(hastar_handle h, int row0, int row1, const float* src) {
+  if (!h || (!src && row1 > row0)) return fail(HASTAR_EINVAL, "bad argument");
+  if (row0 < 0 || row1 < row0 || row1 > h->desc.N) return fail(HASTAR_EINVAL, "rows must satisfy 0 <= row0 <= row1 <= N");
+  HIPCHK(hipSetDevice(h->device));
+  const size_t N = (size_t)h->desc.N;
+  if (row1 > row0)
+    HIPCHK(hipMemcpyAsync(h->desc.occ + (size_t)row0 * N, src, (size_t)(row1 - row0) * N * sizeof(float),
+                          hipMemcpyDeviceToDevice, h->dc->stream));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
   return HASTAR_OK;
 }
 

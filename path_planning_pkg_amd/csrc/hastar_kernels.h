@@ -15,10 +15,10 @@ hipError_t launch_decay(float* occ, size_t NN, float lp_free, float lp_min, floa
 hipError_t launch_relocate(int N, float c, float s, float ox, float oy, const float* src, float* dst, int* winner,
                            hipStream_t st);
 hipError_t launch_raster_boxes(float* occ, int* cnt, int N, const int* rp, const float* dl, const int* ids, int nid,
-                               float c, float s, float lp_min, float lp_max, hipStream_t st);
+                               float c, float s, float lp_min, float lp_max, int row0, int row1, hipStream_t st);
 hipError_t launch_raster_lines(float* occ, int* cnt, int N, int n45, int n2, float res, const float* lp,
                                const float* seq_len, const float* seq_wid, int seq_stride, int nline, float lp_min,
-                               float lp_max, hipStream_t st);
+                               float lp_max, int row0, int row1, hipStream_t st);
 hipError_t launch_test_math(int fn, const float* a, const float* b, float* out, int n, hipStream_t st);
 hipError_t launch_test_field(const PlannerDev& P, const float* poses, int n, float* out, hipStream_t st);
 hipError_t launch_test_dubins_len(float r, const float* starts, int n, float gx, float gy, float gh, float* out,

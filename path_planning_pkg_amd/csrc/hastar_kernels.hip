@@ -1282,11 +1282,16 @@ __global__ void k_init_nodemap(PlannerDev P) {
   }
 }
 
-// Grid2D::update_obstacles() (Grid2D.cpp:197-208), float4-vectorised.
+// Grid2D::update_obstacles() (Grid2D.cpp:197-208), float4-vectorised.  `occ` may start
+// anywhere (a row window of the map, see hastar_set_row_window): the cells before the first
+// 16-B boundary and after the last one are done one by one.
 __global__ void k_decay(float* __restrict__ occ, size_t NN, float lp_free, float lp_min, float lp_max) {
-  const size_t n4 = NN / 4;
-  float4* o4 = reinterpret_cast<float4*>(occ);
-  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n4; t += (size_t)gridDim.x * blockDim.x) {
+  const size_t mis = (size_t)((4 - ((reinterpret_cast<uintptr_t>(occ) >> 2) & 3)) & 3);
+  const size_t head = mis < NN ? mis : NN;
+  const size_t n4 = (NN - head) / 4;
+  float4* o4 = reinterpret_cast<float4*>(occ + head);
+  const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x, dt = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = t0; t < n4; t += dt) {
     float4 v = o4[t];
     v.x = stl_max(stl_min(v.x + lp_free, lp_max), lp_min);
     v.y = stl_max(stl_min(v.y + lp_free, lp_max), lp_min);
@@ -1294,7 +1299,8 @@ __global__ void k_decay(float* __restrict__ occ, size_t NN, float lp_free, float
     v.w = stl_max(stl_min(v.w + lp_free, lp_max), lp_min);
     o4[t] = v;
   }
-  for (size_t t = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x)
+  if (t0 < head) occ[t0] = stl_max(stl_min(occ[t0] + lp_free, lp_max), lp_min);
+  for (size_t t = head + n4 * 4 + t0; t < NN; t += dt)
     occ[t] = stl_max(stl_min(occ[t] + lp_free, lp_max), lp_min);
 }
 
@@ -1334,7 +1340,7 @@ __global__ void k_relocate_gather(size_t NN, const float* __restrict__ src, int*
 __global__ __launch_bounds__(256) void k_raster_boxes(float* __restrict__ occ, int* __restrict__ cnt, int N,
                                                       const int* __restrict__ rp, const float* __restrict__ dl,
                                                       const int* __restrict__ ids, int nid, float c, float s,
-                                                      float lp_min, float lp_max) {
+                                                      float lp_min, float lp_max, int r0, int r1) {
   for (int q = blockIdx.x; q < nid; q += gridDim.x) {
     const int k = ids[q];
     const int si = rp[4 * k], sj = rp[4 * k + 1], ni = rp[4 * k + 2], nj = rp[4 * k + 3];
@@ -1347,7 +1353,7 @@ __global__ __launch_bounds__(256) void k_raster_boxes(float* __restrict__ occ, i
         const float x = x0 * c + y0 * s;
         const float y = -x0 * s + y0 * c;
         const int ip = si + trunc_f(roundf(x)), jp = sj + trunc_f(roundf(y));
-        if (ip > -1 && ip < N && jp > -1 && jp < N) {
+        if (ip >= r0 && ip < r1 && jp > -1 && jp < N) {
           const size_t cell = (size_t)ip * N + jp;
           if (pass == 0) {
             atomicAdd(&cnt[cell], 1);
@@ -1374,7 +1380,7 @@ __global__ __launch_bounds__(1024) void k_raster_lines(float* __restrict__ occ, 
                                                        int n2, float res, const float* __restrict__ lp,
                                                        const float* __restrict__ seq_len,
                                                        const float* __restrict__ seq_wid, int seq_stride, int nline,
-                                                       float lp_min, float lp_max) {
+                                                       float lp_min, float lp_max, int r0, int r1) {
   for (int k = 0; k < nline; ++k) {
     const float* L = lp + 9 * k;
     const float ax = L[0], ay = L[1], dx = L[2], dy = L[3], nx = L[4], ny = L[5], d = L[6];
@@ -1392,7 +1398,7 @@ __global__ __launch_bounds__(1024) void k_raster_lines(float* __restrict__ occ, 
         const int j1 = trunc_f(roundf(p1y / res)) + n2, j2 = trunc_f(roundf(p2y / res)) + n2;
         for (int e = 0; e < 2; ++e) {
           const int ii = e ? i2 : i1, jj = e ? j2 : j1;
-          if (ii > -1 && ii < N && jj > -1 && jj < N) {
+          if (ii >= r0 && ii < r1 && jj > -1 && jj < N) {
             const size_t cell = (size_t)ii * N + jj;
             if (pass == 0) {
               atomicAdd(&cnt[cell], 1);
@@ -1496,6 +1502,7 @@ hipError_t launch_init_nodemap(const PlannerDev& P, hipStream_t st) {
   return hipGetLastError();
 }
 hipError_t launch_decay(float* occ, size_t NN, float fr, float mn, float mx, hipStream_t st) {
+  if (NN == 0) return hipSuccess;
   const int blocks = (int)((NN / 4 + 255) / 256 < 2048 ? (NN / 4 + 255) / 256 + 1 : 2048);
   hipLaunchKernelGGL(k_decay, dim3(blocks), dim3(256), 0, st, occ, NN, fr, mn, mx);
   return hipGetLastError();
@@ -1509,16 +1516,16 @@ hipError_t launch_relocate(int N, float c, float s, float ox, float oy, const fl
   return hipGetLastError();
 }
 hipError_t launch_raster_boxes(float* occ, int* cnt, int N, const int* rp, const float* dl, const int* ids, int nid,
-                               float c, float s, float mn, float mx, hipStream_t st) {
+                               float c, float s, float mn, float mx, int r0, int r1, hipStream_t st) {
   if (nid <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_raster_boxes, dim3(nid), dim3(256), 0, st, occ, cnt, N, rp, dl, ids, nid, c, s, mn, mx);
+  hipLaunchKernelGGL(k_raster_boxes, dim3(nid), dim3(256), 0, st, occ, cnt, N, rp, dl, ids, nid, c, s, mn, mx, r0, r1);
   return hipGetLastError();
 }
 hipError_t launch_raster_lines(float* occ, int* cnt, int N, int n45, int n2, float res, const float* lp,
                                const float* seq_len, const float* seq_wid, int stride, int nline, float mn, float mx,
-                               hipStream_t st) {
+                               int r0, int r1, hipStream_t st) {
   hipLaunchKernelGGL(k_raster_lines, dim3(1), dim3(1024), 0, st, occ, cnt, N, n45, n2, res, lp, seq_len, seq_wid,
-                     stride, nline, mn, mx);
+                     stride, nline, mn, mx, r0, r1);
   return hipGetLastError();
 }
 hipError_t launch_test_math(int fn, const float* a, const float* b, float* out, int n, hipStream_t st) {

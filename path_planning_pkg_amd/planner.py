@@ -53,6 +53,9 @@ def load_library():
                                          C.POINTER(HastarStats)]
     L.hastar_get_obstacles.argtypes = [vp, fp]
     L.hastar_grid_size.argtypes = [vp]
+    L.hastar_set_row_window.argtypes = [vp, C.c_int, C.c_int]
+    L.hastar_export_rows.argtypes = [vp, C.c_int, C.c_int, C.c_void_p]
+    L.hastar_import_rows.argtypes = [vp, C.c_int, C.c_int, C.c_void_p]
     L.hastar_last_error.restype = C.c_char_p
     L.hastar_last_search_ms.restype = C.c_float
     L.hastar_test_math.argtypes = [C.c_int, fp, fp, fp, C.c_int]
@@ -137,6 +140,19 @@ class HybridAStar:
         out = np.empty((self.N, self.N), np.float32)
         _check(load_library().hastar_get_obstacles(self.h, fptr(out)))
         return out
+
+    # ---- row-block sharding of the map build (include/hastar.h)
+    def set_row_window(self, row0, row1):
+        _check(load_library().hastar_set_row_window(self.h, int(row0), int(row1)))
+
+    def export_rows(self, row0, row1, dst_ptr):
+        """Copy log-odds rows [row0, row1) into the device buffer at `dst_ptr` (e.g. a
+        torch tensor's data_ptr() on this planner's device); synchronous."""
+        _check(load_library().hastar_export_rows(self.h, int(row0), int(row1), C.c_void_p(int(dst_ptr))))
+
+    def import_rows(self, row0, row1, src_ptr):
+        """Overwrite log-odds rows [row0, row1) from the device buffer at `src_ptr`; synchronous."""
+        _check(load_library().hastar_import_rows(self.h, int(row0), int(row1), C.c_void_p(int(src_ptr))))
 
     # HybridAStar::find_path (HybridAStar.cpp:68-88)
     def find_path(self, vel_init, start, cap=4096):

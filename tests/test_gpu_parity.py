@@ -337,3 +337,43 @@ def test_small_output_buffer(gpu):
     r = g.find_path(proto["vel"], proto["start"], cap=5)   # wrapper retries after HASTAR_ENOSPC
     assert r["ok"] and len(r["path"]) == 43
     assert planner.HASTAR_ENOSPC == -28
+
+
+@pytest.mark.parametrize("N,world", [(254, 3), (256, 4)])
+def test_row_sharded_map_build(gpu, oracle_lib, N, world):
+    """cfg4's map build: `world` planners on this GPU stand in for the ranks.
+    Each builds only its row block (hastar_set_row_window), exports it into one buffer laid out
+    as all_gather_into_tensor would, and imports the whole map back.  The window must confine
+    decay and both rasters to its rows (N = 254, world = 3: blocks start off a 16-B boundary),
+    and the gathered map and the search on it must equal the oracle's single-core build."""
+    import torch
+    from path_planning_pkg_amd.shard import row_blocks
+    cfg, proto = synthetic(N, 36, 10, 7)
+    proto["lines"] = np.array([[-60.0, -20.0, -20.0, 10.0], [-90.0, 30.0, -40.0, -30.0]], np.float32)
+    o = oracle_lib.OraclePlanner(cfg)
+    drive(o, proto)
+    ref = o.get_obstacles()
+    blocks, R = row_blocks(N, world)
+    buf = torch.zeros(world * R * N, dtype=torch.float32, device="cuda:0")
+    torch.cuda.synchronize()
+    shards = [gpu.HybridAStar(cfg) for _ in range(world)]
+    for r, (p, (r0, r1)) in enumerate(zip(shards, blocks)):
+        p.update_goal(proto["goal"], proto["start"])
+        p.set_row_window(r0, r1)
+        for _ in range(proto["cycles"]):
+            p.decay()
+            p.update_lines(proto["lines"], [proto["line_conf"]] * len(proto["lines"]), proto["line_width"])
+            p.update_boxes(proto["boxes"], [proto["box_conf"]] * len(proto["boxes"]), proto["apf_r"])
+        p.set_row_window(0, N)
+        m = p.get_obstacles()
+        assert_bits_equal(m[r0:r1], ref[r0:r1], f"rank {r} block")
+        assert not m[:r0].any() and not m[r1:].any(), f"rank {r} wrote outside its rows"
+        p.export_rows(r0, r1, buf.data_ptr() + r * R * N * 4)
+    for p in shards:
+        p.import_rows(0, N, buf.data_ptr())
+        p.reset()
+        assert_bits_equal(p.get_obstacles(), ref, "gathered map")
+    compare_results(shards[-1].find_path(proto["vel"], proto["start"]), o.find_path(proto["vel"], proto["start"]),
+                    f"search on the gathered map N{N} x{world}")
+    with pytest.raises(gpu.HastarError):
+        shards[0].set_row_window(5, N + 1)

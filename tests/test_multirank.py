@@ -61,3 +61,83 @@ def test_single_rank_identity():
     import bench
     assert bench.reduce_over_ranks(None, 1.5, 7, "cpu") == (1.5, 7.0)
     assert bench.shard_query_ids(0, 1, 3) == [0, 1, 2]
+
+
+class _FakePlanner:
+    """Host stand-in for a planner (no GPU here): its map update writes f(i, j, cycle) into the
+    rows of the current window, so a wrong block order or a write outside the window shows."""
+
+    def __init__(self, N):
+        import numpy as np
+        self.N = N
+        self.map = np.zeros((N, N), np.float32)
+        self.win = (0, N)
+
+    def update_goal(self, goal, start):
+        pass
+
+    def set_row_window(self, r0, r1):
+        self.win = (r0, r1)
+
+    def decay(self):
+        r0, r1 = self.win
+        self.map[r0:r1] = self.map[r0:r1] * 0.5 + 1.0
+
+    def update_boxes(self, boxes, conf, r):
+        import numpy as np
+        r0, r1 = self.win
+        i, j = np.mgrid[r0:r1, 0:self.N]
+        self.map[r0:r1] += (i * 7 + j).astype(np.float32)
+
+    def export_rows(self, r0, r1, ptr):
+        import ctypes
+        ctypes.memmove(ptr, self.map[r0:r1].ctypes.data, (r1 - r0) * self.N * 4)
+
+    def import_rows(self, r0, r1, ptr):
+        import ctypes
+        ctypes.memmove(self.map[r0:r1].ctypes.data, ptr, (r1 - r0) * self.N * 4)
+
+    def reset(self):
+        pass
+
+
+def _fake_proto():
+    import numpy as np
+    return dict(goal=[0, 0, 0], start=[0, 0, 0], cycles=3, lines=np.zeros((0, 4), np.float32),
+                boxes=np.zeros((1, 4), np.float32), box_conf=0.75, apf_r=2.5)
+
+
+def _shard_rank_main(rank, world, port, q):
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from path_planning_pkg_amd.shard import drive_sharded
+    p = _FakePlanner(37)              # 37 rows over 2 ranks: blocks of 19 and 18
+    full = drive_sharded(p, _fake_proto(), rank, world, "cpu")
+    q.put((rank, p.map.tobytes(), full.numpy().tobytes()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_row_sharded_map_build():
+    """path_planning_pkg_amd.shard over gloo: every rank ends with the full single-rank map."""
+    sys.path.insert(0, str(ROOT))
+    from path_planning_pkg_amd.shard import drive_sharded, row_blocks
+    assert row_blocks(37, 2) == ([(0, 19), (19, 37)], 19)
+    assert row_blocks(5, 4) == ([(0, 2), (2, 4), (4, 5), (5, 5)], 2)
+    ref = _FakePlanner(37)
+    drive_sharded(ref, _fake_proto(), 0, 1, "cpu")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for _, m, full in out:
+        assert m == ref.map.tobytes() and full == ref.map.tobytes()
