@@ -88,7 +88,7 @@ def main():
     if args.grid is None:
         args.grid = 2048 if args.workload == "cfg4" else 1024
     if args.workload == "cfg4" and "--batch" not in sys.argv and "HASTAR_BENCH_BATCH" not in os.environ:
-        args.batch = 2048
+        args.batch = 6144  # 2048^2 maps: 32 MiB per planner; the arena pool takes the rest of the HBM
 
     # search arenas may take 95% of the HBM left after the planners' maps (library default 80%)
     os.environ.setdefault("HASTAR_ARENA_FRAC", "0.95")
