@@ -1274,11 +1274,22 @@ __global__ __launch_bounds__(256) void k_clear_bitmaps(uint32_t* const* __restri
   }
 }
 
-__global__ void k_init_nodemap(PlannerDev P) {
-  const size_t NN = (size_t)P.N * P.N;
-  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x) {
-    const int i = (int)(t / P.N), j = (int)(t % P.N);
-    gp(P.nm_f)[t] = euclid_h(P, i, j);
+// Grid2D ctor (Grid2D.cpp:7-62) + compute_heuristic (303-316): f plane = Euclidean h of every
+// cell.  One workgroup per row (grid-strided): the row term dx² is computed once and the
+// columns are written coalesced; no 64-bit divide per cell.  Same float expression as
+// euclid_h, so the values are bit-identical.
+__global__ __launch_bounds__(256) void k_init_nodemap(PlannerDev P) {
+  const int N = P.N;
+  GAS float* f = gp(P.nm_f);
+  for (int i = blockIdx.x; i < N; i += gridDim.x) {
+    const float dx = (float)(P.n45 - i) * P.res;
+    const float dx2 = dx * dx;
+    GAS float* row = f + (size_t)i * N;
+    for (int j = threadIdx.x; j < N; j += blockDim.x) {
+      const float dy = (float)(P.n2 - j) * P.res;
+      const float dy2 = dy * dy;
+      row[j] = sqrtf(dx2 + dy2);
+    }
   }
 }
 
@@ -1498,7 +1509,8 @@ hipError_t launch_clear_bitmaps(uint32_t* const* ptrs, int n, size_t words, hipS
   return hipGetLastError();
 }
 hipError_t launch_init_nodemap(const PlannerDev& P, hipStream_t st) {
-  hipLaunchKernelGGL(k_init_nodemap, dim3(1024), dim3(256), 0, st, P);
+  if (P.N <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_init_nodemap, dim3(std::min(P.N, 8192)), dim3(256), 0, st, P);
   return hipGetLastError();
 }
 hipError_t launch_decay(float* occ, size_t NN, float fr, float mn, float mx, hipStream_t st) {
