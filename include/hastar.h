@@ -138,6 +138,27 @@ int hastar_set_row_window(hastar_handle h, int row0, int row1);
 int hastar_export_rows(hastar_handle h, int row0, int row1, float* dst_device);
 int hastar_import_rows(hastar_handle h, int row0, int row1, const float* src_device);
 
+/* ---- VelocityGenerator<float> (post-search path products) ----
+ * Replaces VelocityGenerator<T>::VelocityGenerator (VelocityGenerator.cpp:7-15) and
+ * generate_velocity_profile (VelocityGenerator.cpp:19-84), called by local_planner.cpp:323,
+ * 332, 451, 460 on find_path's output.  One call profiles n paths on `device`:
+ * path p is points [offsets[p], offsets[p+1]) of xyh (3 floats per point, goal -> start
+ * order as find_path returns it) and curv; flags[p] bit 0 = coast_to_goal, bit 1 =
+ * stop_at_goal.  velocity gets one float per point, feasible[p] the reference's return
+ * value.  Host buffers in and out.  A path with 0 points (undefined behaviour in the
+ * reference) is -EINVAL. */
+typedef struct hastar_velocity_params {
+  float max_velocity;   /* _max_velocity (m/s) */
+  float coast_velocity; /* _coast_velocity (m/s) */
+  float max_lat_acc;    /* _max_lat_acc (m/s^2) */
+  float max_long_acc;   /* _max_long_acc (m/s^2) */
+  float max_long_dec;   /* _max_long_dec (m/s^2) */
+} hastar_velocity_params;
+int hastar_velocity_profile_batch(int device, const hastar_velocity_params* vp, int n,
+                                  const long long* offsets, const float* xyh, const float* curv,
+                                  const float* vel_init, const float* max_velocity_curr,
+                                  const unsigned char* flags, float* velocity, unsigned char* feasible);
+
 /* Grid size N of the handle. */
 int hastar_grid_size(hastar_handle h);
 

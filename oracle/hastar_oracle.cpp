@@ -931,6 +931,57 @@ int orc_vehicle_chain_d(double ts, double a_lat, double wheelbase, double rear_t
   return n;
 }
 
+// VelocityGenerator<float>::generate_velocity_profile (VelocityGenerator.cpp:19-84), restated
+// with the reference's own containers and expression types (T = float; `1.0 - x` promotes
+// to double as in the reference).  prm = {max_velocity, coast_velocity, max_lat_acc,
+// max_long_acc, max_long_dec}; xyh is goal -> start, 3 floats per point.  Returns feasible.
+int orc_velocity_profile(const float prm[5], float vel_init, float max_velocity_curr, const float* xyh,
+                         const float* curv, int n, int coast_to_goal, int stop_at_goal, float* out) {
+  using T = float;
+  const T vmax_param = prm[0], vcoast = prm[1], a_lat = prm[2], a_lat2 = prm[2] * prm[2], a_acc = prm[3],
+          a_dec = prm[4];
+  struct P3 { T _x, _y, _h; };
+  std::vector<P3> path((size_t)n);
+  for (int i = 0; i < n; ++i) path[i] = {xyh[3 * i], xyh[3 * i + 1], xyh[3 * i + 2]};
+  std::vector<T> curvature(curv, curv + n);
+  T max_velocity = coast_to_goal ? vcoast : vmax_param;
+  max_velocity = std::min(max_velocity, max_velocity_curr);
+  const T max_velocity_sqr = max_velocity * max_velocity;
+  const std::size_t path_size = path.size();
+  std::vector<T> velocity(path_size), velocity_sqr(path_size);
+  velocity_sqr[0] = vel_init * vel_init;
+  T max_velocity_sqr_curr = velocity_sqr[0];
+  for (std::size_t i = 0; i + 1 < path_size; i++) {  // initial profile (VelocityGenerator.cpp:35-48)
+    const std::size_t pi = path_size - i - 1;
+    T step = std::hypot(path[pi - 1]._x - path[pi]._x, path[pi - 1]._y - path[pi]._y);
+    T lat = velocity_sqr[i] * curvature[pi];
+    T rem = a_dec * std::sqrt(1.0 - (lat * lat) / a_lat2);
+    max_velocity_sqr_curr = std::max(max_velocity_sqr_curr - 2 * rem * step, max_velocity_sqr);
+    velocity_sqr[i + 1] = (curvature[pi - 1] != 0) ? std::min(a_lat / curvature[pi - 1], max_velocity_sqr_curr)
+                                                   : max_velocity_sqr_curr;
+  }
+  velocity_sqr[path_size - 1] = stop_at_goal ? 0 : velocity_sqr[path_size - 1];  // (51)
+  for (std::size_t i = 0; i + 1 < path_size; i++) {  // forward pass (54-63)
+    const std::size_t pi = path_size - i - 1;
+    T step = std::hypot(path[pi - 1]._x - path[pi]._x, path[pi - 1]._y - path[pi]._y);
+    T lat = velocity_sqr[i] * curvature[pi];
+    T rem = a_acc * std::sqrt(1.0 - (lat * lat) / a_lat2);
+    velocity_sqr[i + 1] = std::min(velocity_sqr[i] + 2 * rem * step, velocity_sqr[i + 1]);
+  }
+  for (std::size_t i = path_size - 1; i > 0; i--) {  // backward pass (66-76)
+    const std::size_t pi = path_size - i - 1;
+    T step = std::hypot(path[pi + 1]._x - path[pi]._x, path[pi + 1]._y - path[pi]._y);
+    T lat = velocity_sqr[i] * curvature[pi];
+    T rem = a_dec * std::sqrt(1.0 - (lat * lat) / a_lat2);
+    velocity_sqr[i - 1] = std::min(velocity_sqr[i] + 2 * rem * step, velocity_sqr[i - 1]);
+    velocity[i - 1] = std::sqrt(velocity_sqr[i - 1]);
+  }
+  velocity[path_size - 1] = std::sqrt(velocity_sqr[path_size - 1]);  // (79-82)
+  for (int i = 0; i < n; ++i) out[i] = velocity[i];
+  constexpr T tol = static_cast<T>(0.25);
+  return vel_init < (velocity[0] + tol) ? 1 : 0;
+}
+
 }  // extern "C"
 
 // glibc reference values for the GPU libm-port test (fn numbering of hastar_test_math).

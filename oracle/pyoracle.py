@@ -53,6 +53,7 @@ def lib():
         L.orc_vehicle_chain_d.argtypes = [C.c_double, C.c_double, C.c_double, C.c_double, C.c_int, C.c_int,
                                           dp, dp, C.c_int, C.c_double, C.c_int, ip, C.c_int, dp]
         L.orc_libm.argtypes = [C.c_int, fp, fp, fp, C.c_int]
+        L.orc_velocity_profile.argtypes = [fp, C.c_float, C.c_float, fp, fp, C.c_int, C.c_int, C.c_int, fp]
         _lib = L
     return _lib
 
@@ -199,6 +200,20 @@ def vehicle_chain_d(ts, a_lat, wheelbase, rear_to_cg, bins, na, steering, weight
     return out[:n].copy()
 
 
+
+
+def velocity_profile(params, vel_init, max_velocity_curr, xyh, curv, coast_to_goal, stop_at_goal=False):
+    """VelocityGenerator<float>::generate_velocity_profile (VelocityGenerator.cpp:19-84).
+    params = (max_velocity, coast_velocity, max_lat_acc, max_long_acc, max_long_dec).
+    Returns (feasible, velocity) for a goal -> start path."""
+    prm = _f32(params)
+    xyh = _f32(xyh, (-1, 3))
+    curv = _f32(curv)
+    assert len(curv) == len(xyh) and len(xyh) > 0
+    out = np.empty(len(xyh), np.float32)
+    ok = lib().orc_velocity_profile(fptr(prm), vel_init, max_velocity_curr, fptr(xyh), fptr(curv), len(xyh),
+                                    int(bool(coast_to_goal)), int(bool(stop_at_goal)), fptr(out))
+    return bool(ok), out
 
 
 def libm(fn, a, b=None):

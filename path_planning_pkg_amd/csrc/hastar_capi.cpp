@@ -1074,6 +1074,63 @@ int hastar_copy_path(hastar_handle h, float* xyh, float* curv, int cap, int* len
   return r;
 }
 
+// VelocityGenerator<float> (VelocityGenerator.cpp:7-84) over a batch of paths: inputs are
+// packed into one device slab, profiled by k_velocity_profile (one thread per path) on the
+// device context's stream, and copied back.
+int hastar_velocity_profile_batch(int device, const hastar_velocity_params* vp, int n, const long long* offsets,
+                                  const float* xyh, const float* curv, const float* vel_init,
+                                  const float* max_velocity_curr, const unsigned char* flags, float* velocity,
+                                  unsigned char* feasible) {
+  if (!vp || n < 0 || (n > 0 && (!offsets || !xyh || !curv || !vel_init || !max_velocity_curr || !flags ||
+                                 !velocity || !feasible)))
+    return fail(HASTAR_EINVAL, "velocity_profile: null argument");
+  if (n == 0) return HASTAR_OK;
+  if (offsets[0] != 0) return fail(HASTAR_EINVAL, "velocity_profile: offsets[0] must be 0");
+  for (int p = 0; p < n; ++p)
+    if (offsets[p + 1] <= offsets[p]) return fail(HASTAR_EINVAL, "velocity_profile: path " + std::to_string(p) + " is empty");
+  const size_t pts = (size_t)offsets[n];
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev || device > 63)
+    return fail(HASTAR_EDEVICE, "velocity_profile: no HIP device " + std::to_string(device));
+  DeviceCtx* D = nullptr;
+  if (int r = device_ctx(device, &D)) return r;
+  HIPCHK(hipSetDevice(device));
+  const size_t b_off = align256((n + 1) * sizeof(long long)), b_xyh = align256(3 * pts * sizeof(float)),
+               b_pt = align256(pts * sizeof(float)), b_pf = align256(n * sizeof(float)), b_pb = align256(n);
+  const size_t total = b_off + b_xyh + 2 * b_pt + 2 * b_pf + 2 * b_pb;
+  char* slab = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&slab), total) != hipSuccess)
+    return fail(HASTAR_ENOMEM, "velocity_profile: hipMalloc failed");
+  char* q = slab;
+  auto take = [&](size_t b) { char* r = q; q += b; return r; };
+  long long* d_off = reinterpret_cast<long long*>(take(b_off));
+  float* d_xyh = reinterpret_cast<float*>(take(b_xyh));
+  float* d_curv = reinterpret_cast<float*>(take(b_pt));
+  float* d_vel = reinterpret_cast<float*>(take(b_pt));
+  float* d_v0 = reinterpret_cast<float*>(take(b_pf));
+  float* d_vmax = reinterpret_cast<float*>(take(b_pf));
+  unsigned char* d_flags = reinterpret_cast<unsigned char*>(take(b_pb));
+  unsigned char* d_feas = reinterpret_cast<unsigned char*>(take(b_pb));
+  hipStream_t st = D->stream;
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) { if (e == hipSuccess) e = x; };
+  chk(hipMemcpyAsync(d_off, offsets, (n + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
+  chk(hipMemcpyAsync(d_xyh, xyh, 3 * pts * sizeof(float), hipMemcpyHostToDevice, st));
+  chk(hipMemcpyAsync(d_curv, curv, pts * sizeof(float), hipMemcpyHostToDevice, st));
+  chk(hipMemcpyAsync(d_v0, vel_init, n * sizeof(float), hipMemcpyHostToDevice, st));
+  chk(hipMemcpyAsync(d_vmax, max_velocity_curr, n * sizeof(float), hipMemcpyHostToDevice, st));
+  chk(hipMemcpyAsync(d_flags, flags, n, hipMemcpyHostToDevice, st));
+  const hastar::VelParams P{vp->max_velocity, vp->coast_velocity, vp->max_lat_acc, vp->max_lat_acc * vp->max_lat_acc,
+                            vp->max_long_acc, vp->max_long_dec};
+  if (e == hipSuccess) chk(hastar::launch_velocity_profile(P, n, d_off, d_xyh, d_curv, d_v0, d_vmax, d_flags, d_vel, d_feas, st));
+  chk(hipMemcpyAsync(velocity, d_vel, pts * sizeof(float), hipMemcpyDeviceToHost, st));
+  chk(hipMemcpyAsync(feasible, d_feas, n, hipMemcpyDeviceToHost, st));
+  chk(hipStreamSynchronize(st));
+  hipFree(slab);
+  if (e != hipSuccess) return fail(HASTAR_EDEVICE, std::string("velocity_profile: ") + hipGetErrorString(e));
+  return HASTAR_OK;
+}
+
 // ---------------------------------------------------------------- test hooks --------
 int hastar_test_math(int fn, const float* a, const float* b, float* out, int n) {
   if (n <= 0) return HASTAR_OK;

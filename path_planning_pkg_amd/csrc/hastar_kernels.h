@@ -19,6 +19,10 @@ hipError_t launch_raster_boxes(float* occ, int* cnt, int N, const int* rp, const
 hipError_t launch_raster_lines(float* occ, int* cnt, int N, int n45, int n2, float res, const float* lp,
                                const float* seq_len, const float* seq_wid, int seq_stride, int nline, float lp_min,
                                float lp_max, int row0, int row1, hipStream_t st);
+struct VelParams { float max_velocity, coast_velocity, max_lat_acc, max_lat_acc_sqr, max_long_acc, max_long_dec; };
+hipError_t launch_velocity_profile(const VelParams& vp, int n, const long long* off, const float* xyh, const float* curv,
+                                   const float* vel_init, const float* vmax_curr, const unsigned char* flags, float* vel,
+                                   unsigned char* feasible, hipStream_t st);
 hipError_t launch_test_math(int fn, const float* a, const float* b, float* out, int n, hipStream_t st);
 hipError_t launch_test_field(const PlannerDev& P, const float* poses, int n, float* out, hipStream_t st);
 hipError_t launch_test_dubins_len(float r, const float* starts, int n, float gx, float gy, float gh, float* out,

@@ -1430,6 +1430,74 @@ __global__ __launch_bounds__(1024) void k_raster_lines(float* __restrict__ occ, 
   }
 }
 
+// ------------------------------------------------ VelocityGenerator (post-search) -----
+// VelocityGenerator<float>::generate_velocity_profile (VelocityGenerator.cpp:19-84), one
+// thread per path.  The three passes are sequential along a path, so the parallelism is
+// across paths.  velocity_sqr lives in the output array and the pass carries its running
+// value in a register; the backward pass reads v²[i-1] before it overwrites it with v.
+// The reference's float expressions are kept: `1.0 - x` promotes to double, so the
+// remaining-acceleration term is a double sqrt rounded to float; hypot is glibc's hypotf.
+__device__ __forceinline__ float vg_step(const float* X, int a, int b) {
+  return g_hypotf(X[3 * a] - X[3 * b], X[3 * a + 1] - X[3 * b + 1]);
+}
+__device__ __forceinline__ float vg_long_rem(float acc, float vsq, float k, float lat2) {
+  const float lat = vsq * k;
+  return (float)((double)acc * sqrt(1.0 - (double)((lat * lat) / lat2)));
+}
+__global__ __launch_bounds__(64) void k_velocity_profile(VelParams vp, int n, const long long* __restrict__ off,
+                                                         const float* __restrict__ xyh, const float* __restrict__ curv,
+                                                         const float* __restrict__ vel_init,
+                                                         const float* __restrict__ vmax_curr,
+                                                         const unsigned char* __restrict__ flags, float* vel,
+                                                         unsigned char* __restrict__ feasible) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const long long o = off[p];
+  const int P = (int)(off[p + 1] - o);
+  const float* X = xyh + 3 * o;
+  const float* K = curv + o;
+  float* V = vel + o;
+  const unsigned char fl = flags[p];
+  float vmax = (fl & 1u) ? vp.coast_velocity : vp.max_velocity;
+  vmax = stl_min(vmax, vmax_curr[p]);
+  const float vmax2 = vmax * vmax;
+  const float v0 = vel_init[p];
+  // initial profile: lateral-acceleration limits and braking to the velocity cap
+  float cur = v0 * v0;
+  V[0] = cur;
+  float mcur = cur;
+  for (int i = 0; i < P - 1; ++i) {
+    const int pi = P - i - 1;
+    const float step = vg_step(X, pi - 1, pi);
+    const float rem = vg_long_rem(vp.max_long_dec, cur, K[pi], vp.max_lat_acc_sqr);
+    mcur = stl_max(mcur - 2.0f * rem * step, vmax2);
+    cur = (K[pi - 1] != 0.0f) ? stl_min(vp.max_lat_acc / K[pi - 1], mcur) : mcur;
+    V[i + 1] = cur;
+  }
+  if (fl & 2u) V[P - 1] = 0.0f;
+  // forward pass (acceleration limit)
+  cur = V[0];
+  for (int i = 0; i < P - 1; ++i) {
+    const int pi = P - i - 1;
+    const float step = vg_step(X, pi - 1, pi);
+    const float rem = vg_long_rem(vp.max_long_acc, cur, K[pi], vp.max_lat_acc_sqr);
+    cur = stl_min(cur + 2.0f * rem * step, V[i + 1]);
+    V[i + 1] = cur;
+  }
+  // backward pass (braking limit), writing velocities
+  cur = V[P - 1];
+  const float last = cur;
+  for (int i = P - 1; i > 0; --i) {
+    const int pi = P - i - 1;
+    const float step = vg_step(X, pi + 1, pi);
+    const float rem = vg_long_rem(vp.max_long_dec, cur, K[pi], vp.max_lat_acc_sqr);
+    cur = stl_min(cur + 2.0f * rem * step, V[i - 1]);
+    V[i - 1] = sqrtf(cur);
+  }
+  V[P - 1] = sqrtf(last);
+  feasible[p] = (v0 < (V[0] + 0.25f)) ? 1 : 0;
+}
+
 // ---------------------------------------------------------------- test kernels -------
 __global__ void k_test_math(int fn, const float* a, const float* b, float* out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1538,6 +1606,14 @@ hipError_t launch_raster_lines(float* occ, int* cnt, int N, int n45, int n2, flo
                                int r0, int r1, hipStream_t st) {
   hipLaunchKernelGGL(k_raster_lines, dim3(1), dim3(1024), 0, st, occ, cnt, N, n45, n2, res, lp, seq_len, seq_wid,
                      stride, nline, mn, mx, r0, r1);
+  return hipGetLastError();
+}
+hipError_t launch_velocity_profile(const VelParams& vp, int n, const long long* off, const float* xyh, const float* curv,
+                                   const float* vel_init, const float* vmax_curr, const unsigned char* flags, float* vel,
+                                   unsigned char* feasible, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_velocity_profile, dim3((n + 63) / 64), dim3(64), 0, st, vp, n, off, xyh, curv, vel_init,
+                     vmax_curr, flags, vel, feasible);
   return hipGetLastError();
 }
 hipError_t launch_test_math(int fn, const float* a, const float* b, float* out, int n, hipStream_t st) {

@@ -70,6 +70,9 @@ def load_library():
     L.hastar_debug_astar_modes.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_timing.argtypes = [vp, C.POINTER(C.c_ulonglong)]
     L.hastar_debug_slots.argtypes = [vp, C.POINTER(C.c_longlong)]
+    L.hastar_velocity_profile_batch.argtypes = [C.c_int, C.POINTER(HastarVelocityParams), C.c_int,
+                                                C.POINTER(C.c_longlong), fp, fp, fp, fp, C.POINTER(C.c_ubyte), fp,
+                                                C.POINTER(C.c_ubyte)]
     _lib = L
     return L
 
@@ -83,6 +86,54 @@ def _check(rc):
 def _f32(a, shape=None):
     a = np.ascontiguousarray(a, dtype=np.float32)
     return a.reshape(shape) if shape is not None else a
+
+
+class HastarVelocityParams(C.Structure):
+    """hastar_velocity_params (include/hastar.h)."""
+    _fields_ = [("max_velocity", C.c_float), ("coast_velocity", C.c_float), ("max_lat_acc", C.c_float),
+                ("max_long_acc", C.c_float), ("max_long_dec", C.c_float)]
+
+
+class VelocityGenerator:
+    """Mirror of planning::VelocityGenerator<float> (VelocityGenerator.h:10-28) on the GPU.
+
+    generate_velocity_profile keeps the reference's arguments (VelocityGenerator.cpp:19-21)
+    and returns (feasible, velocity) instead of filling `velocity` in place;
+    generate_velocity_profiles runs many paths in one launch (one thread per path)."""
+
+    def __init__(self, max_velocity, coast_velocity, max_lat_acc, max_long_acc, max_long_dec, device=0):
+        self.params = HastarVelocityParams(max_velocity, coast_velocity, max_lat_acc, max_long_acc, max_long_dec)
+        self.device = int(device)
+
+    def generate_velocity_profile(self, vel_init, max_velocity_curr, path, curvature, coast_to_goal,
+                                  stop_at_goal=False):
+        ok, vel = self.generate_velocity_profiles([vel_init], [max_velocity_curr], [path], [curvature],
+                                                  [coast_to_goal], [stop_at_goal])
+        return bool(ok[0]), vel[0]
+
+    def generate_velocity_profiles(self, vel_init, max_velocity_curr, paths, curvatures, coast_to_goal,
+                                   stop_at_goal=None):
+        n = len(paths)
+        xyh = [_f32(p, (-1, 3)) for p in paths]
+        cv = [_f32(c) for c in curvatures]
+        lens = np.array([len(p) for p in xyh], np.int64)
+        if any(len(c) != l for c, l in zip(cv, lens)):
+            raise ValueError("path and curvature lengths differ")
+        off = np.zeros(n + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        X = np.ascontiguousarray(np.concatenate(xyh) if n else np.zeros((0, 3), np.float32))
+        K = np.ascontiguousarray(np.concatenate(cv) if n else np.zeros(0, np.float32))
+        v0 = _f32(vel_init)
+        vm = _f32(max_velocity_curr)
+        stop = [False] * n if stop_at_goal is None else stop_at_goal
+        flags = np.array([int(bool(c)) | (int(bool(s)) << 1) for c, s in zip(coast_to_goal, stop)], np.uint8)
+        vel = np.empty(int(off[-1]), np.float32)
+        feas = np.zeros(n, np.uint8)
+        u8 = C.POINTER(C.c_ubyte)
+        _check(load_library().hastar_velocity_profile_batch(
+            self.device, C.byref(self.params), n, off.ctypes.data_as(C.POINTER(C.c_longlong)), fptr(X), fptr(K),
+            fptr(v0), fptr(vm), flags.ctypes.data_as(u8), fptr(vel), feas.ctypes.data_as(u8)))
+        return feas.astype(bool), [vel[off[i]:off[i + 1]] for i in range(n)]
 
 
 class HybridAStar:

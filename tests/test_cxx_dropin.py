@@ -49,3 +49,47 @@ def test_dropin_harness_matches_oracle_and_golden(tmp_path, oracle_lib):
     # the reference's printed path (start -> goal, 43 poses)
     mine = [[float("%g" % v) for v in row] for row in pts[::-1, :3].view(np.float32).astype(np.float64)]
     assert mine == g["path_start_to_goal"]
+
+
+VG_MAIN = r"""
+#include <cstdio>
+#include "VelocityGenerator.h"
+int main() {
+  planning::VelocityGenerator<float> vg(12.f, 4.f, 2.5f, 1.5f, 3.f);
+  std::vector<planning::Vector3D<float>> path{{2.f, 0.f, 0.f}, {1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+  std::vector<float> curv{0.f, 0.1f, 0.f}, vel;
+  bool ok = vg.generate_velocity_profile(1.f, 9.f, path, curv, vel, false, true);
+  std::printf("%d", ok ? 1 : 0);
+  for (float v : vel) std::printf(" %08x", *reinterpret_cast<unsigned*>(&v));
+  std::printf("\n");
+  return 0;
+}
+"""
+
+
+def _build_vg(tmp_path):
+    src, exe = tmp_path / "vg_main.cpp", tmp_path / "vg_main"
+    src.write_text(VG_MAIN)
+    cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", f"-I{ROOT / 'tests' / 'cxx'}",
+           f"-I{ROOT / 'include' / 'path_planning_pkg'}", str(src), f"-L{LIB}", "-lhastar_amd",
+           f"-Wl,-rpath,{LIB}", "-o", str(exe)]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    return exe
+
+
+def test_velocity_generator_header_compiles_and_links(tmp_path):
+    if not (LIB / "libhastar_amd.so").exists():
+        pytest.skip("library not built")
+    assert _build_vg(tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_velocity_generator_dropin_matches_oracle(tmp_path):
+    from oracle import pyoracle
+    out = subprocess.run([str(_build_vg(tmp_path))], check=True, capture_output=True, text=True,
+                         timeout=120).stdout.split()
+    xyh = np.array([[2, 0, 0], [1, 0, 0], [0, 0, 0]], np.float32)
+    ok, v = pyoracle.velocity_profile((12, 4, 2.5, 1.5, 3), 1.0, 9.0, xyh, np.array([0, 0.1, 0], np.float32),
+                                      False, True)
+    assert int(out[0]) == int(ok)
+    assert [int(t, 16) for t in out[1:]] == v.view(np.uint32).tolist()
