@@ -172,6 +172,7 @@ def main():
             p.reset()
             r, kms = gpu.find_path_batch([p], [c[1]["vel"]], [c[1]["start"]], cap=8192)
             lat.append(kms)
+        vel_prof = velocity_profile_phase(gpu, last, device, [c[1]["vel"] for c in cfgs])
         traffic = None
         pmc = ROOT / "profiles" / "pmc_search_summary.json"
         if pmc.exists():
@@ -212,6 +213,7 @@ def main():
         }
         if map_build:
             out["map_build"] = map_build
+        out["velocity_profile"] = vel_prof
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps)
     if dist:
@@ -219,6 +221,37 @@ def main():
         dist.destroy_process_group()
     if out is not None:
         print(json.dumps(out))
+
+
+# VelocityGenerator parameters for the post-search stage (synthetic; the reference's
+# ROS parameters are not part of the benchmark config): max, coast, lateral, accel, decel.
+VEL_PARAMS = (10.0, 3.0, 2.5, 1.5, 3.0)
+
+
+def velocity_profile_phase(gpu, last, device, vels):
+    """VelocityGenerator<float> over every successful path of the last timed step
+    (SURVEY §8(f) rank 3): one packed hastar_velocity_profile_batch call, timed after a
+    warm-up call.  Host buffers in and out, so the time is PCIe-inclusive."""
+    idx = np.nonzero(last.ok & (last.lens > 0))[0]
+    if len(idx) == 0:
+        return None
+    lens = last.lens[idx].astype(np.int64)
+    off = np.zeros(len(idx) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    X = np.concatenate([last.xyh[i, :last.lens[i]] for i in idx]).reshape(-1, 3)
+    K = np.concatenate([last.curv[i, :last.lens[i]] for i in idx])
+    v0 = np.asarray([vels[i] for i in idx], np.float32)
+    vm = np.full(len(idx), VEL_PARAMS[0], np.float32)
+    flags = np.full(len(idx), 2, np.uint8)  # stop_at_goal
+    vg = gpu.VelocityGenerator(*VEL_PARAMS, device=device)
+    vg.profile_packed(off, X, K, v0, vm, flags)
+    t0 = time.perf_counter()
+    feas, _ = vg.profile_packed(off, X, K, v0, vm, flags)
+    ms = (time.perf_counter() - t0) * 1e3
+    return {"paths": int(len(idx)), "points": int(off[-1]), "ms_pcie_inclusive": ms,
+            "paths_per_s": len(idx) / (ms * 1e-3), "feasible_rate": float(feas.mean()),
+            "params": dict(zip(("max_velocity", "coast_velocity", "max_lat_acc", "max_long_acc", "max_long_dec"),
+                               VEL_PARAMS))}
 
 
 def map_build_phase(args, gpu, dist, torch, rank, world, device):

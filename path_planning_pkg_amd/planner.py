@@ -127,13 +127,27 @@ class VelocityGenerator:
         vm = _f32(max_velocity_curr)
         stop = [False] * n if stop_at_goal is None else stop_at_goal
         flags = np.array([int(bool(c)) | (int(bool(s)) << 1) for c, s in zip(coast_to_goal, stop)], np.uint8)
+        feas, vel = self.profile_packed(off, X, K, v0, vm, flags)
+        return feas.astype(bool), [vel[off[i]:off[i + 1]] for i in range(n)]
+
+    def profile_packed(self, off, xyh, curv, vel_init, max_velocity_curr, flags):
+        """One hastar_velocity_profile_batch call on packed arrays: off (n+1, int64), xyh
+        (points x 3, f32), curv, vel_init, max_velocity_curr (f32), flags (u8: bit 0 coast,
+        bit 1 stop).  Returns (feasible u8[n], velocity f32[points])."""
+        n = len(off) - 1
+        off = np.ascontiguousarray(off, np.int64)
+        X, K = _f32(xyh, (-1, 3)), _f32(curv)
+        v0, vm = _f32(vel_init), _f32(max_velocity_curr)
+        flags = np.ascontiguousarray(flags, np.uint8)
+        if len(v0) != n or len(vm) != n or len(flags) != n or len(X) != off[-1] or len(K) != off[-1]:
+            raise ValueError("profile_packed: inconsistent array lengths")
         vel = np.empty(int(off[-1]), np.float32)
         feas = np.zeros(n, np.uint8)
         u8 = C.POINTER(C.c_ubyte)
         _check(load_library().hastar_velocity_profile_batch(
             self.device, C.byref(self.params), n, off.ctypes.data_as(C.POINTER(C.c_longlong)), fptr(X), fptr(K),
             fptr(v0), fptr(vm), flags.ctypes.data_as(u8), fptr(vel), feas.ctypes.data_as(u8)))
-        return feas.astype(bool), [vel[off[i]:off[i + 1]] for i in range(n)]
+        return feas, vel
 
 
 class HybridAStar:
