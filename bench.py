@@ -246,10 +246,22 @@ def velocity_profile_phase(gpu, last, device, vels):
     vg = gpu.VelocityGenerator(*VEL_PARAMS, device=device)
     vg.profile_packed(off, X, K, v0, vm, flags)
     t0 = time.perf_counter()
-    feas, _ = vg.profile_packed(off, X, K, v0, vm, flags)
+    feas, vel = vg.profile_packed(off, X, K, v0, vm, flags)
     ms = (time.perf_counter() - t0) * 1e3
+    # the oracle (1 thread) over the same paths: CPU time and bit parity
+    from oracle import pyoracle
+    cpu_s, same = 0.0, True
+    for j in range(len(idx)):
+        a, b = int(off[j]), int(off[j + 1])
+        t1 = time.perf_counter()
+        ok_o, vo = pyoracle.velocity_profile(VEL_PARAMS, float(v0[j]), float(vm[j]), X[a:b], K[a:b], False, True)
+        cpu_s += time.perf_counter() - t1
+        vg_ = vel[a:b]
+        nan = np.isnan(vo) & np.isnan(vg_)  # NaN payloads are not part of the contract
+        same = same and ok_o == bool(feas[j]) and bool((nan | (vo.view(np.uint32) == vg_.view(np.uint32))).all())
     return {"paths": int(len(idx)), "points": int(off[-1]), "ms_pcie_inclusive": ms,
             "paths_per_s": len(idx) / (ms * 1e-3), "feasible_rate": float(feas.mean()),
+            "cpu_oracle_ms": cpu_s * 1e3, "cpu_oracle_cores": 1, "parity_with_oracle": bool(same),
             "params": dict(zip(("max_velocity", "coast_velocity", "max_lat_acc", "max_long_acc", "max_long_dec"),
                                VEL_PARAMS))}
 
