@@ -1462,37 +1462,85 @@ __global__ __launch_bounds__(64) void k_velocity_profile(VelParams vp, int n, co
   vmax = stl_min(vmax, vmax_curr[p]);
   const float vmax2 = vmax * vmax;
   const float v0 = vel_init[p];
+  // Each pass walks its path in blocks of U points: the block's inputs (positions,
+  // curvatures, v² of the previous pass) are loaded first, so the dependent chain waits
+  // for memory once per block instead of once per point.  The step lengths are
+  // hypot(x[a] - x[b], y[a] - y[b]) in the reference's operand order.
+  constexpr int U = 8;
+  const int S = P - 1;  // iterations per pass
   // initial profile: lateral-acceleration limits and braking to the velocity cap
   float cur = v0 * v0;
   V[0] = cur;
   float mcur = cur;
-  for (int i = 0; i < P - 1; ++i) {
-    const int pi = P - i - 1;
-    const float step = vg_step(X, pi - 1, pi);
-    const float rem = vg_long_rem(vp.max_long_dec, cur, K[pi], vp.max_lat_acc_sqr);
-    mcur = stl_max(mcur - 2.0f * rem * step, vmax2);
-    cur = (K[pi - 1] != 0.0f) ? stl_min(vp.max_lat_acc / K[pi - 1], mcur) : mcur;
-    V[i + 1] = cur;
+  for (int b = 0; b < S; b += U) {  // i = b + u, pi = P-1-i; points pi and pi-1
+    float xs[U + 1], ys[U + 1], ks[U + 1];
+#pragma unroll
+    for (int u = 0; u <= U; ++u) {
+      const int pi = P - 1 - (b + u);
+      const bool in = b + u <= S;
+      xs[u] = in ? X[3 * pi] : 0.0f;
+      ys[u] = in ? X[3 * pi + 1] : 0.0f;
+      ks[u] = in ? K[pi] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (b + u >= S) break;
+      const float step = g_hypotf(xs[u + 1] - xs[u], ys[u + 1] - ys[u]);
+      const float rem = vg_long_rem(vp.max_long_dec, cur, ks[u], vp.max_lat_acc_sqr);
+      mcur = stl_max(mcur - 2.0f * rem * step, vmax2);
+      cur = (ks[u + 1] != 0.0f) ? stl_min(vp.max_lat_acc / ks[u + 1], mcur) : mcur;
+      V[b + u + 1] = cur;
+    }
   }
   if (fl & 2u) V[P - 1] = 0.0f;
   // forward pass (acceleration limit)
   cur = V[0];
-  for (int i = 0; i < P - 1; ++i) {
-    const int pi = P - i - 1;
-    const float step = vg_step(X, pi - 1, pi);
-    const float rem = vg_long_rem(vp.max_long_acc, cur, K[pi], vp.max_lat_acc_sqr);
-    cur = stl_min(cur + 2.0f * rem * step, V[i + 1]);
-    V[i + 1] = cur;
+  for (int b = 0; b < S; b += U) {
+    float xs[U + 1], ys[U + 1], ks[U], vs[U];
+#pragma unroll
+    for (int u = 0; u <= U; ++u) {
+      const int pi = P - 1 - (b + u);
+      const bool in = b + u <= S;
+      xs[u] = in ? X[3 * pi] : 0.0f;
+      ys[u] = in ? X[3 * pi + 1] : 0.0f;
+      if (u < U) {
+        ks[u] = (b + u < S) ? K[pi] : 0.0f;
+        vs[u] = (b + u < S) ? V[b + u + 1] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (b + u >= S) break;
+      const float step = g_hypotf(xs[u + 1] - xs[u], ys[u + 1] - ys[u]);
+      const float rem = vg_long_rem(vp.max_long_acc, cur, ks[u], vp.max_lat_acc_sqr);
+      cur = stl_min(cur + 2.0f * rem * step, vs[u]);
+      V[b + u + 1] = cur;
+    }
   }
-  // backward pass (braking limit), writing velocities
+  // backward pass (braking limit), writing velocities: i = P-1 .. 1, pi = P-1-i = j
   cur = V[P - 1];
   const float last = cur;
-  for (int i = P - 1; i > 0; --i) {
-    const int pi = P - i - 1;
-    const float step = vg_step(X, pi + 1, pi);
-    const float rem = vg_long_rem(vp.max_long_dec, cur, K[pi], vp.max_lat_acc_sqr);
-    cur = stl_min(cur + 2.0f * rem * step, V[i - 1]);
-    V[i - 1] = sqrtf(cur);
+  for (int b = 0; b < S; b += U) {  // j = b + u: points j and j+1, v² index i-1 = P-2-j
+    float xs[U + 1], ys[U + 1], ks[U], vs[U];
+#pragma unroll
+    for (int u = 0; u <= U; ++u) {
+      const int j = b + u;
+      const bool in = j <= S;
+      xs[u] = in ? X[3 * j] : 0.0f;
+      ys[u] = in ? X[3 * j + 1] : 0.0f;
+      if (u < U) {
+        ks[u] = (j < S) ? K[j] : 0.0f;
+        vs[u] = (j < S) ? V[P - 2 - j] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (b + u >= S) break;
+      const float step = g_hypotf(xs[u + 1] - xs[u], ys[u + 1] - ys[u]);
+      const float rem = vg_long_rem(vp.max_long_dec, cur, ks[u], vp.max_lat_acc_sqr);
+      cur = stl_min(cur + 2.0f * rem * step, vs[u]);
+      V[P - 2 - (b + u)] = sqrtf(cur);
+    }
   }
   V[P - 1] = sqrtf(last);
   feasible[p] = (v0 < (V[0] + 0.25f)) ? 1 : 0;
