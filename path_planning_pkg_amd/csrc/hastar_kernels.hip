@@ -1466,7 +1466,7 @@ __global__ __launch_bounds__(64) void k_velocity_profile(VelParams vp, int n, co
   // curvatures, v² of the previous pass) are loaded first, so the dependent chain waits
   // for memory once per block instead of once per point.  The step lengths are
   // hypot(x[a] - x[b], y[a] - y[b]) in the reference's operand order.
-  constexpr int U = 8;
+  constexpr int U = 16;
   const int S = P - 1;  // iterations per pass
   // initial profile: lateral-acceleration limits and braking to the velocity cap
   float cur = v0 * v0;
