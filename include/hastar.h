@@ -55,7 +55,9 @@ typedef struct hastar_params {
   const float* steering;           /* radians */
   const float* curvature_weights;
   /* ---- extensions (0 = default) ---- */
-  int max_pops;                    /* arena: Hybrid A* pops per search (default 262144) */
+  int max_pops;                    /* initial arena of a search, in pops (default 262144); a search
+                                      that outgrows it is parked and resumed in a 4x larger arena,
+                                      so this is NOT a limit (the reference has none) */
   int max_astar_nodes;             /* arena: open-set nodes of one inner A* search (default min(N*N+16, 65536)) */
   int max_dubins_samples;          /* arena: samples of one Dubins shot (default from N) */
 } hastar_params;
@@ -73,7 +75,11 @@ typedef struct hastar_stats {
   unsigned long long pop_digest;    /* ordered digest of (cell, bin, g bits) of every pop */
   unsigned long long closed_digest; /* order-independent digest of the closed-set keys */
   int via_shot;                /* success came from an analytic Dubins shot */
-  int status;                  /* 0 ok, HASTAR_EOVERFLOW if the arena overflowed */
+  int status;                  /* this planner's outcome: 0, HASTAR_EOVERFLOW (HASTAR_MAX_POPS_HARD
+                                  budget or device memory exhausted), HASTAR_ENOSPC (path longer
+                                  than the caller's cap: *len is the length needed) */
+  int parks;                   /* times the search outgrew its arena and was resumed in a larger one */
+  int pad;
 } hastar_stats;
 
 /* HybridAStar(...) (HybridAStar.cpp:7-24). device = HIP device ordinal. */
@@ -158,6 +164,15 @@ int hastar_velocity_profile_batch(int device, const hastar_velocity_params* vp, 
                                   const long long* offsets, const float* xyh, const float* curv,
                                   const float* vel_init, const float* max_velocity_curr,
                                   const unsigned char* flags, float* velocity, unsigned char* feasible);
+
+/* The same profile over the paths of this device's last hastar_find_path_batch, which
+ * stay packed in HBM (local_planner.cpp:316-323 profiles the search's own output): no path
+ * upload.  n must equal that batch's planner count; path i has the len[i] points the batch
+ * returned (0 points: feasible[i] = 0, no velocities) and velocity receives sum(len)
+ * floats in planner order. */
+int hastar_velocity_profile_last_batch(int device, const hastar_velocity_params* vp, int n, const float* vel_init,
+                                       const float* max_velocity_curr, const unsigned char* flags, float* velocity,
+                                       unsigned char* feasible);
 
 /* Grid size N of the handle. */
 int hastar_grid_size(hastar_handle h);

@@ -11,6 +11,8 @@
 // Differences a caller can observe:
 //   * only T = float exists (the ROS node instantiates float, local_planner.cpp:509);
 //   * a HIP/device failure throws std::runtime_error (the reference has no device to fail);
+//   * a search ended by HASTAR_MAX_POPS_HARD or by exhausted device memory returns
+//     {FLT_MAX, false} (the reference has no pop limit and would throw bad_alloc);
 //   * find_path appends to `path`/`curvature` like the reference does for the empty
 //     vectors its caller passes (HybridAStar.cpp:208-262 mixes push_back and resize, so
 //     non-empty inputs are not a supported contract there either);
@@ -135,6 +137,11 @@ class HybridAStar<float> {
       _curv.resize(_cap);
       rc = hastar_copy_path(_h, _xyh.data(), _curv.data(), (int)_cap, &len);
     }
+    // A search never stops at a fixed arena size (it is parked and resumed in a larger one),
+    // so HASTAR_EOVERFLOW only means an explicit HASTAR_MAX_POPS_HARD budget or exhausted
+    // device memory: reported as the reference's failure pair, like a search that found
+    // no path, not as an exception the unchanged caller would not catch.
+    if (rc == HASTAR_EOVERFLOW) return {std::numeric_limits<float>::max(), false};
     check(rc);
     for (int i = 0; i < len; ++i) {
       path.emplace_back(_xyh[3 * i], _xyh[3 * i + 1], _xyh[3 * i + 2]);

@@ -24,7 +24,9 @@
 //   * float/double promotions follow the reference expressions (M_PI literals,
 //     std::fmod(float, double), std::pow(double, 2) -> x*x as GCC folds it);
 //   * transcendental calls go to the host glibc libm, like the reference.
-// Build: oracle/Makefile (g++ -O2 -ffp-contract=off, x86-64 baseline ISA).
+// Build: oracle/Makefile (g++ -O3 -ffp-contract=off, x86-64 baseline ISA; -O3 as the
+// reference's CMakeLists.txt:128 build, so the CPU timing proxy uses the same optimisation).
+#include <atomic>
 #include <cmath>
 #include <cfloat>
 #include <cstdint>
@@ -36,10 +38,14 @@
 #include <algorithm>
 #include <numeric>
 #include <chrono>
+#include <thread>
 
 #include "../include/hastar.h"
 
 namespace orc {
+// Optional pop limit for census tools (0 = none, the reference's behaviour): a search that
+// reaches it stops with stats.status = HASTAR_EOVERFLOW and is reported as failed.
+long long g_max_pops = 0;
 #ifdef ORC_SHAPE_STATS
 long long g_shape[8];
 #endif
@@ -646,6 +652,10 @@ template <class T> struct Planner {
     uint64_t dig = 0x243f6a8885a308d3ull;
     std::pair<T, bool> out{std::numeric_limits<T>::max(), false};
     while (!op3.empty()) {
+      if (g_max_pops > 0 && st.pops >= g_max_pops) {
+        st.status = HASTAR_EOVERFLOW;
+        break;
+      }
       auto it = op3.begin();
       const N3<T>* cur = &*cl3.insert(*it).first;
       op3.erase(it);
@@ -698,6 +708,7 @@ template <class T> struct Planner {
       cd += mix64(((uint64_t)(uint32_t)n.cx << 40) | ((uint64_t)(uint32_t)n.cy << 16) | (uint64_t)(uint32_t)n.bin);
     st.closed_digest = cd;
     st.via_shot = shot_ok ? 1 : 0;
+    if (st.status != 0) out = {std::numeric_limits<T>::max(), false};
     return out;
   }
   // HybridAStar::find_path (HybridAStar.cpp:68-88) incl. Grid3D::set_start_node (127-160)
@@ -1000,6 +1011,45 @@ extern "C" void orc_libm(int fn, const float* a, const float* b, float* out, int
     }
     out[i] = v;
   }
+}
+
+extern "C" void orc_set_max_pops(long long n) { orc::g_max_pops = n; }
+
+// CPU baseline (bench.py cpu_baseline): `threads` std::threads, each taking whole planners
+// from a shared counter (one private planner per thread at a time, as BASELINE.md's plan
+// says), and running `replans` x (reset + find_path) on it, timed around find_path only
+// (test_hybrid_astar.cpp:123-126).  out[0] = total pops, out[1] = wall seconds of the
+// parallel region, out[2] = sum of find_path seconds (for the mean plan latency), out[3] =
+// plans; per_plan_ms (n x replans, may be null) receives each plan's latency.
+extern "C" void orc_run_batch_threads(void* const* hs, int n, const float* vel, const float* starts, int replans,
+                                      int threads, double* out, double* per_plan_ms) {
+  std::atomic<int> next{0};
+  std::atomic<long long> pops{0};
+  std::vector<double> tsum((size_t)std::max(threads, 1), 0.0);
+  auto work = [&](int t) {
+    for (int i = next++; i < n; i = next++) {
+      auto* P = static_cast<OP*>(hs[i]);
+      for (int r = 0; r < replans; ++r) {
+        P->reset();
+        std::vector<orc::P3<float>> path;
+        std::vector<float> cv;
+        const auto t0 = std::chrono::steady_clock::now();
+        P->find_path(vel[i], {starts[3 * i], starts[3 * i + 1], starts[3 * i + 2]}, path, cv);
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        tsum[t] += s;
+        if (per_plan_ms) per_plan_ms[(size_t)i * replans + r] = s * 1e3;
+        pops += P->st.pops;
+      }
+    }
+  };
+  const auto w0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> pool;
+  for (int t = 0; t < std::max(threads, 1); ++t) pool.emplace_back(work, t);
+  for (auto& th : pool) th.join();
+  out[1] = std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
+  out[0] = (double)pops.load();
+  out[2] = std::accumulate(tsum.begin(), tsum.end(), 0.0);
+  out[3] = (double)n * replans;
 }
 
 #ifdef ORC_SHAPE_STATS

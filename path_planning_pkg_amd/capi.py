@@ -52,6 +52,8 @@ class HastarStats(C.Structure):
         ("closed_digest", C.c_ulonglong),
         ("via_shot", C.c_int),
         ("status", C.c_int),
+        ("parks", C.c_int),
+        ("pad", C.c_int),
     ]
 
     def as_dict(self):

@@ -179,7 +179,7 @@ struct DeviceCtx {
   SearchResult* h_results = nullptr;   // pinned
   long long* d_off = nullptr;          // path point offsets of the packed hand-back
   int* d_len = nullptr;
-  long long* h_offlen = nullptr;       // pinned: n offsets then n lengths (as int)
+  long long* h_offlen = nullptr;       // pinned: n + 1 offsets then n lengths (as int)
   int batch_cap = 0;
   // packed paths of a batch (device staging + pinned host copy)
   float* d_pxyh = nullptr;
@@ -189,6 +189,20 @@ struct DeviceCtx {
   size_t pts_cap = 0;
   uint32_t** d_ptrs = nullptr;  // bitmap pointers of a batched reset
   size_t ptrs_cap = 0;
+  int last_n = 0;                 // the last batch's packed paths (d_pxyh/d_pcurv, offsets d_off)
+  long long last_total = 0;
+  char* vel_slab = nullptr;       // velocity-profile staging (grown, reused)
+  size_t vel_cap = 0;
+  SlotArena* d_resume = nullptr;  // arena descriptors of a resume launch
+  int* d_resume_order = nullptr;
+  size_t resume_cap = 0;
+};
+
+// A larger arena that continues one parked search (hastar_find_path_batch).
+struct ResumeArena {
+  void* slab = nullptr;
+  SlotArena desc{};
+  int planner = -1;
 };
 DeviceCtx g_dev[64];
 
@@ -219,6 +233,23 @@ int device_ctx(int dev, DeviceCtx** out) {
   return 0;
 }
 
+// the velocity-profile staging slab: grown on demand, kept (hipFree would synchronise the
+// device, stalling a search batch in flight on it)
+int vel_slab_acquire(DeviceCtx& D, size_t bytes) {
+  if (D.vel_cap >= bytes) return 0;
+  HIPCHK(hipStreamSynchronize(D.stream));
+  if (D.vel_slab) hipFree(D.vel_slab);
+  D.vel_slab = nullptr;
+  D.vel_cap = 0;
+  const size_t want = bytes + bytes / 2;
+  if (hipMalloc(reinterpret_cast<void**>(&D.vel_slab), want) != hipSuccess) {
+    D.vel_slab = nullptr;
+    return fail(HASTAR_ENOMEM, "velocity_profile: hipMalloc failed");
+  }
+  D.vel_cap = want;
+  return 0;
+}
+
 int scratch_acquire(DeviceCtx& D, size_t NN) {
   if (D.scratch_cap >= NN) return 0;
   if (D.tmp) hipFree(D.tmp);
@@ -236,6 +267,62 @@ int scratch_acquire(DeviceCtx& D, size_t NN) {
   return 0;
 }
 
+// Byte layout of one arena covering `r` (a slot arena of the pool, or a resume arena).
+struct ArenaLayout {
+  size_t open3, closed3, slots, open2, cell, gens, dub, dubc, chain, prevl;
+  size_t total() const { return open3 + closed3 + slots + open2 + cell + gens + dub + dubc + chain + prevl; }
+};
+ArenaLayout arena_layout(const ArenaReq& r) {
+  ArenaLayout L;
+  L.open3 = align256((size_t)r.open3 * sizeof(Node3));
+  L.closed3 = align256((size_t)r.closed3 * sizeof(Closed3));
+  L.slots = align256((size_t)r.slots * sizeof(Slot3));
+  L.open2 = align256((size_t)r.open2 * sizeof(Node2));
+  L.cell = align256(r.cells * sizeof(Cell2));
+  L.gens = 256;
+  L.dub = align256((size_t)r.dub * 3 * sizeof(float));
+  L.dubc = align256((size_t)r.dub * sizeof(float));
+  L.chain = align256((size_t)r.chain * sizeof(int));
+  L.prevl = align256((size_t)ASTAR_LDS_CAP * sizeof(int));
+  return L;
+}
+// Carve the arena at `q` and queue the clearing of its generation-stamped tables.
+hipError_t carve_arena(char* q, const ArenaReq& r, const ArenaLayout& L, SlotArena* out, hipStream_t st) {
+  SlotArena& A = *out;
+  std::memset(&A, 0, sizeof(A));
+  A.open3 = reinterpret_cast<Node3*>(q); q += L.open3;
+  A.closed3 = reinterpret_cast<Closed3*>(q); q += L.closed3;
+  A.slots3 = reinterpret_cast<Slot3*>(q); q += L.slots;
+  A.open2 = reinterpret_cast<Node2*>(q); q += L.open2;
+  A.cell2 = reinterpret_cast<Cell2*>(q); q += L.cell;
+  A.gens = reinterpret_cast<uint32_t*>(q); q += L.gens;
+  A.dub_xyh = reinterpret_cast<float*>(q); q += L.dub;
+  A.dub_curv = reinterpret_cast<float*>(q); q += L.dubc;
+  A.out_chain = reinterpret_cast<int*>(q); q += L.chain;
+  A.prevl = reinterpret_cast<int*>(q); q += L.prevl;
+  A.open3_cap = r.open3;
+  A.closed3_cap = r.closed3;
+  A.slots3_mask = r.slots - 1;
+  A.open2_cap = r.open2;
+  A.cells = r.cells;
+  A.dub_cap = r.dub;
+  A.chain_cap = r.chain;
+  // generation-stamped tables start at generation 0 (all stale)
+  hipError_t e = hipMemsetAsync(A.slots3, 0, L.slots, st);
+  if (e == hipSuccess) e = hipMemsetAsync(A.cell2, 0, L.cell, st);
+  if (e == hipSuccess) e = hipMemsetAsync(A.gens, 0, L.gens, st);
+  return e;
+}
+// Outer-search capacities of an arena for `pops` pops (a pop frees one open node and adds
+// at most `span` successors; a replacement erases before it inserts).
+void size_outer(ArenaReq& R, long long pops, int span) {
+  R.open3 = (int)std::min<long long>(2 + (long long)(span - 1) * pops + 64, (long long)INT32_MAX / 2);
+  R.closed3 = (int)std::min<long long>(pops + 1, (long long)SLOT3_IDX_MASK);
+  R.slots = 1;
+  while (R.slots < 2u * (uint32_t)R.closed3 + 64) R.slots <<= 1;
+  R.chain = R.closed3 + 2;
+}
+
 // (Re)build the arena pool so that n arenas each cover `need`.
 // The pool may come out smaller than n when n arenas do not fit the memory budget.
 int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
@@ -250,14 +337,8 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
   D.slab = nullptr;
   D.d_arenas = nullptr;
   D.n_arenas = 0;
-  const size_t b_open3 = align256((size_t)r.open3 * sizeof(Node3)), b_closed3 = align256((size_t)r.closed3 * sizeof(Closed3));
-  const size_t b_slots = align256((size_t)r.slots * sizeof(Slot3)), b_open2 = align256((size_t)r.open2 * sizeof(Node2));
-  const size_t b_cell = align256(r.cells * sizeof(Cell2));
-  const size_t b_gens = 256, b_dub = align256((size_t)r.dub * 3 * sizeof(float));
-  const size_t b_dubc = align256((size_t)r.dub * sizeof(float)), b_chain = align256((size_t)r.chain * sizeof(int));
-  const size_t b_prevl = align256((size_t)ASTAR_LDS_CAP * sizeof(int));
-  const size_t per =
-      b_open3 + b_closed3 + b_slots + b_open2 + b_cell + b_gens + b_dub + b_dubc + b_chain + b_prevl;
+  const ArenaLayout lay = arena_layout(r);
+  const size_t per = lay.total();
   // memory budget of the pool: HASTAR_ARENA_MB, else HASTAR_ARENA_FRAC (default 0.8) of
   // the free HBM
   size_t budget = 0;
@@ -278,32 +359,7 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
   }
   std::vector<SlotArena> host(n);
   char* base = static_cast<char*>(D.slab);
-  for (int i = 0; i < n; ++i) {
-    char* q = base + per * (size_t)i;
-    SlotArena& A = host[i];
-    std::memset(&A, 0, sizeof(A));
-    A.open3 = reinterpret_cast<Node3*>(q); q += b_open3;
-    A.closed3 = reinterpret_cast<Closed3*>(q); q += b_closed3;
-    A.slots3 = reinterpret_cast<Slot3*>(q); q += b_slots;
-    A.open2 = reinterpret_cast<Node2*>(q); q += b_open2;
-    A.cell2 = reinterpret_cast<Cell2*>(q); q += b_cell;
-    A.gens = reinterpret_cast<uint32_t*>(q); q += b_gens;
-    A.dub_xyh = reinterpret_cast<float*>(q); q += b_dub;
-    A.dub_curv = reinterpret_cast<float*>(q); q += b_dubc;
-    A.out_chain = reinterpret_cast<int*>(q); q += b_chain;
-    A.prevl = reinterpret_cast<int*>(q); q += b_prevl;
-    A.open3_cap = r.open3;
-    A.closed3_cap = r.closed3;
-    A.slots3_mask = r.slots - 1;
-    A.open2_cap = r.open2;
-    A.cells = r.cells;
-    A.dub_cap = r.dub;
-    A.chain_cap = r.chain;
-    // generation-stamped tables start at generation 0 (all stale)
-    HIPCHK(hipMemsetAsync(A.slots3, 0, b_slots, D.stream));
-    HIPCHK(hipMemsetAsync(A.cell2, 0, b_cell, D.stream));
-    HIPCHK(hipMemsetAsync(A.gens, 0, b_gens, D.stream));
-  }
+  for (int i = 0; i < n; ++i) HIPCHK(carve_arena(base + per * (size_t)i, r, lay, &host[i], D.stream));
   HIPCHK(dalloc(&D.d_arenas, (size_t)n));
   HIPCHK(hipMemcpyAsync(D.d_arenas, host.data(), (size_t)n * sizeof(SlotArena), hipMemcpyHostToDevice, D.stream));
   HIPCHK(hipStreamSynchronize(D.stream));
@@ -321,7 +377,8 @@ struct hastar_handle_s {
   DeviceCtx* dc = nullptr;
   PlannerDev desc{};            // host copy of the descriptor (device copies are batch-local)
   float lp_min = 0, lp_max = 0, lp_free = 0;
-  int max_pops = 0;
+  int max_pops = 0;              // initial outer-search arena capacity in pops
+  int span = 2;
   ArenaReq areq;
   std::vector<float> curv_abs;
   // grid-frame state (Grid2D::_grid_heading/_goal_location, Grid3D::_goal_location3D)
@@ -382,7 +439,8 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   if (p->num_steering < 1 || p->num_steering > 16 || !p->steering || !p->curvature_weights)
     return fail(HASTAR_EINVAL, "num_steering must be in [1, 16] with steering/curvature_weights arrays");
   if (p->num_actions < 0) return fail(HASTAR_EINVAL, "num_actions must be >= 0");
-  if (p->max_pops > (int)SLOT3_IDX_MASK - 1) return fail(HASTAR_EINVAL, "max_pops must be below 2^20 - 1");
+  if (p->max_pops > (int)SLOT3_IDX_MASK - 1) return fail(HASTAR_EINVAL, "max_pops must be below 2^24 - 1");
+  if (p->max_pops < 0) return fail(HASTAR_EINVAL, "max_pops must be >= 0");
   if (!(p->grid_resolution > 0) || !(p->step_size > 0)) return fail(HASTAR_EINVAL, "resolution/step must be > 0");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -472,10 +530,10 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   // replacement erases before it inserts), so after max_pops pops at most
   // 1 + max_pops * (span - 1) are live; freed nodes are reused before the pool grows
   const int span = std::max(2, std::min(2 * D.na + 1, D.nsteer));
-  R.open3 = 2 + (span - 1) * h->max_pops + 64;
-  R.closed3 = h->max_pops + 1;
-  R.slots = 1;
-  while (R.slots < 2u * (uint32_t)h->max_pops + 64) R.slots <<= 1;
+  h->span = span;
+  D.arena_pops = h->max_pops;
+  D.span_alloc = span;
+  size_outer(R, h->max_pops, span);
   // inner A*: the closed records are bounded by the cells (N^2); the open tree by its
   // frontier, which stays far below N^2 (max_astar_nodes, default min(N^2 + 16, 65536))
   const int astar_cap =
@@ -488,7 +546,6 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
     dub_cap = (int)(span / D.step) + 2 * (int)(2 * M_PI / D.ang_step + 2) + 64;
   }
   R.dub = dub_cap;
-  R.chain = h->max_pops + 2;
   // path buffer of the planner: Dubins samples + the prev chain of the terminal node.  A
   // chain visits distinct (cell, bin) keys one step apart, so 8 N poses cover any
   // realistic path; a longer one ends the search with HASTAR_ENOSPC (reported, never
@@ -909,6 +966,8 @@ static void fill_stats(const SearchResult& R, hastar_stats* st) {
   st->closed_digest = R.closed_digest;
   st->via_shot = R.via_shot;
   st->status = R.status;
+  st->parks = R.parks;
+  st->pad = 0;
 }
 
 static int copy_path_out(hastar_handle h, float* xyh, float* curv, int cap, int* len, hipStream_t st) {
@@ -934,12 +993,10 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   if (!hs || n <= 0 || !vel || !starts || !len || !cost || !ok || cap < 0 || (cap > 0 && (!xyh || !curv)))
     return fail(HASTAR_EINVAL, "bad argument");
   const int dev = hs[0] ? hs[0]->device : -1;
-  int max_pops = 0;
   ArenaReq need;
   for (int i = 0; i < n; ++i) {
     if (!hs[i] || hs[i]->device != dev) return fail(HASTAR_EINVAL, "null handle or handles on different devices");
     if (!hs[i]->goal_set) return fail(HASTAR_EINVAL, "update_goal must be called before find_path");
-    max_pops = std::max(max_pops, hs[i]->max_pops);
     need.merge(hs[i]->areq);
   }
   HIPCHK(hipSetDevice(dev));
@@ -970,10 +1027,10 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     HIPCHK(dalloc(&DC.d_descs, (size_t)n));
     HIPCHK(dalloc(&DC.d_order, (size_t)n));
     HIPCHK(dalloc(&DC.d_results, (size_t)n));
-    HIPCHK(dalloc(&DC.d_off, (size_t)n));
+    HIPCHK(dalloc(&DC.d_off, (size_t)n + 1));
     HIPCHK(dalloc(&DC.d_len, (size_t)n));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_results), (size_t)n * sizeof(SearchResult)));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_offlen), (size_t)n * 2 * sizeof(long long)));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_offlen), ((size_t)n * 2 + 1) * sizeof(long long)));
     DC.batch_cap = n;
   }
   std::vector<PlannerDev> descs(n);
@@ -988,7 +1045,6 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return hs[a]->last_pops > hs[b]->last_pops; });
   HIPCHK(hipMemcpyAsync(DC.d_descs, descs.data(), (size_t)n * sizeof(PlannerDev), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(DC.d_order, order.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
-  HIPCHK(hipEventRecord(DC.ev0, st));
   // raised issue priority for the head of the longest-first queue (HASTAR_PRIO_N overrides)
   int n_prio = std::max(1, slots / 8);
   if (const char* e = std::getenv("HASTAR_PRIO_N")) n_prio = std::atoi(e);
@@ -998,21 +1054,137 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   // profiles/iso_sweep_r01g.txt) for ~5 of 1536 slots.  HASTAR_ISO = 0 off, 1 SIMD, 2 CU.
   int iso = n > slots ? 2 : 0;
   if (const char* e = std::getenv("HASTAR_ISO")) iso = std::atoi(e);
-  HIPCHK(launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, max_pops, iso, st));
-  HIPCHK(hipEventRecord(DC.ev1, st));
-  HIPCHK(hipMemcpyAsync(DC.h_results, DC.d_results, (size_t)n * sizeof(SearchResult), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  float ms = 0.0f;
-  hipEventElapsedTime(&ms, DC.ev0, DC.ev1);
-  g_last_ms = ms;
+  // an explicit pop budget (0 = none: a search runs until the reference's loop would end)
+  long long hard_pops = 0;
+  if (const char* e = std::getenv("HASTAR_MAX_POPS_HARD")) hard_pops = std::atoll(e);
+  // every result starts as "not run" (a wave that parks a search stops taking work, so a
+  // launch can end with queue entries nobody took)
+  HIPCHK(hipMemsetAsync(DC.d_results, 0xff, (size_t)n * sizeof(SearchResult), st));
+  float ms_total = 0.0f;
+  auto timed = [&](auto&& launch) -> int {
+    HIPCHK(hipEventRecord(DC.ev0, st));
+    HIPCHK(launch());
+    HIPCHK(hipEventRecord(DC.ev1, st));
+    HIPCHK(hipMemcpyAsync(DC.h_results, DC.d_results, (size_t)n * sizeof(SearchResult), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0.0f;
+    hipEventElapsedTime(&ms, DC.ev0, DC.ev1);
+    ms_total += ms;
+    return 0;
+  };
+  if (int r = timed([&] { return launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next,
+                                               hard_pops, iso, st); }))
+    return r;
+  // Parked searches (their arena could not take one more pop) continue in larger arenas,
+  // planners no wave took run in a new queue pass: until every search has ended.
+  {
+    std::vector<char> in_resume(n, 0);      // 1: the planner's last launch was a resume launch
+    std::vector<ResumeArena> cur, nxt;      // resume arenas of the last resume launch, by index
+    std::vector<int> notrun, parked;
+    for (;;) {
+      notrun.clear();
+      parked.clear();
+      for (int i = 0; i < n; ++i) {
+        const int stt = DC.h_results[i].status;
+        if (stt == SEARCH_NOT_RUN) notrun.push_back(i);
+        else if (stt == SEARCH_PARKED) parked.push_back(i);
+      }
+      if (notrun.empty() && parked.empty()) break;
+      // 1. move every parked search into an arena 4x its current outer capacity
+      nxt.clear();
+      for (int i : parked) {
+        const SearchResult& R = DC.h_results[i];
+        const SlotArena* from = nullptr;
+        SlotArena host_from;
+        if (in_resume[i]) {
+          from = &cur[(size_t)R.park_arena].desc;
+        } else {
+          HIPCHK(hipMemcpy(&host_from, DC.d_arenas + R.park_arena, sizeof(SlotArena), hipMemcpyDeviceToHost));
+          from = &host_from;
+        }
+        // the planner's capacity after R.parks parks (4x each), as the kernel computes it
+        const long long was = std::min((long long)hs[i]->max_pops << (2 * std::min(R.parks - 1, 12)),
+                                       (long long)SLOT3_IDX_MASK - 1);
+        const long long pops = std::min((long long)hs[i]->max_pops << (2 * std::min(R.parks, 12)),
+                                        (long long)SLOT3_IDX_MASK - 1);
+        ArenaReq r = need;
+        size_outer(r, pops, hs[i]->span);
+        ResumeArena ra;
+        const size_t bytes = arena_layout(r).total();
+        if (pops <= was || hipMalloc(&ra.slab, bytes) != hipSuccess) {
+          // no larger arena can be had: this search ends here, reported as an overflow
+          if (ra.slab) hipFree(ra.slab);
+          DC.h_results[i].status = HASTAR_EOVERFLOW;
+          DC.h_results[i].ok = 0;
+          DC.h_results[i].path_len = 0;
+          HIPCHK(hipMemcpyAsync(DC.d_results + i, DC.h_results + i, sizeof(SearchResult), hipMemcpyHostToDevice, st));
+          continue;
+        }
+        HIPCHK(carve_arena(static_cast<char*>(ra.slab), r, arena_layout(r), &ra.desc, st));
+        HIPCHK(hipMemcpyAsync(ra.desc.open3, from->open3, (size_t)R.ps3_next * sizeof(Node3), hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(ra.desc.closed3, from->closed3, (size_t)R.n_closed3 * sizeof(Closed3),
+                              hipMemcpyDeviceToDevice, st));
+        ra.planner = i;
+        nxt.push_back(ra);
+      }
+      HIPCHK(hipStreamSynchronize(st));
+      for (ResumeArena& ra : cur) hipFree(ra.slab);  // their states have been copied out
+      cur.swap(nxt);
+      // 2. planners no wave took: a new queue pass over the slot arenas (free again)
+      if (!notrun.empty()) {
+        HIPCHK(hipMemcpyAsync(DC.d_order, notrun.data(), notrun.size() * sizeof(int), hipMemcpyHostToDevice, st));
+        for (int i : notrun) in_resume[i] = 0;
+        const int w = std::min<int>(slots, (int)notrun.size());
+        if (int r = timed([&] { return launch_search(DC.d_descs, (int)notrun.size(), DC.d_arenas, w, DC.d_order, 0,
+                                                     DC.d_next, hard_pops, 0, st); }))
+          return r;
+      }
+      // 3. the parked searches continue, one wave each
+      if (!cur.empty()) {
+        std::vector<SlotArena> descs_r(cur.size());
+        std::vector<int> ord(cur.size());
+        for (size_t k = 0; k < cur.size(); ++k) {
+          descs_r[k] = cur[k].desc;
+          ord[k] = cur[k].planner;
+          in_resume[cur[k].planner] = 1;
+        }
+        if (cur.size() > DC.resume_cap) {
+          if (DC.d_resume) hipFree(DC.d_resume);
+          if (DC.d_resume_order) hipFree(DC.d_resume_order);
+          DC.d_resume = nullptr;
+          DC.d_resume_order = nullptr;
+          DC.resume_cap = 0;
+          HIPCHK(dalloc(&DC.d_resume, cur.size()));
+          HIPCHK(dalloc(&DC.d_resume_order, cur.size()));
+          DC.resume_cap = cur.size();
+        }
+        HIPCHK(hipMemcpyAsync(DC.d_resume, descs_r.data(), cur.size() * sizeof(SlotArena), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(DC.d_resume_order, ord.data(), ord.size() * sizeof(int), hipMemcpyHostToDevice, st));
+        if (int r = timed([&] { return launch_resume(DC.d_descs, (int)cur.size(), DC.d_resume, DC.d_resume_order,
+                                                     hard_pops, st); }))
+          return r;
+      } else if (notrun.empty()) {
+        break;
+      }
+    }
+    for (ResumeArena& ra : cur) hipFree(ra.slab);
+  }
+  g_last_ms = ms_total;
   int rc = HASTAR_OK;
-  // pack the paths that fit the caller's buffers: offsets, one gather kernel, one copy
+  // pack the paths that fit the caller's buffers: offsets, one gather kernel, one copy.
+  // Every planner reports its own outcome in stats[i].status: 0, HASTAR_EOVERFLOW (the
+  // search needed more device memory than it could get, or hit HASTAR_MAX_POPS_HARD),
+  // HASTAR_ENOSPC (kernel: path longer than the planner's output buffer; host: longer than
+  // `cap` — then len[i] is the length needed and hastar_copy_path fetches it).  The return
+  // code is the first ENOSPC, else the first EOVERFLOW.
   long long* h_off = DC.h_offlen;
-  int* h_len = reinterpret_cast<int*>(DC.h_offlen + n);
+  int* h_len = reinterpret_cast<int*>(DC.h_offlen + n + 1);
   long long total = 0;
+  int rc_over = HASTAR_OK;
   for (int i = 0; i < n; ++i) {
-    const SearchResult& R = DC.h_results[i];
+    SearchResult& R = DC.h_results[i];
     hastar_handle h = hs[i];
+    if (R.status == -75) R.ok = 0;
     h->last = R;
     h->have_last = true;
     // longest-first key: the search's own duration (s_memrealtime ticks) — it weighs outer
@@ -1022,20 +1194,26 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     cost[i] = R.ok ? R.cost : FLT_MAX;
     fill_stats(R, stats ? &stats[i] : nullptr);
     len[i] = R.path_len;
-    if (R.status != 0 && rc == HASTAR_OK) {
-      rc = R.status == -75 ? HASTAR_EOVERFLOW : HASTAR_ENOSPC;
-      g_err = R.status == -75 ? "search arena overflow (raise max_pops / max_astar_nodes)"
-                              : "path longer than the planner's output buffer";
+    if (R.status == -75 && rc_over == HASTAR_OK) {
+      rc_over = HASTAR_EOVERFLOW;
+      g_err = "search ended by an arena overflow (device memory) or HASTAR_MAX_POPS_HARD";
+    } else if (R.status == -28 && rc == HASTAR_OK) {
+      rc = fail(HASTAR_ENOSPC, "path longer than the planner's output buffer");
     }
     int take = R.path_len;
     if (take > cap) {
       take = 0;  // the caller fetches it with hastar_copy_path
+      if (stats) stats[i].status = HASTAR_ENOSPC;
       if (rc == HASTAR_OK) rc = fail(HASTAR_ENOSPC, "path buffer too small");
     }
     h_off[i] = total;
     h_len[i] = take;
     total += take;
   }
+  if (rc == HASTAR_OK && rc_over != HASTAR_OK) rc = rc_over;
+  h_off[n] = total;
+  DC.last_n = n;
+  DC.last_total = total;
   if (total > 0) {
     if ((size_t)total > DC.pts_cap) {
       if (DC.d_pxyh) hipFree(DC.d_pxyh);
@@ -1051,7 +1229,7 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
       HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_pcurv), c2 * sizeof(float)));
       DC.pts_cap = c2;
     }
-    HIPCHK(hipMemcpyAsync(DC.d_off, h_off, (size_t)n * sizeof(long long), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(DC.d_off, h_off, ((size_t)n + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(DC.d_len, h_len, (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
     HIPCHK(launch_gather_paths(DC.d_descs, DC.d_off, DC.d_len, n, DC.d_pxyh, DC.d_pcurv, st));
     HIPCHK(hipMemcpyAsync(DC.h_pxyh, DC.d_pxyh, (size_t)total * 3 * sizeof(float), hipMemcpyDeviceToHost, st));
@@ -1092,16 +1270,16 @@ int hastar_velocity_profile_batch(int device, const hastar_velocity_params* vp, 
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev || device > 63)
     return fail(HASTAR_EDEVICE, "velocity_profile: no HIP device " + std::to_string(device));
+  std::lock_guard<std::mutex> lk(g_dev[device].mu);  // the device context and its stream
   DeviceCtx* D = nullptr;
   if (int r = device_ctx(device, &D)) return r;
   HIPCHK(hipSetDevice(device));
   const size_t b_off = align256((n + 1) * sizeof(long long)), b_xyh = align256(3 * pts * sizeof(float)),
                b_pt = align256(pts * sizeof(float)), b_pf = align256(n * sizeof(float)), b_pb = align256(n);
   const size_t total = b_off + b_xyh + 2 * b_pt + 2 * b_pf + 2 * b_pb;
-  char* slab = nullptr;
-  if (hipMalloc(reinterpret_cast<void**>(&slab), total) != hipSuccess)
-    return fail(HASTAR_ENOMEM, "velocity_profile: hipMalloc failed");
-  char* q = slab;
+  hipStream_t st = D->stream;
+  if (int r = vel_slab_acquire(*D, total)) return r;
+  char* q = D->vel_slab;
   auto take = [&](size_t b) { char* r = q; q += b; return r; };
   long long* d_off = reinterpret_cast<long long*>(take(b_off));
   float* d_xyh = reinterpret_cast<float*>(take(b_xyh));
@@ -1111,7 +1289,6 @@ int hastar_velocity_profile_batch(int device, const hastar_velocity_params* vp, 
   float* d_vmax = reinterpret_cast<float*>(take(b_pf));
   unsigned char* d_flags = reinterpret_cast<unsigned char*>(take(b_pb));
   unsigned char* d_feas = reinterpret_cast<unsigned char*>(take(b_pb));
-  hipStream_t st = D->stream;
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) { if (e == hipSuccess) e = x; };
   chk(hipMemcpyAsync(d_off, offsets, (n + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
@@ -1126,8 +1303,49 @@ int hastar_velocity_profile_batch(int device, const hastar_velocity_params* vp, 
   chk(hipMemcpyAsync(velocity, d_vel, pts * sizeof(float), hipMemcpyDeviceToHost, st));
   chk(hipMemcpyAsync(feasible, d_feas, n, hipMemcpyDeviceToHost, st));
   chk(hipStreamSynchronize(st));
-  hipFree(slab);
   if (e != hipSuccess) return fail(HASTAR_EDEVICE, std::string("velocity_profile: ") + hipGetErrorString(e));
+  return HASTAR_OK;
+}
+
+// VelocityGenerator over the paths of the device's last hastar_find_path_batch, which are
+// still packed in HBM (local_planner.cpp:316-323 profiles the search's own output): no
+// path upload.  Path i is the batch's planner i with len[i] points at the offsets the
+// batch packed (a planner with len 0 gets feasible 0 and no velocities).
+int hastar_velocity_profile_last_batch(int device, const hastar_velocity_params* vp, int n, const float* vel_init,
+                                       const float* max_velocity_curr, const unsigned char* flags, float* velocity,
+                                       unsigned char* feasible) {
+  if (!vp || n < 0 || (n > 0 && (!vel_init || !max_velocity_curr || !flags || !feasible)))
+    return fail(HASTAR_EINVAL, "velocity_profile_last_batch: null argument");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev || device > 63)
+    return fail(HASTAR_EDEVICE, "velocity_profile_last_batch: no HIP device " + std::to_string(device));
+  std::lock_guard<std::mutex> lk(g_dev[device].mu);
+  DeviceCtx* D = nullptr;
+  if (int r = device_ctx(device, &D)) return r;
+  if (n != D->last_n) return fail(HASTAR_EINVAL, "velocity_profile_last_batch: n differs from the last batch");
+  if (n == 0) return HASTAR_OK;
+  const size_t pts = (size_t)D->last_total;
+  if (pts > 0 && !velocity) return fail(HASTAR_EINVAL, "velocity_profile_last_batch: null velocity");
+  HIPCHK(hipSetDevice(device));
+  const size_t b_pt = align256(std::max<size_t>(pts, 1) * sizeof(float)), b_pf = align256(n * sizeof(float)),
+               b_pb = align256(n);
+  if (int r = vel_slab_acquire(*D, b_pt + 2 * b_pf + 2 * b_pb)) return r;
+  char* q = D->vel_slab;
+  float* d_vel = reinterpret_cast<float*>(q); q += b_pt;
+  float* d_v0 = reinterpret_cast<float*>(q); q += b_pf;
+  float* d_vmax = reinterpret_cast<float*>(q); q += b_pf;
+  unsigned char* d_flags = reinterpret_cast<unsigned char*>(q); q += b_pb;
+  unsigned char* d_feas = reinterpret_cast<unsigned char*>(q);
+  hipStream_t st = D->stream;
+  HIPCHK(hipMemcpyAsync(d_v0, vel_init, n * sizeof(float), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_vmax, max_velocity_curr, n * sizeof(float), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_flags, flags, n, hipMemcpyHostToDevice, st));
+  const hastar::VelParams P{vp->max_velocity, vp->coast_velocity, vp->max_lat_acc, vp->max_lat_acc * vp->max_lat_acc,
+                            vp->max_long_acc, vp->max_long_dec};
+  HIPCHK(hastar::launch_velocity_profile(P, n, D->d_off, D->d_pxyh, D->d_pcurv, d_v0, d_vmax, d_flags, d_vel, d_feas, st));
+  if (pts > 0) HIPCHK(hipMemcpyAsync(velocity, d_vel, pts * sizeof(float), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(feasible, d_feas, n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
   return HASTAR_OK;
 }
 

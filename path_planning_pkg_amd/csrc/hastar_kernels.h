@@ -5,7 +5,9 @@
 
 namespace hastar {
 hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots, const int* d_order, int n_prio,
-                         int* d_next, int max_pops, int iso, hipStream_t st);
+                         int* d_next, long long hard_pops, int iso, hipStream_t st);
+hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, const int* d_order,
+                         long long hard_pops, hipStream_t st);
 int search_slots_per_cu();
 hipError_t launch_gather_paths(const PlannerDev* d_descs, const long long* d_off, const int* d_len, int n, float* xyh,
                                float* curv, hipStream_t st);

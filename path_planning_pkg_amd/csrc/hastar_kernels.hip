@@ -136,6 +136,38 @@ __device__ __forceinline__ void closed3_next_gen(SearchCtx& c) {
   }
 }
 
+// Resume of a parked search (SearchResult): the host copied the closed records into this
+// arena; their hash slots are rebuilt here with the arena's next generation.  Lanes insert
+// different keys concurrently: a slot is claimed by a compare-and-swap of its generation
+// word, so every probe sequence stays contiguous (claims are never undone).
+__device__ __forceinline__ void closed3_rebuild(SearchCtx& c, int n) {
+  const SlotArena& A = *c.A;
+  const uint32_t gbits = (c.gen3 & SLOT3_GEN_MASK) << SLOT3_IDX_BITS;
+  GAS Slot3* t = gp(A.slots3);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // after a generation-wrap zeroing of the table
+  for (int i = c.lane; i < n; i += 64) {
+    const uint32_t key = gp(A.closed3)[i].key;
+    uint32_t h = slot_hash(key) & A.slots3_mask;
+    uint32_t cur = __hip_atomic_load((uint32_t*)&t[h].gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      if ((cur & ~SLOT3_IDX_MASK) == gbits) {
+        h = (h + 1) & A.slots3_mask;
+        cur = __hip_atomic_load((uint32_t*)&t[h].gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        continue;
+      }
+      const uint32_t prev = atomicCAS((uint32_t*)&t[h].gi, cur, gbits | (uint32_t)i);
+      if (prev == cur) {
+        t[h].key = key;
+        break;
+      }
+      cur = prev;
+    }
+  }
+  // the wave's later plain loads of the table must see the claims and keys
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // -------------------------------------------------------- holonomic A* (AStar.cpp) -----
 // Each lazy A* search (AStar::find_path(int, int), AStar.cpp:100-113) keeps its open
 // tree in LDS as compact nodes (16-bit links, 20 B per node, A_CAP nodes per wavefront);
@@ -824,29 +856,37 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, in
 // ------------------------------------------------------------------- the search -------
 // One find_path (HybridAStar.cpp:68-88 incl. hybrid_a_star_search 93-199 and
 // reconstruct_path 208-262) of planner *c.P in arena *c.A, run by one wavefront.
-__device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLds& alds, int max_pops) {
+// Returns true when the search parked (its arena could not take one more pop; the state
+// stays in this arena, see SearchResult).  resume: continue a parked search whose records
+// the host copied into this (larger) arena.  hard_pops > 0 ends a search after that many
+// pops with HASTAR_EOVERFLOW (an explicit budget; 0 = none, the reference's behaviour).
+__device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLds& alds, long long hard_pops,
+                                           bool resume) {
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
 #ifdef HASTAR_STAMPS
   for (int q = 0; q < NSTAMP; ++q) c.cyc[q] = 0;
 #endif
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   apf_stage(P, apfs, lane);
   c.o3.t = gp(A.open3);
   c.o3.lane = lane;
   c.o3.reset_cache();
   closed3_next_gen(c);
-  c.n_closed3 = 0;
-  c.pops = c.succ = c.apops = c.asearch = c.shots = c.amigr = c.apops_g = 0;
   c.status = 0;
-  c.o3.clear();
-  c.ps3.next = 1;
-  c.ps3.free = NIL;
-
-  // Grid3D::set_start_node soft-resets the start cell's node (Grid3D.cpp:145-148 / 153-154)
-  gp(P.nm_f)[(size_t)P.start_cx * P.N + P.start_cy] = euclid_h(P, P.start_cx, P.start_cy);
-  {
+  int counter = 0, interval = P.shot_interval;
+  bool shot_allowed = false;
+  uint64_t dig = 0x243f6a8885a308d3ull;
+  int parks = 0;
+  if (!resume) {
+    c.n_closed3 = 0;
+    c.pops = c.succ = c.apops = c.asearch = c.shots = c.amigr = c.apops_g = 0;
+    c.o3.clear();
+    c.ps3.next = 1;
+    c.ps3.free = NIL;
+    // Grid3D::set_start_node soft-resets the start cell's node (Grid3D.cpp:145-148 / 153-154)
+    gp(P.nm_f)[(size_t)P.start_cx * P.N + P.start_cy] = euclid_h(P, P.start_cx, P.start_cy);
     Succ s0;
     s0.x = P.start_x;
     s0.y = P.start_y;
@@ -858,16 +898,40 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     s0.cx = P.start_cx;
     s0.cy = P.start_cy;
     insert3(c, s0, FLT_MAX, NIL);
+  } else {
+    // the loop state of the parked search; its open tree (header = node 0) and closed
+    // records were copied into this arena by index
+    const GAS SearchResult* R = gp(P.result);
+    c.pops = R->pops;
+    c.succ = R->successors;
+    c.apops = R->astar_pops;
+    c.asearch = R->astar_searches;
+    c.shots = R->shots;
+    c.amigr = R->astar_migrations;
+    c.apops_g = R->astar_pops_hbm;
+    dig = R->pop_digest;
+    t_start = R->t_start;
+    counter = R->counter;
+    interval = R->interval;
+    shot_allowed = R->shot_allowed != 0;
+    c.n_closed3 = R->n_closed3;
+    c.ps3.next = R->ps3_next;
+    c.ps3.free = R->ps3_free;
+    parks = R->parks;
+    closed3_rebuild(c, c.n_closed3);
   }
   // goal circles are the same for every Dubins evaluation of this search
   const float r = P.r_min;
   const GoalC GC = goal_centres(r, P.goal_x, P.goal_y, P.goal_h);
-  int counter = 0, interval = P.shot_interval;
-  bool shot_allowed = false;
-  uint64_t dig = 0x243f6a8885a308d3ull;
   int ok = 0, via_shot = 0, terminal = NIL, dub_n = 0;
   float cost = FLT_MAX;
+  bool parked = false;
   const int span = 2 * P.na + 1;
+  // the planner's outer capacity after `parks` resumes (4x each), bounded by this arena: a
+  // search parks at the same pop whatever arena the pool happens to hand it
+  const long long pcap = min((long long)P.arena_pops << (2 * min(parks, 12)), (long long)SLOT3_IDX_MASK - 1);
+  const int closed_lim = (int)min((long long)A.closed3_cap, pcap + 1);
+  const int open_lim = (int)min((long long)A.open3_cap, 2 + (long long)(P.span_alloc - 1) * pcap + 64);
   // lanes per candidate action: 16 when the window has at most 4 actions (the Dubins
   // libm calls then spread over the group), else 4 (one Dubins word per lane)
 #ifdef HASTAR_DBG_NARROW
@@ -878,7 +942,12 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
   STAMP_T tloop = STAMP_NOW();
 
   while (!c.o3.empty()) {
-    if (c.pops >= max_pops) { c.status = -75; break; }
+    if (hard_pops > 0 && c.pops >= hard_pops) { c.status = -75; break; }
+    // one more pop needs a closed record and at most `span` open nodes (the pop frees one)
+    if (c.n_closed3 + 1 >= closed_lim || c.ps3.next + span + 1 > open_lim) {
+      parked = true;
+      break;
+    }
     STAMP_T tp = STAMP_NOW();
     const int b = c.o3.begin();
     const Node3 top = c.o3.node(b);  // usually cached: the leftmost node was touched by the last walks
@@ -1095,6 +1164,33 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     if (c.status != 0) break;
   }
   STAMP_ADD(6, tloop);
+  if (parked) {
+    if (lane == 0) {
+      GAS SearchResult* R = gp(P.result);
+      R->pops = c.pops;
+      R->successors = c.succ;
+      R->astar_pops = c.apops;
+      R->astar_searches = c.asearch;
+      R->shots = c.shots;
+      R->astar_migrations = (int)c.amigr;
+      R->astar_pops_hbm = c.apops_g;
+      R->pop_digest = dig;
+      R->t_start = t_start;
+      R->counter = counter;
+      R->interval = interval;
+      R->shot_allowed = shot_allowed ? 1 : 0;
+      R->n_closed3 = c.n_closed3;
+      R->ps3_next = c.ps3.next;
+      R->ps3_free = c.ps3.free;
+      R->parks = parks + 1;
+      R->park_arena = (int)blockIdx.x;
+      R->ok = 0;
+      R->path_len = 0;
+      R->status = SEARCH_PARKED;
+    }
+    wave_lds_sync();
+    return true;
+  }
   if (c.status != 0) ok = 0;
 
   // ---- reconstruct_path (HybridAStar.cpp:208-262) into out_xyh / out_curv
@@ -1174,6 +1270,7 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     R->t_start = t_start;
     R->t_end = __builtin_amdgcn_s_memrealtime();
     R->slot = (int)blockIdx.x;
+    R->parks = parks;
 #ifdef HASTAR_STAMPS
     c.cyc[22] = c.o3.n_fill;
     c.cyc[23] = c.o3.n_step;
@@ -1187,15 +1284,17 @@ __device__ __forceinline__ void search_one(SearchCtx& c, ApfStage& apfs, AStarLd
 #endif
   }
   wave_lds_sync();
+  return false;
 }
 
 // Persistent work-queue kernel: grid = W resident slots (one wavefront each).  Each slot
 // pulls planner indices (in `order`, longest-expected-first when the host knows) from a
 // device counter until the queue is drained, so early finishers take the next planner.
+// resume = 1: wave b continues parked planner order[b] in arena b (no queue).
 __global__ __launch_bounds__(64, HASTAR_WAVES_PER_EU) void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners,
                                                            const SlotArena* __restrict__ arenas,
                                                            const int* __restrict__ order, int* __restrict__ next,
-                                                           int max_pops, int n_prio, int iso) {
+                                                           long long hard_pops, int n_prio, int iso, int resume) {
   __shared__ ApfStage apfs;
   __shared__ AStarLds alds;
   SearchCtx c;
@@ -1204,6 +1303,17 @@ __global__ __launch_bounds__(64, HASTAR_WAVES_PER_EU) void hastar_search_kernel(
   c.lane = threadIdx.x;
   c.gen3 = gp(A.gens)[0];
   c.gen2 = gp(A.gens)[1];
+  if (resume) {
+    if ((int)blockIdx.x < n_planners) {
+      c.P = descs + order[blockIdx.x];
+      search_one(c, apfs, alds, hard_pops, true);
+    }
+    if (c.lane == 0) {
+      gp(A.gens)[0] = c.gen3;
+      gp(A.gens)[1] = c.gen2;
+    }
+    return;
+  }
   // Head isolation (iso = 1: SIMD, 2: CU).  Slot 0 runs queue entry 0, the longest expected
   // search, and publishes its placement (HW_ID bits 4-15: SIMD, CU, SH, SE; XCC_ID); the
   // other waves wait for that (bounded), and the ones sharing its SIMD / CU take no work,
@@ -1241,7 +1351,8 @@ __global__ __launch_bounds__(64, HASTAR_WAVES_PER_EU) void hastar_search_kernel(
     if (q < n_prio) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(0);
     c.P = descs + order[q];
-    search_one(c, apfs, alds, max_pops);
+    // a parked search keeps its state in this wave's arena: the wave takes no more work
+    if (search_one(c, apfs, alds, hard_pops, false)) break;
   }
   if (c.lane == 0) {
     gp(A.gens)[0] = c.gen3;
@@ -1454,6 +1565,10 @@ __global__ __launch_bounds__(64) void k_velocity_profile(VelParams vp, int n, co
   if (p >= n) return;
   const long long o = off[p];
   const int P = (int)(off[p + 1] - o);
+  if (P <= 0) {  // no path (a failed search of a batch): nothing to profile
+    feasible[p] = 0;
+    return;
+  }
   const float* X = xyh + 3 * o;
   const float* K = curv + o;
   float* V = vel + o;
@@ -1600,13 +1715,20 @@ __global__ __launch_bounds__(64) void k_test_dubins_path(PlannerDev P, float sx,
 
 // ------------------------------------------------------------- launch wrappers -------
 hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots, const int* d_order, int n_prio,
-                         int* d_next, int max_pops, int iso, hipStream_t st) {
+                         int* d_next, long long hard_pops, int iso, hipStream_t st) {
   // work counter 0 (1 with isolation: slot 0 takes queue entry 0 itself), no head yet
   const int init[4] = {iso ? 1 : 0, 0, 0, 0};
   hipError_t e = hipMemcpyAsync(d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(hastar_search_kernel, dim3(n_slots), dim3(64), 0, st, d_descs, n, d_arenas, d_order, d_next,
-                     max_pops, n_prio, iso);
+                     hard_pops, n_prio, iso, 0);
+  return hipGetLastError();
+}
+hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, const int* d_order,
+                         long long hard_pops, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hastar_search_kernel, dim3(n), dim3(64), 0, st, d_descs, n, d_arenas, d_order, (int*)nullptr,
+                     hard_pops, 0, 0, 1);
   return hipGetLastError();
 }
 int search_slots_per_cu() {

@@ -75,21 +75,33 @@ constexpr int CELL2_OGEN_SHIFT = 17;
 constexpr uint32_t CELL2_OGEN_MASK = 0x7fffu;
 constexpr uint32_t CELL2_HINT_MASK = 0x1ffffu;
 
-// Closed-set hash slot (open addressing).  gi = generation (12 bits) << 20 | record
+// Closed-set hash slot (open addressing).  gi = generation (8 bits) << 24 | record
 // index; a slot is live iff its generation is the search's, so clear() is O(1).  The
-// generation cycles through 1..4095; when it wraps the wave zeroes its table.
+// generation cycles through 1..255; when it wraps the wave zeroes its table.  24 index
+// bits allow 16 M closed records (a search that outgrows its arena is parked and resumed
+// in a bigger one, see SearchResult).
 struct Slot3 {
   uint32_t key;
   uint32_t gi;
 };
-constexpr int SLOT3_IDX_BITS = 20;
+constexpr int SLOT3_IDX_BITS = 24;
 constexpr uint32_t SLOT3_IDX_MASK = (1u << SLOT3_IDX_BITS) - 1;
-constexpr uint32_t SLOT3_GEN_MASK = 0xfffu;
+constexpr uint32_t SLOT3_GEN_MASK = 0xffu;
 
 // diagnostic phase counters of the search kernel (-DHASTAR_STAMPS)
 constexpr int NSTAMP = 32;
 
+// Search status codes of SearchResult::status besides 0 / HASTAR_E* (host-side only).
+constexpr int SEARCH_NOT_RUN = -1;  // the host's sentinel: no wave took this planner
+constexpr int SEARCH_PARKED = 1;    // the arena filled up at a pop boundary: state kept for a resume
+
 // Per-search result block (written by the search kernel, read by the host).
+// A search whose arena cannot take one more pop PARKS (status SEARCH_PARKED): the open tree
+// and closed records stay in the arena it ran in (arena index park_arena of its launch),
+// and the loop state needed to continue lives here (pop_digest holds the running digest).
+// The host copies the records into a larger arena and relaunches the search in resume
+// mode, so no search the reference would finish is cut short by a fixed capacity
+// (the reference's sets grow without limit, HybridAStar.cpp:107).
 struct SearchResult {
   long long pops, successors, astar_pops, astar_searches, shots, closed_size, astar_pops_hbm;
   unsigned long long pop_digest, closed_digest;
@@ -101,6 +113,11 @@ struct SearchResult {
   unsigned long long cycles[NSTAMP]; // diagnostic build (-DHASTAR_STAMPS): s_memtime per phase
   unsigned long long t_start, t_end;  // s_memrealtime (100 MHz, chip-wide) around the search
   int slot, pad_r;                    // slot (wavefront) that ran it
+  // park state (status == SEARCH_PARKED)
+  int park_arena;                     // arena index (in the launch's arena array) holding the state
+  int counter, interval, shot_allowed;  // Dubins-shot schedule (HybridAStar.cpp:96-154)
+  int n_closed3, ps3_next, ps3_free;  // closed records and open-pool state in that arena
+  int parks;                          // times this search was parked (diagnostic)
 };
 
 // Descriptor of one planner: constants + device pointers.  Lives in HBM; the kernel
@@ -109,7 +126,7 @@ struct PlannerDev {
   // --- grid / vehicle constants (Grid2D.cpp:7-62, VehicleModel.cpp:7-47, HybridAStar.cpp:7-24)
   int N, n2, n45, diag;
   int bins, nsteer, na, shot_interval;
-  int shot_decay, n_apf, pad_i0, pad_i1;
+  int shot_decay, n_apf, arena_pops, span_alloc;  // arena_pops: initial outer capacity in pops (max_pops)
   float res, thr, apf_rep, apf_ang;
   float ts, a_lat, a_lat2, prec;
   float r_min, step, ang_step, act_cost_diag;   // Dubins radius/step; 2D diagonal move cost

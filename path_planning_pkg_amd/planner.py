@@ -73,6 +73,8 @@ def load_library():
     L.hastar_velocity_profile_batch.argtypes = [C.c_int, C.POINTER(HastarVelocityParams), C.c_int,
                                                 C.POINTER(C.c_longlong), fp, fp, fp, fp, C.POINTER(C.c_ubyte), fp,
                                                 C.POINTER(C.c_ubyte)]
+    L.hastar_velocity_profile_last_batch.argtypes = [C.c_int, C.POINTER(HastarVelocityParams), C.c_int, fp, fp,
+                                                     C.POINTER(C.c_ubyte), fp, C.POINTER(C.c_ubyte)]
     _lib = L
     return L
 
@@ -148,6 +150,24 @@ class VelocityGenerator:
             self.device, C.byref(self.params), n, off.ctypes.data_as(C.POINTER(C.c_longlong)), fptr(X), fptr(K),
             fptr(v0), fptr(vm), flags.ctypes.data_as(u8), fptr(vel), feas.ctypes.data_as(u8)))
         return feas, vel
+
+
+    def profile_last_batch(self, lens, vel_init, max_velocity_curr, flags):
+        """Profile the paths of this device's last find_path batch where they already are, in
+        HBM (hastar_velocity_profile_last_batch; local_planner.cpp:316-323): lens = the
+        batch's returned lengths.  Returns (feasible u8[n], velocity f32[sum(lens)])."""
+        n = len(lens)
+        v0, vm = _f32(vel_init), _f32(max_velocity_curr)
+        flags = np.ascontiguousarray(flags, np.uint8)
+        if len(v0) != n or len(vm) != n or len(flags) != n:
+            raise ValueError("profile_last_batch: inconsistent array lengths")
+        vel = np.empty(max(int(np.sum(lens)), 1), np.float32)
+        feas = np.zeros(n, np.uint8)
+        u8 = C.POINTER(C.c_ubyte)
+        _check(load_library().hastar_velocity_profile_last_batch(
+            self.device, C.byref(self.params), n, fptr(v0), fptr(vm), flags.ctypes.data_as(u8), fptr(vel),
+            feas.ctypes.data_as(u8)))
+        return feas, vel[:int(np.sum(lens))]
 
 
 class HybridAStar:
@@ -229,15 +249,25 @@ class HybridAStar:
         curv = np.empty(max(cap, 1), np.float32)
         rc = L.hastar_find_path(self.h, float(vel_init), fptr(_f32(start)), fptr(xyh), fptr(curv), cap, C.byref(ln),
                                 C.byref(cost), C.byref(ok), C.byref(st))
-        if rc == HASTAR_ENOSPC:
+        if rc == HASTAR_ENOSPC and st.status == HASTAR_ENOSPC:  # our buffer was short: fetch again
             cap = ln.value
             xyh = np.empty((cap, 3), np.float32)
             curv = np.empty(cap, np.float32)
             rc = L.hastar_copy_path(self.h, fptr(xyh), fptr(curv), cap, C.byref(ln))
-        _check(rc)
+            st.status = 0
+        if rc != HASTAR_EOVERFLOW:  # an explicit pop budget ended the search: stats["status"]
+            _check(rc)
         n = ln.value
         return dict(cost=cost.value, ok=bool(ok.value), path=xyh[:n].copy(), curvature=curv[:n].copy(),
                     stats=st.as_dict())
+
+    def copy_path(self, n):
+        """The last search's path again (hastar_copy_path), into buffers of n poses."""
+        xyh = np.empty((max(n, 1), 3), np.float32)
+        curv = np.empty(max(n, 1), np.float32)
+        ln = C.c_int(0)
+        _check(load_library().hastar_copy_path(self.h, fptr(xyh), fptr(curv), n, C.byref(ln)))
+        return xyh[:ln.value].copy(), curv[:ln.value].copy()
 
     # ---- debug / unit hooks (include/hastar_test.h)
     def memo(self):
@@ -306,12 +336,17 @@ class HybridAStar:
 
 
 class BatchResult:
-    """Array view of one hastar_find_path_batch call (no per-planner Python objects)."""
+    """Array view of one hastar_find_path_batch call (no per-planner Python objects).
 
-    def __init__(self, cost, ok, lens, xyh, curv, stats, kernel_ms):
+    stats["status"][i] is planner i's own outcome: 0, HASTAR_EOVERFLOW (search ended by
+    HASTAR_MAX_POPS_HARD or by device memory) or HASTAR_ENOSPC (its path did not fit `cap`:
+    lens[i] is the length needed; result(i) fetches it with hastar_copy_path)."""
+
+    def __init__(self, cost, ok, lens, xyh, curv, stats, kernel_ms, planners=None):
         self.cost, self.ok, self.lens, self.xyh, self.curv = cost, ok, lens, xyh, curv
         self.stats = stats            # numpy structured array with the hastar_stats fields
         self.kernel_ms = kernel_ms
+        self.planners = planners
 
     def __len__(self):
         return len(self.cost)
@@ -319,6 +354,10 @@ class BatchResult:
     def result(self, i):
         k = int(self.lens[i])
         st = {name: self.stats[name][i].item() for name in self.stats.dtype.names}
+        if st["status"] == HASTAR_ENOSPC and self.planners is not None and k > self.xyh.shape[1]:
+            path, curv = self.planners[i].copy_path(k)
+            st["status"] = 0
+            return dict(cost=float(self.cost[i]), ok=bool(self.ok[i]), path=path, curvature=curv, stats=st)
         return dict(cost=float(self.cost[i]), ok=bool(self.ok[i]), path=self.xyh[i, :k].copy(),
                     curvature=self.curv[i, :k].copy(), stats=st)
 
@@ -363,9 +402,9 @@ def find_path_batch_arrays(planners, vels, starts, cap=4096, buffers=None):
     s = _f32(starts, (b.n, 3))
     rc = L.hastar_find_path_batch(b.hs, b.n, fptr(v), fptr(s), fptr(b.xyh), fptr(b.curv), b.cap, iptr(b.ln),
                                   fptr(b.cost), iptr(b.ok), b.stats)
-    if rc != HASTAR_EOVERFLOW:  # per-planner arena overflows are reported in stats["status"]
+    if rc not in (HASTAR_EOVERFLOW, HASTAR_ENOSPC):  # per-planner outcomes are in stats["status"]
         _check(rc)
-    return BatchResult(b.cost, b.ok, b.ln, b.xyh, b.curv, b.st, float(L.hastar_last_search_ms()))
+    return BatchResult(b.cost, b.ok, b.ln, b.xyh, b.curv, b.st, float(L.hastar_last_search_ms()), planners)
 
 
 def find_path_batch(planners, vels, starts, cap=4096):
@@ -383,14 +422,20 @@ def find_path_batch(planners, vels, starts, cap=4096):
     stats = (HastarStats * n)()
     rc = L.hastar_find_path_batch(hs, n, fptr(v), fptr(s), fptr(xyh), fptr(curv), cap, iptr(ln), fptr(cost),
                                   iptr(ok), stats)
-    if rc != HASTAR_EOVERFLOW:  # per-planner arena overflows are reported in stats[i]["status"]
+    if rc not in (HASTAR_EOVERFLOW, HASTAR_ENOSPC):  # per-planner outcomes are in stats[i]["status"]
         _check(rc)
+    ms = float(L.hastar_last_search_ms())
     out = []
     for i in range(n):
         k = int(ln[i])
-        out.append(dict(cost=float(cost[i]), ok=bool(ok[i]), path=xyh[i, :k].copy(), curvature=curv[i, :k].copy(),
-                        stats=stats[i].as_dict()))
-    return out, float(L.hastar_last_search_ms())
+        st = stats[i].as_dict()
+        if st["status"] == HASTAR_ENOSPC and k > cap:  # the path did not fit `cap`: fetch it
+            path, cv = planners[i].copy_path(k)
+            st["status"] = 0
+        else:
+            path, cv = xyh[i, :k].copy(), curv[i, :k].copy()
+        out.append(dict(cost=float(cost[i]), ok=bool(ok[i]), path=path, curvature=cv, stats=st))
+    return out, ms
 
 
 def gpu_math(fn, a, b=None):

@@ -178,7 +178,8 @@ def test_harness_search_parity_and_golden(gpu, oracle_lib):
     assert (g.closed_keys() == o.closed_keys()).all()
 
 
-@pytest.mark.parametrize("N,bins,K,seed", [(256, 36, 10, s) for s in (1, 2, 3, 4)] + [(512, 72, 50, 1), (512, 72, 50, 2)])
+@pytest.mark.parametrize("N,bins,K,seed", [(256, 36, 10, s) for s in (1, 2, 3, 4)] + [(512, 72, 50, 1), (512, 72, 50, 2)]
+                         + [(256, 36, 40, s) for s in (1, 2, 4)] + [(256, 72, 60, s) for s in (1, 2, 4, 5)])
 def test_synthetic_parity(gpu, oracle_lib, N, bins, K, seed):
     cfg, proto = synthetic(N, bins, K, seed)
     g, o = both(cfg, gpu, oracle_lib)

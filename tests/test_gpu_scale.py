@@ -1,0 +1,187 @@
+"""GPU vs oracle at the BASELINE.json configurations' own sizes, and the arena park/resume path.
+
+BASELINE.json configs[2..4]: cfg3 1024x1024x72 with K = 200 boxes, cfg4
+2048x2048x72 (plus its row-sharded map build), cfg5 the 1024^2 replan loop without reset.
+The query ids are bench.py's (seed = id + 1); the long ones come from the oracle's pop
+census (profiles/census_cfg*_r02.csv, tools/pop_census.py): cfg3 query 10226 (177,407 pops)
+and cfg4 query 3298 (590,557 pops), which outgrows the default 262,144-pop arena and must
+finish through a park + resume, as the reference (no limit, HybridAStar.cpp:107) does.
+
+The bar is the one of test_gpu_parity.py: bit-identical pops, successors, A* pops, shots,
+ordered pop digest, closed-set digest, path, curvature and cost.
+"""
+import numpy as np
+import pytest
+
+from tests.scenarios import drive, replan_pairs, replan_tick, replan_tick_inputs, synthetic
+from tests.test_gpu_parity import assert_bits_equal, compare_results
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    from path_planning_pkg_amd import planner
+    planner.load_library()
+    return planner
+
+
+def _pair(gpu, oracle_lib, cfg, proto):
+    g, o = gpu.HybridAStar(cfg), oracle_lib.OraclePlanner(cfg)
+    drive(g, proto)
+    drive(o, proto)
+    return g, o
+
+
+# ----------------------------------------------------------------- park / resume ------
+@pytest.mark.parametrize("N,bins,K,seed", [(256, 36, 40, 1), (256, 36, 40, 2), (256, 36, 40, 4), (512, 72, 50, 1)])
+def test_park_resume_tiny_arena(gpu, oracle_lib, N, bins, K, seed):
+    """An initial arena of 64 pops: the search parks at every 4x boundary (64, 256, 1024,
+    ...) and resumes in a larger arena; the result must be the oracle's, bit for bit."""
+    cfg, proto = synthetic(N, bins, K, seed)
+    cfg.values["max_pops"] = 64
+    g, o = _pair(gpu, oracle_lib, cfg, proto)
+    rg = g.find_path(proto["vel"], proto["start"])
+    ro = o.find_path(proto["vel"], proto["start"])
+    compare_results(rg, ro, f"tiny arena N{N} seed{seed}")
+    assert rg["stats"]["parks"] >= 1, "the 64-pop arena should have been outgrown"
+    fg, vg = g.memo()
+    fo, vo = o.get_memo()
+    assert_bits_equal(fg, fo, "memo f")
+    assert (vg == vo).all()
+
+
+def test_park_resume_with_fewer_slots(gpu, oracle_lib, monkeypatch):
+    """Two slots, seven planners with 64-pop arenas: every wave parks its search and stops
+    taking work, the host re-queues the planners no wave took, moves the parked ones into
+    larger arenas and resumes them — until all are done.  Every result is the oracle's."""
+    monkeypatch.setenv("HASTAR_SLOTS", "2")
+    cases = [synthetic(128, 36, 6, s) for s in (31, 32, 33, 34, 35, 36, 37)]
+    gs, os_ = [], []
+    for cfg, proto in cases:
+        cfg.values["max_pops"] = 64
+        g, o = _pair(gpu, oracle_lib, cfg, proto)
+        gs.append(g)
+        os_.append(o)
+    res, _ = gpu.find_path_batch(gs, [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases])
+    for i, ((cfg, proto), o) in enumerate(zip(cases, os_)):
+        compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"2 slots, planner {i}")
+    assert sum(r["stats"]["parks"] for r in res) > 0
+
+
+def test_statuses_reported_per_planner(gpu, oracle_lib, monkeypatch):
+    """One batch, two outcomes: planner 0 exceeds an explicit pop budget
+    (HASTAR_MAX_POPS_HARD -> HASTAR_EOVERFLOW, a failed search), planner 1 finishes with a
+    path longer than the caller's cap (HASTAR_ENOSPC: its length is reported and the path is
+    fetched with hastar_copy_path).  Neither hides the other."""
+    monkeypatch.setenv("HASTAR_MAX_POPS_HARD", "400")
+    (cfg_a, pa), (cfg_b, pb) = synthetic(256, 36, 40, 1), synthetic(256, 36, 10, 1)  # 2947 and 307 pops
+    ga, oa = _pair(gpu, oracle_lib, cfg_a, pa)
+    gb, ob = _pair(gpu, oracle_lib, cfg_b, pb)
+    br = gpu.find_path_batch_arrays([ga, gb], [pa["vel"], pb["vel"]], [pa["start"], pb["start"]], cap=8)
+    assert int(br.stats["status"][0]) == gpu.HASTAR_EOVERFLOW and not br.ok[0]
+    assert int(br.stats["pops"][0]) == 400
+    assert int(br.stats["status"][1]) == gpu.HASTAR_ENOSPC and br.ok[1] and br.lens[1] > 8
+    oracle_lib.set_max_pops(400)
+    try:
+        ro_a = oa.find_path(pa["vel"], pa["start"])
+    finally:
+        oracle_lib.set_max_pops(0)
+    assert not ro_a["ok"] and ro_a["stats"]["pops"] == 400
+    assert br.stats["pop_digest"][0] == ro_a["stats"]["pop_digest"]
+    compare_results(br.result(1), ob.find_path(pb["vel"], pb["start"]), "short cap planner")
+
+
+# ------------------------------------------------------------------ cfg3 (1024^2) ------
+def test_cfg3_parity_batch(gpu, oracle_lib):
+    """BASELINE configs[2]: 1024x1024x72, K = 200, bench query ids 0, 1, 2 and the longest
+    query of the bench batch (10226, 177,407 pops), searched in one batched launch."""
+    qs = [0, 1, 2, 10226]
+    cases = [synthetic(1024, 72, 200, seed=q + 1) for q in qs]
+    gs, os_ = [], []
+    for cfg, proto in cases:
+        g, o = _pair(gpu, oracle_lib, cfg, proto)
+        gs.append(g)
+        os_.append(o)
+    res, _ = gpu.find_path_batch(gs, [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases], cap=8192)
+    for q, r, o, (cfg, proto), g in zip(qs, res, os_, cases, gs):
+        ro = o.find_path(proto["vel"], proto["start"])
+        compare_results(r, ro, f"cfg3 query {q}")
+        fg, vg = g.memo()
+        fo, vo = o.get_memo()
+        assert_bits_equal(fg, fo, f"cfg3 query {q} memo f")
+        assert (vg == vo).all()
+    assert max(r["stats"]["pops"] for r in res) > 100000  # the long query is in the batch
+
+
+# ------------------------------------------------------------------ cfg4 (2048^2) ------
+@pytest.mark.parametrize("q", [0, 3, 3298])
+def test_cfg4_parity(gpu, oracle_lib, q):
+    """BASELINE configs[3] at its own size: 2048x2048x72, K = 200.  Query 3298 needs 590,557
+    pops (census): it parks at the default arena's 262,144 and resumes, and must end with
+    the oracle's success, cost and path (round 1 reported it as an overflow failure)."""
+    cfg, proto = synthetic(2048, 72, 200, seed=q + 1)
+    g, o = _pair(gpu, oracle_lib, cfg, proto)
+    assert_bits_equal(g.get_obstacles(), o.get_obstacles(), f"cfg4 query {q} map")
+    rg = g.find_path(proto["vel"], proto["start"], cap=16384)
+    ro = o.find_path(proto["vel"], proto["start"])
+    compare_results(rg, ro, f"cfg4 query {q}")
+    if ro["stats"]["pops"] > 262144:
+        assert rg["stats"]["parks"] >= 1
+
+
+def test_cfg4_row_sharded_map_build(gpu, oracle_lib):
+    """cfg4's sharded map build at its own size: 2048^2 over 4 stand-in ranks."""
+    from tests import test_gpu_parity as tp  # (a module import: pytest must not collect it here)
+    tp.test_row_sharded_map_build(gpu, oracle_lib, 2048, 4)
+
+
+# ------------------------------------------------------------------ cfg5 (replans) -----
+def test_cfg5_replan_loop_parity(gpu, oracle_lib):
+    """BASELINE configs[4] at its own size: 1024x1024x72 maps, K = 200 moving boxes, bench
+    pair ids 0..7 (bench.py run_cfg5), 3 batched ticks WITHOUT reset (local_planner.cpp:
+    204-205, 241, 316): memo and stale node-map values carry over between ticks."""
+    pairs = []
+    for q in range(8):
+        pairs += replan_pairs(1024, 72, 200, 1, seed=1000 + q)
+    gs, os_ = [], []
+    for cfg, proto, _ in pairs:
+        g, o = _pair(gpu, oracle_lib, cfg, proto)
+        gs.append(g)
+        os_.append(o)
+    bufs = gpu.BatchBuffers(gs, cap=8192)
+    for tick in range(3):
+        starts = [replan_tick_inputs(proto, v, tick)[0] for _, proto, v in pairs]
+        br = gpu.find_path_batch_arrays(gs, [proto["vel"] for _, proto, _ in pairs], starts, buffers=bufs)
+        for i, (o, (_, proto, v)) in enumerate(zip(os_, pairs)):
+            compare_results(br.result(i), o.find_path(proto["vel"], starts[i]), f"cfg5 tick {tick} pair {i}")
+            replan_tick(gs[i], proto, v, tick)
+            replan_tick(o, proto, v, tick)
+
+
+# ------------------------------------------------- device-resident velocity profile ----
+def test_velocity_profile_of_last_batch(gpu, oracle_lib):
+    """hastar_velocity_profile_last_batch profiles the batch's paths where they are (HBM);
+    it must equal the host-buffer entry point and the oracle, bit for bit."""
+    cases = [synthetic(256, 36, 10, s) for s in (1, 2, 3, 4, 5)]
+    gs = []
+    for cfg, proto in cases:
+        g = gpu.HybridAStar(cfg)
+        drive(g, proto)
+        gs.append(g)
+    br = gpu.find_path_batch_arrays(gs, [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases], cap=4096)
+    lens = br.lens.astype(np.int64).copy()
+    prm = (10.0, 3.0, 2.5, 1.5, 3.0)
+    vg = gpu.VelocityGenerator(*prm)
+    v0 = np.full(len(gs), 2.0, np.float32)
+    vm = np.full(len(gs), 10.0, np.float32)
+    flags = np.array([2, 0, 1, 3, 2], np.uint8)
+    feas, vel = vg.profile_last_batch(lens, v0, vm, flags)
+    off = np.zeros(len(gs) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    for i in range(len(gs)):
+        a, b = off[i], off[i + 1]
+        ok_o, vo = oracle_lib.velocity_profile(prm, 2.0, 10.0, br.xyh[i, :lens[i]], br.curv[i, :lens[i]],
+                                               bool(flags[i] & 1), bool(flags[i] & 2))
+        assert bool(feas[i]) == ok_o
+        assert_bits_equal(vel[a:b], vo, f"velocity of path {i}")
