@@ -108,6 +108,20 @@ int hastar_update_lines(hastar_handle h, const float* lines, const float* confid
 /* update_obstacles() (HybridAStar.cpp:43-46): free-space decay of every cell. */
 int hastar_decay(hastar_handle h);
 
+/* ---- batched map updates: the calls above for n planners of ONE device at once (the
+ * reference updates one instance at a time, Grid2D.cpp:99-208, Grid3D.cpp:22-44, 102-203;
+ * a batch equals n single calls in planner order, bit for bit).  One staged upload and a
+ * few launches serve the whole batch, instead of ~12 C calls with their pageable copies and
+ * launches per planner. ---- */
+/* update_goal of planner i with goals[3i..3i+2], starts[3i..3i+2]. */
+int hastar_update_goal_batch(const hastar_handle* hs, int n, const float* goals, const float* starts);
+/* update_obstacles() of every planner. */
+int hastar_decay_batch(const hastar_handle* hs, int n);
+/* update_obstacles(boxes, confidence, apf_added_radius): planner i takes counts[i] boxes
+ * (4 floats each) and confidences, packed after planner i-1's. */
+int hastar_update_boxes_batch(const hastar_handle* hs, int n, const float* boxes, const float* confidence,
+                              const int* counts, float apf_added_radius);
+
 /* find_path(vel_init, start, path, curvature) (HybridAStar.cpp:68-88).
  * xyh receives len x {x, y, heading} in the order the reference appends them
  * (goal first, start last; HybridAStar.cpp:208-262), curv receives len curvatures.

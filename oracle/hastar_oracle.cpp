@@ -1020,9 +1020,11 @@ extern "C" void orc_set_max_pops(long long n) { orc::g_max_pops = n; }
 // says), and running `replans` x (reset + find_path) on it, timed around find_path only
 // (test_hybrid_astar.cpp:123-126).  out[0] = total pops, out[1] = wall seconds of the
 // parallel region, out[2] = sum of find_path seconds (for the mean plan latency), out[3] =
-// plans; per_plan_ms (n x replans, may be null) receives each plan's latency.
+// plans; per_plan_ms (n x replans, may be null) receives each plan's latency; last_digest /
+// last_cost / last_ok (n, may be null) the last replan's pop digest and result.
 extern "C" void orc_run_batch_threads(void* const* hs, int n, const float* vel, const float* starts, int replans,
-                                      int threads, double* out, double* per_plan_ms) {
+                                      int threads, double* out, double* per_plan_ms, unsigned long long* last_digest,
+                                      float* last_cost, int* last_ok) {
   std::atomic<int> next{0};
   std::atomic<long long> pops{0};
   std::vector<double> tsum((size_t)std::max(threads, 1), 0.0);
@@ -1034,11 +1036,16 @@ extern "C" void orc_run_batch_threads(void* const* hs, int n, const float* vel, 
         std::vector<orc::P3<float>> path;
         std::vector<float> cv;
         const auto t0 = std::chrono::steady_clock::now();
-        P->find_path(vel[i], {starts[3 * i], starts[3 * i + 1], starts[3 * i + 2]}, path, cv);
+        const auto res = P->find_path(vel[i], {starts[3 * i], starts[3 * i + 1], starts[3 * i + 2]}, path, cv);
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         tsum[t] += s;
         if (per_plan_ms) per_plan_ms[(size_t)i * replans + r] = s * 1e3;
         pops += P->st.pops;
+        if (r == replans - 1) {
+          if (last_digest) last_digest[i] = P->st.pop_digest;
+          if (last_cost) last_cost[i] = res.first;
+          if (last_ok) last_ok[i] = res.second ? 1 : 0;
+        }
       }
     }
   };

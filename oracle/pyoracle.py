@@ -55,7 +55,8 @@ def lib():
         L.orc_libm.argtypes = [C.c_int, fp, fp, fp, C.c_int]
         L.orc_velocity_profile.argtypes = [fp, C.c_float, C.c_float, fp, fp, C.c_int, C.c_int, C.c_int, fp]
         L.orc_set_max_pops.argtypes = [C.c_longlong]
-        L.orc_run_batch_threads.argtypes = [C.POINTER(C.c_void_p), C.c_int, fp, fp, C.c_int, C.c_int, dp, dp]
+        L.orc_run_batch_threads.argtypes = [C.POINTER(C.c_void_p), C.c_int, fp, fp, C.c_int, C.c_int, dp, dp,
+                                            C.POINTER(C.c_ulonglong), fp, ip]
         _lib = L
     return _lib
 
@@ -211,17 +212,23 @@ def set_max_pops(n):
 
 def run_batch_threads(planners, vels, starts, replans, threads):
     """replans x (reset + find_path) of every planner on `threads` C++ threads (one planner
-    per thread at a time).  Returns dict(pops, wall_s, plan_s_sum, plans, plan_ms[n, replans])."""
+    per thread at a time).  Returns dict(pops, wall_s, plan_s_sum, plans, plan_ms[n, replans],
+    digest / cost / ok of each planner's last replan)."""
     n = len(planners)
     hs = (C.c_void_p * n)(*[p.h for p in planners])
     v = _f32(vels)
     s = _f32(starts, (n, 3))
     out = np.zeros(4, np.float64)
     per = np.zeros((n, replans), np.float64)
+    dig = np.zeros(n, np.uint64)
+    cost = np.zeros(n, np.float32)
+    ok = np.zeros(n, np.int32)
     dp = C.POINTER(C.c_double)
     lib().orc_run_batch_threads(hs, n, fptr(v), fptr(s), int(replans), int(threads), out.ctypes.data_as(dp),
-                                per.ctypes.data_as(dp))
-    return dict(pops=int(out[0]), wall_s=float(out[1]), plan_s_sum=float(out[2]), plans=int(out[3]), plan_ms=per)
+                                per.ctypes.data_as(dp), dig.ctypes.data_as(C.POINTER(C.c_ulonglong)), fptr(cost),
+                                iptr(ok))
+    return dict(pops=int(out[0]), wall_s=float(out[1]), plan_s_sum=float(out[2]), plans=int(out[3]), plan_ms=per,
+                digest=dig, cost=cost, ok=ok.astype(bool))
 
 
 def velocity_profile(params, vel_init, max_velocity_curr, xyh, curv, coast_to_goal, stop_at_goal=False):

@@ -189,6 +189,10 @@ struct DeviceCtx {
   size_t pts_cap = 0;
   uint32_t** d_ptrs = nullptr;  // bitmap pointers of a batched reset
   size_t ptrs_cap = 0;
+  char* stage = nullptr;          // batched map updates: staged items / lists (grown, reused)
+  size_t stage_cap = 0;
+  char* bscratch = nullptr;       // batched relocation: bs_maps tmp maps, then bs_maps winner maps (-1)
+  size_t bs_maps = 0, bs_nn = 0;  // capacity: maps x cells per map
   int last_n = 0;                 // the last batch's packed paths (d_pxyh/d_pcurv, offsets d_off)
   long long last_total = 0;
   char* vel_slab = nullptr;       // velocity-profile staging (grown, reused)
@@ -247,6 +251,41 @@ int vel_slab_acquire(DeviceCtx& D, size_t bytes) {
     return fail(HASTAR_ENOMEM, "velocity_profile: hipMalloc failed");
   }
   D.vel_cap = want;
+  return 0;
+}
+
+// device staging for the batched map updates (stream-ordered reuse; growth waits for the
+// stream so no queued kernel still reads the old buffer)
+int stage_acquire(DeviceCtx& D, size_t bytes) {
+  if (D.stage_cap >= bytes) return 0;
+  HIPCHK(hipStreamSynchronize(D.stream));
+  if (D.stage) hipFree(D.stage);
+  D.stage = nullptr;
+  D.stage_cap = 0;
+  const size_t want = bytes + bytes / 2 + 4096;
+  if (hipMalloc(reinterpret_cast<void**>(&D.stage), want) != hipSuccess) {
+    D.stage = nullptr;
+    return fail(HASTAR_ENOMEM, "batched map update: staging hipMalloc failed");
+  }
+  D.stage_cap = want;
+  return 0;
+}
+// relocation scratch for `maps` maps of up to NN cells: bs_maps tmp maps (floats) followed
+// by bs_maps winner maps (ints), each bs_nn cells; the winner maps start (and stay) at -1
+int bscratch_acquire(DeviceCtx& D, size_t maps, size_t NN) {
+  if (D.bs_maps >= maps && D.bs_nn >= NN) return 0;
+  HIPCHK(hipStreamSynchronize(D.stream));
+  if (D.bscratch) hipFree(D.bscratch);
+  D.bscratch = nullptr;
+  D.bs_maps = D.bs_nn = 0;
+  const size_t bytes = maps * NN * 8;
+  if (hipMalloc(reinterpret_cast<void**>(&D.bscratch), bytes) != hipSuccess) {
+    D.bscratch = nullptr;
+    return fail(HASTAR_ENOMEM, "batched relocation: scratch hipMalloc failed");
+  }
+  HIPCHK(hipMemsetAsync(D.bscratch + maps * NN * 4, 0xff, maps * NN * 4, D.stream));
+  D.bs_maps = maps;
+  D.bs_nn = NN;
   return 0;
 }
 
@@ -609,10 +648,31 @@ int hastar_destroy(hastar_handle h) {
 
 // HybridAStar::update_goal -> Grid3D::update_goal_heading + relocate_obstacles
 // (Grid3D.cpp:102-124, 169-203); AStar::update_goal_node takes the goal cell.
+struct RelocPrep {
+  float c, s, ox, oy;
+};
+// Host half of update_goal: the new grid frame, the goal node, and the rotation + origin of
+// the map relocation (Grid3D.cpp:102-124, 169-203), with the reference's float arithmetic.
+static RelocPrep goal_prep(hastar_handle h, const float goal[3], const float start[3]);
+static int update_boxes_legacy(hastar_handle h, const float* boxes, const float* conf, int n, float apf_added_radius);
+static int update_boxes_impl(const hastar_handle* hs, int n, const float* boxes, const float* conf, const int* counts,
+                             float apf_added_radius);
+
 int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3]) {
   if (!h || !goal || !start) return fail(HASTAR_EINVAL, "null argument");
   HIPCHK(hipSetDevice(h->device));
   DeviceCtx& DC = *h->dc;
+  PlannerDev& D = h->desc;
+  const RelocPrep rp = goal_prep(h, goal, start);
+  std::lock_guard<std::mutex> lk(DC.mu);
+  const size_t NN = (size_t)D.N * D.N;
+  if (int rc = scratch_acquire(DC, NN)) return rc;
+  HIPCHK(launch_relocate(D.N, rp.c, rp.s, rp.ox, rp.oy, D.occ, DC.tmp, DC.winner, DC.stream));
+  HIPCHK(hipMemcpyAsync(D.occ, DC.tmp, NN * sizeof(float), hipMemcpyDeviceToDevice, DC.stream));
+  return HASTAR_OK;
+}
+
+static RelocPrep goal_prep(hastar_handle h, const float goal[3], const float start[3]) {
   PlannerDev& D = h->desc;
   const float gh_prev = h->grid_heading;
   const float g3px = h->goal3x, g3py = h->goal3y;
@@ -628,13 +688,7 @@ int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3
   const V2 gno = rot2(g3px - h->goal3x, g3py - h->goal3y, gh);
   V2 org{(float)D.n45 + gno.x / D.res, (float)D.n2 + gno.y / D.res};
   org = {org.x - gp.x, org.y - gp.y};
-  {
-    std::lock_guard<std::mutex> lk(DC.mu);
-    const size_t NN = (size_t)D.N * D.N;
-    if (int rc = scratch_acquire(DC, NN)) return rc;
-    HIPCHK(launch_relocate(D.N, g_cosf(dh), g_sinf(dh), org.x, org.y, D.occ, DC.tmp, DC.winner, DC.stream));
-    HIPCHK(hipMemcpyAsync(D.occ, DC.tmp, NN * sizeof(float), hipMemcpyDeviceToDevice, DC.stream));
-  }
+  const RelocPrep out{g_cosf(dh), g_sinf(dh), org.x, org.y};
   // the goal node (Grid3D.cpp:115-123)
   D.goal_x = D.n45 * D.res;
   D.goal_y = D.n2 * D.res;
@@ -648,7 +702,7 @@ int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3
   D.rot_c = g_cosf(-gh);
   D.rot_s = g_sinf(-gh);
   h->goal_set = true;
-  return HASTAR_OK;
+  return out;
 }
 
 // HybridAStar::reset -> AStar::reset (AStar.cpp:56-60)
@@ -695,6 +749,260 @@ int hastar_reset_batch(const hastar_handle* hs, int n) {
   return HASTAR_OK;
 }
 
+// Host half of Grid3D::update_obstacles(boxes) for one planner: the APF list in the grid
+// frame (Grid3D.cpp:22-44), each box's sub-sample origin and counts and log-odds delta
+// (Grid2D.cpp:99-139), and its raster footprint and layer.  Layers: box k goes one layer
+// above every earlier box whose footprint it may share, so boxes within a layer touch
+// disjoint cells (applied concurrently) and overlapping boxes are applied in the
+// reference's order.  Footprint: the rotated sub-sample rectangle's bounds plus a 2-cell
+// margin for rounding.
+struct BoxPrep {
+  std::vector<float> apf, dl;
+  std::vector<int> rp, bb, layer;
+  int n_layers = 0;
+  bool big = false;  // some footprint exceeds RASTER_HIST cells
+};
+static void boxes_prep(hastar_handle h, const float* boxes, const float* conf, int n, float apf_added_radius,
+                       BoxPrep& P) {
+  const PlannerDev& D = h->desc;
+  const float gh = h->grid_heading;
+  P.apf.resize((size_t)n * 3);
+  P.rp.resize((size_t)n * 4);
+  P.dl.resize((size_t)n);
+  P.bb.resize((size_t)n * 4);
+  P.layer.assign((size_t)n, 0);
+  P.n_layers = 0;
+  P.big = false;
+  const float cg = g_cosf(gh), sg = g_sinf(gh);
+  for (int k = 0; k < n; ++k) {
+    const float ox = boxes[4 * k], oy = boxes[4 * k + 1], dx = boxes[4 * k + 2], dy = boxes[4 * k + 3];
+    V2 pp = rot2(ox - h->goal3x, oy - h->goal3y, gh);
+    pp.x += D.n45 * D.res;
+    pp.y += D.n2 * D.res;
+    P.apf[3 * k] = pp.x;
+    P.apf[3 * k + 1] = pp.y;
+    P.apf[3 * k + 2] = std::max(dx, dy) / 2 + apf_added_radius;
+    const V2 bl = rot2((ox - dx / 2) - h->goal2x, (oy - dy / 2) - h->goal2y, gh);
+    int* rp = &P.rp[4 * k];
+    rp[0] = gmath::x86_trunc_int(std::round(bl.x / D.res) + (float)D.n45);
+    rp[1] = gmath::x86_trunc_int(std::round(bl.y / D.res) + (float)D.n2);
+    rp[2] = std::max(0, 2 * gmath::x86_trunc_int(std::ceil(dx / D.res)));
+    rp[3] = std::max(0, 2 * gmath::x86_trunc_int(std::ceil(dy / D.res)));
+    const float lc = (float)std::log((double)conf[k] / (1.0 - (double)conf[k]));
+    P.dl[k] = lc - h->lp_free;
+    const float X = (rp[2] - 1) * 0.5f, Y = (rp[3] - 1) * 0.5f;
+    const float xs[4] = {0.0f, X * cg, Y * sg, X * cg + Y * sg};
+    const float ys[4] = {0.0f, -X * sg, Y * cg, -X * sg + Y * cg};
+    int* bb = &P.bb[4 * k];
+    bb[0] = rp[0] + (int)std::floor(*std::min_element(xs, xs + 4)) - 2;
+    bb[1] = rp[0] + (int)std::ceil(*std::max_element(xs, xs + 4)) + 2;
+    bb[2] = rp[1] + (int)std::floor(*std::min_element(ys, ys + 4)) - 2;
+    bb[3] = rp[1] + (int)std::ceil(*std::max_element(ys, ys + 4)) + 2;
+    if ((long long)(bb[1] - bb[0] + 1) * (bb[3] - bb[2] + 1) > RASTER_HIST) P.big = true;
+    int l = 0;
+    for (int j = 0; j < k; ++j) {
+      const int* b2 = &P.bb[4 * j];
+      if (P.layer[j] >= l && b2[0] <= bb[1] && bb[0] <= b2[1] && b2[2] <= bb[3] && bb[2] <= b2[3]) l = P.layer[j] + 1;
+    }
+    P.layer[k] = l;
+    P.n_layers = std::max(P.n_layers, l + 1);
+  }
+}
+
+// update_obstacles(boxes) of n planners of one device (planner i's counts[i] boxes follow
+// planner i-1's in `boxes` / `conf`): one staged upload, one copy launch for the APF lists,
+// and one raster launch per layer index over every planner's boxes of that layer.
+static int update_boxes_impl(const hastar_handle* hs, int n, const float* boxes, const float* conf, const int* counts,
+                             float apf_added_radius) {
+  if (n <= 0) return HASTAR_OK;
+  const int dev = hs[0]->device;
+  for (int i = 0; i < n; ++i) {
+    if (!hs[i] || hs[i]->device != dev) return fail(HASTAR_EINVAL, "null handle or handles on different devices");
+    if (counts[i] < 0) return fail(HASTAR_EINVAL, "negative box count");
+  }
+  HIPCHK(hipSetDevice(dev));
+  DeviceCtx& DC = *hs[0]->dc;
+  std::vector<BoxPrep> prep(n);
+  std::vector<long long> first(n + 1, 0);
+  for (int i = 0; i < n; ++i) first[i + 1] = first[i] + counts[i];
+  int max_layers = 0;
+  for (int i = 0; i < n; ++i) {
+    const long long o = first[i];
+    boxes_prep(hs[i], boxes + 4 * o, conf + o, counts[i], apf_added_radius, prep[i]);
+    if (!prep[i].big) max_layers = std::max(max_layers, prep[i].n_layers);
+  }
+  // planners with an oversized box footprint take the per-planner kernel
+  for (int i = 0; i < n; ++i)
+    if (prep[i].big)
+      if (int rc = update_boxes_legacy(hs[i], boxes + 4 * first[i], conf + first[i], counts[i], apf_added_radius)) return rc;
+  std::lock_guard<std::mutex> lk(DC.mu);
+  // APF buffers of the planners (grown on demand; growth waits for queued readers)
+  bool grow = false;
+  for (int i = 0; i < n; ++i) grow |= !prep[i].big && counts[i] > hs[i]->apf_cap;
+  if (grow) {
+    HIPCHK(hipStreamSynchronize(DC.stream));
+    for (int i = 0; i < n; ++i) {
+      hastar_handle h = hs[i];
+      if (prep[i].big || counts[i] <= h->apf_cap) continue;
+      side_free(DC, h->desc.apf, (size_t)h->apf_cap * 3);
+      h->desc.apf = nullptr;
+      h->apf_cap = 0;
+      HIPCHK(side_alloc(DC, &h->desc.apf, (size_t)counts[i] * 3));
+      h->apf_cap = counts[i];
+    }
+  }
+  // staged arrays: maps, boxes by layer, APF copy items, APF floats
+  std::vector<RasterMap> maps;
+  std::vector<CopyItem> copies;
+  std::vector<float> apf;
+  std::vector<std::vector<RasterBox>> by_layer(max_layers);
+  for (int i = 0; i < n; ++i) {
+    if (prep[i].big) continue;
+    hastar_handle h = hs[i];
+    const BoxPrep& P = prep[i];
+    h->desc.n_apf = counts[i];
+    if (counts[i] == 0) continue;
+    CopyItem ci{h->desc.apf, (long long)apf.size(), counts[i] * 3, 0};
+    copies.push_back(ci);
+    apf.insert(apf.end(), P.apf.begin(), P.apf.end());
+    const int mi = (int)maps.size();
+    RasterMap m;
+    m.occ = h->desc.occ;
+    m.N = h->desc.N;
+    m.r0 = h->row0;
+    m.r1 = h->row1;
+    m.c = g_cosf(h->grid_heading);
+    m.s = g_sinf(h->grid_heading);
+    m.lp_min = h->lp_min;
+    m.lp_max = h->lp_max;
+    m.pad = 0;
+    maps.push_back(m);
+    for (int k = 0; k < counts[i]; ++k) {
+      const int* rp = &P.rp[4 * k];
+      const int* bb = &P.bb[4 * k];
+      if (rp[2] == 0 || rp[3] == 0) continue;  // no sub-samples
+      RasterBox b;
+      b.map = mi;
+      b.si = rp[0];
+      b.sj = rp[1];
+      b.ni = rp[2];
+      b.nj = rp[3];
+      b.d = P.dl[k];
+      b.bi0 = bb[0];
+      b.bj0 = bb[2];
+      b.bw = bb[1] - bb[0] + 1;
+      b.bh = bb[3] - bb[2] + 1;
+      b.pad0 = b.pad1 = 0;
+      by_layer[P.layer[k]].push_back(b);
+    }
+  }
+  size_t nbox = 0;
+  for (auto& v : by_layer) nbox += v.size();
+  const size_t b_maps = align256(maps.size() * sizeof(RasterMap)), b_boxes = align256(nbox * sizeof(RasterBox));
+  const size_t b_copy = align256(copies.size() * sizeof(CopyItem)), b_apf = align256(apf.size() * sizeof(float));
+  const size_t total = b_maps + b_boxes + b_copy + b_apf;
+  if (total == 0) return HASTAR_OK;
+  if (int rc = stage_acquire(DC, total)) return rc;
+  std::vector<char> host(total);
+  char* q = host.data();
+  std::memcpy(q, maps.data(), maps.size() * sizeof(RasterMap));
+  std::vector<size_t> layer_off(max_layers + 1, 0);
+  {
+    char* bq = q + b_maps;
+    size_t o = 0;
+    for (int l = 0; l < max_layers; ++l) {
+      layer_off[l] = o;
+      std::memcpy(bq + o * sizeof(RasterBox), by_layer[l].data(), by_layer[l].size() * sizeof(RasterBox));
+      o += by_layer[l].size();
+    }
+    layer_off[max_layers] = o;
+  }
+  std::memcpy(q + b_maps + b_boxes, copies.data(), copies.size() * sizeof(CopyItem));
+  std::memcpy(q + b_maps + b_boxes + b_copy, apf.data(), apf.size() * sizeof(float));
+  hipStream_t st = DC.stream;
+  HIPCHK(hipMemcpyAsync(DC.stage, host.data(), total, hipMemcpyHostToDevice, st));
+  const RasterMap* d_maps = reinterpret_cast<const RasterMap*>(DC.stage);
+  const RasterBox* d_boxes = reinterpret_cast<const RasterBox*>(DC.stage + b_maps);
+  HIPCHK(launch_copy_batch(reinterpret_cast<const CopyItem*>(DC.stage + b_maps + b_boxes), (int)copies.size(),
+                           reinterpret_cast<const float*>(DC.stage + b_maps + b_boxes + b_copy), st));
+  for (int l = 0; l < max_layers; ++l)
+    HIPCHK(launch_raster_boxes_batch(d_maps, d_boxes + layer_off[l], (int)(layer_off[l + 1] - layer_off[l]), st));
+  return HASTAR_OK;
+}
+
+extern "C" {
+
+// update_obstacles(boxes, confidence, apf_added_radius) of n planners of one device.
+int hastar_update_boxes_batch(const hastar_handle* hs, int n, const float* boxes, const float* conf, const int* counts,
+                              float apf_added_radius) {
+  if (!hs || n < 0 || (n > 0 && !counts)) return fail(HASTAR_EINVAL, "bad argument");
+  long long tot = 0;
+  for (int i = 0; i < n; ++i) tot += counts[i] > 0 ? counts[i] : 0;
+  if (tot > 0 && (!boxes || !conf)) return fail(HASTAR_EINVAL, "bad argument");
+  return update_boxes_impl(hs, n, boxes, conf, counts, apf_added_radius);
+}
+
+// update_obstacles() (Grid2D.cpp:197-208) of n planners of one device: one launch.
+int hastar_decay_batch(const hastar_handle* hs, int n) {
+  if (!hs || n < 0) return fail(HASTAR_EINVAL, "bad argument");
+  if (n == 0) return HASTAR_OK;
+  const int dev = hs[0] ? hs[0]->device : -1;
+  std::vector<DecayItem> items(n);
+  size_t max_cells = 0;
+  for (int i = 0; i < n; ++i) {
+    hastar_handle h = hs[i];
+    if (!h || h->device != dev) return fail(HASTAR_EINVAL, "null handle or handles on different devices");
+    const size_t N = (size_t)h->desc.N;
+    items[i] = DecayItem{h->desc.occ + (size_t)h->row0 * N, (long long)((size_t)(h->row1 - h->row0) * N), h->lp_free,
+                         h->lp_min, h->lp_max, 0.0f};
+    max_cells = std::max(max_cells, (size_t)items[i].cells);
+  }
+  HIPCHK(hipSetDevice(dev));
+  DeviceCtx& DC = *hs[0]->dc;
+  std::lock_guard<std::mutex> lk(DC.mu);
+  if (int rc = stage_acquire(DC, (size_t)n * sizeof(DecayItem))) return rc;
+  HIPCHK(hipMemcpyAsync(DC.stage, items.data(), (size_t)n * sizeof(DecayItem), hipMemcpyHostToDevice, DC.stream));
+  HIPCHK(launch_decay_batch(reinterpret_cast<const DecayItem*>(DC.stage), n, max_cells, DC.stream));
+  return HASTAR_OK;
+}
+
+// update_goal(goal, start) of n planners of one device (goals / starts: n x 3): the map
+// relocations run in chunks of maps that share one scratch allocation (<= 1 GiB).
+int hastar_update_goal_batch(const hastar_handle* hs, int n, const float* goals, const float* starts) {
+  if (!hs || n < 0 || (n > 0 && (!goals || !starts))) return fail(HASTAR_EINVAL, "bad argument");
+  if (n == 0) return HASTAR_OK;
+  const int dev = hs[0] ? hs[0]->device : -1;
+  size_t NNmax = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!hs[i] || hs[i]->device != dev) return fail(HASTAR_EINVAL, "null handle or handles on different devices");
+    NNmax = std::max(NNmax, (size_t)hs[i]->desc.N * hs[i]->desc.N);
+  }
+  HIPCHK(hipSetDevice(dev));
+  DeviceCtx& DC = *hs[0]->dc;
+  std::vector<RelocItem> items(n);
+  for (int i = 0; i < n; ++i) {
+    const RelocPrep rp = goal_prep(hs[i], goals + 3 * i, starts + 3 * i);
+    items[i] = RelocItem{hs[i]->desc.occ, nullptr, nullptr, hs[i]->desc.N, rp.c, rp.s, rp.ox, rp.oy, 0};
+  }
+  std::lock_guard<std::mutex> lk(DC.mu);
+  const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, ((size_t)1 << 30) / (8 * NNmax)));
+  if (int rc = bscratch_acquire(DC, (size_t)chunk, NNmax)) return rc;
+  float* tmp0 = reinterpret_cast<float*>(DC.bscratch);
+  int* win0 = reinterpret_cast<int*>(DC.bscratch + DC.bs_maps * DC.bs_nn * 4);
+  if (int rc = stage_acquire(DC, (size_t)n * sizeof(RelocItem))) return rc;
+  for (int i = 0; i < n; ++i) {
+    items[i].tmp = tmp0 + (size_t)(i % chunk) * DC.bs_nn;
+    items[i].winner = win0 + (size_t)(i % chunk) * DC.bs_nn;
+  }
+  HIPCHK(hipMemcpyAsync(DC.stage, items.data(), (size_t)n * sizeof(RelocItem), hipMemcpyHostToDevice, DC.stream));
+  const RelocItem* d_items = reinterpret_cast<const RelocItem*>(DC.stage);
+  for (int c0 = 0; c0 < n; c0 += chunk)
+    HIPCHK(launch_relocate_batch(d_items + c0, std::min(chunk, n - c0), NNmax, DC.stream));
+  return HASTAR_OK;
+}
+
+}  // extern "C"
+
 // Grid2D::update_obstacles() (Grid2D.cpp:197-208)
 int hastar_decay(hastar_handle h) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");
@@ -705,9 +1013,16 @@ int hastar_decay(hastar_handle h) {
   return HASTAR_OK;
 }
 
-// Grid3D::update_obstacles(boxes) (Grid3D.cpp:22-44) + Grid2D boxes (Grid2D.cpp:99-139)
+// Grid3D::update_obstacles(boxes) (Grid3D.cpp:22-44) + Grid2D boxes (Grid2D.cpp:99-139):
+// one planner is a batch of one (see update_boxes_impl below)
 int hastar_update_boxes(hastar_handle h, const float* boxes, const float* conf, int n, float apf_added_radius) {
   if (!h || n < 0 || (n > 0 && (!boxes || !conf))) return fail(HASTAR_EINVAL, "bad argument");
+  return update_boxes_impl(&h, 1, boxes, conf, &n, apf_added_radius);
+}
+
+// The same update through the per-planner raster kernel with a device-wide hit-counter map
+// (DC.cnt): used for boxes whose footprint exceeds the LDS counters of the batched kernel.
+static int update_boxes_legacy(hastar_handle h, const float* boxes, const float* conf, int n, float apf_added_radius) {
   HIPCHK(hipSetDevice(h->device));
   DeviceCtx& DC = *h->dc;
   PlannerDev& D = h->desc;

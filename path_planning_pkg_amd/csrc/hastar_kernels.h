@@ -21,6 +21,10 @@ hipError_t launch_raster_boxes(float* occ, int* cnt, int N, const int* rp, const
 hipError_t launch_raster_lines(float* occ, int* cnt, int N, int n45, int n2, float res, const float* lp,
                                const float* seq_len, const float* seq_wid, int seq_stride, int nline, float lp_min,
                                float lp_max, int row0, int row1, hipStream_t st);
+hipError_t launch_decay_batch(const DecayItem* items, int n, size_t max_cells, hipStream_t st);
+hipError_t launch_relocate_batch(const RelocItem* items, int n, size_t max_cells, hipStream_t st);
+hipError_t launch_raster_boxes_batch(const RasterMap* maps, const RasterBox* boxes, int nbox, hipStream_t st);
+hipError_t launch_copy_batch(const CopyItem* items, int n, const float* src, hipStream_t st);
 struct VelParams { float max_velocity, coast_velocity, max_lat_acc, max_lat_acc_sqr, max_long_acc, max_long_dec; };
 hipError_t launch_velocity_profile(const VelParams& vp, int n, const long long* off, const float* xyh, const float* curv,
                                    const float* vel_init, const float* vmax_curr, const unsigned char* flags, float* vel,

@@ -1495,6 +1495,126 @@ __global__ __launch_bounds__(256) void k_raster_boxes(float* __restrict__ occ, i
   }
 }
 
+// ---- batched map updates: many planners' maps per launch (hastar_*_batch) ----------
+// Grid2D::update_obstacles() (Grid2D.cpp:197-208) of every map window of the batch:
+// blockIdx.y walks the items, blockIdx.x strides through one window (float4 where aligned).
+__device__ __forceinline__ float decay1(float v, float fr, float mn, float mx) {
+  return stl_max(stl_min(v + fr, mx), mn);
+}
+__global__ __launch_bounds__(256) void k_decay_batch(const DecayItem* __restrict__ items, int n) {
+  for (int q = blockIdx.y; q < n; q += gridDim.y) {
+    const DecayItem it = items[q];
+    float* occ = it.occ;
+    const size_t NN = (size_t)it.cells;
+    const size_t mis = (size_t)((4 - ((reinterpret_cast<uintptr_t>(occ) >> 2) & 3)) & 3);
+    const size_t head = mis < NN ? mis : NN;
+    const size_t n4 = (NN - head) / 4;
+    float4* o4 = reinterpret_cast<float4*>(occ + head);
+    const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x, dt = (size_t)gridDim.x * blockDim.x;
+    for (size_t t = t0; t < n4; t += dt) {
+      float4 v = o4[t];
+      v.x = decay1(v.x, it.lp_free, it.lp_min, it.lp_max);
+      v.y = decay1(v.y, it.lp_free, it.lp_min, it.lp_max);
+      v.z = decay1(v.z, it.lp_free, it.lp_min, it.lp_max);
+      v.w = decay1(v.w, it.lp_free, it.lp_min, it.lp_max);
+      o4[t] = v;
+    }
+    if (t0 < head) occ[t0] = decay1(occ[t0], it.lp_free, it.lp_min, it.lp_max);
+    for (size_t t = head + n4 * 4 + t0; t < NN; t += dt) occ[t] = decay1(occ[t], it.lp_free, it.lp_min, it.lp_max);
+  }
+}
+
+// Grid3D::relocate_obstacles (Grid3D.cpp:169-203) of every map of a chunk: claim pass (last
+// writer = largest linear source index wins, as in the reference's row-major loop), gather
+// into the map's scratch, copy back.
+__global__ __launch_bounds__(256) void k_relocate_claim_batch(const RelocItem* __restrict__ items, int n) {
+  for (int q = blockIdx.y; q < n; q += gridDim.y) {
+    const RelocItem it = items[q];
+    const int N = it.N;
+    const size_t NN = (size_t)N * N;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x) {
+      const float fi = (float)(int)(t / N), fj = (float)(int)(t % N);
+      float x = fi * it.c + fj * it.s;
+      float y = -fi * it.s + fj * it.c;
+      x = x + it.ox;
+      y = y + it.oy;
+      const int a = trunc_f(roundf(x)), b = trunc_f(roundf(y));
+      if (a > -1 && a < N && b > -1 && b < N) atomicMax(&it.winner[(size_t)a * N + b], (int)t);
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_relocate_gather_batch(const RelocItem* __restrict__ items, int n) {
+  for (int q = blockIdx.y; q < n; q += gridDim.y) {
+    const RelocItem it = items[q];
+    const size_t NN = (size_t)it.N * it.N;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x) {
+      const int w = it.winner[t];
+      it.tmp[t] = (w >= 0) ? it.occ[w] : 0.0f;
+      it.winner[t] = -1;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_relocate_copy_batch(const RelocItem* __restrict__ items, int n) {
+  for (int q = blockIdx.y; q < n; q += gridDim.y) {
+    const RelocItem it = items[q];
+    const size_t n4 = (size_t)it.N * it.N / 4, NN = (size_t)it.N * it.N;
+    const float4* s4 = reinterpret_cast<const float4*>(it.tmp);
+    float4* d4 = reinterpret_cast<float4*>(it.occ);
+    const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x, dt = (size_t)gridDim.x * blockDim.x;
+    for (size_t t = t0; t < n4; t += dt) d4[t] = s4[t];
+    for (size_t t = n4 * 4 + t0; t < NN; t += dt) it.occ[t] = it.tmp[t];
+  }
+}
+
+// Grid2D::update_obstacles(boxes) (Grid2D.cpp:99-139), one workgroup per box of one layer
+// (boxes of a layer never share a cell of their map; layers run in the reference's box
+// order).  Within a box every sub-sample applies the same clamped update, so the hits of a
+// cell are counted (LDS counters over the box footprint) and applied m times in a row —
+// the reference's sequential loop, with no device-wide scratch, so the boxes of many
+// planners can share a launch.
+__global__ __launch_bounds__(256) void k_raster_boxes_batch(const RasterMap* __restrict__ maps,
+                                                            const RasterBox* __restrict__ boxes, int nbox) {
+  __shared__ int hist[RASTER_HIST];
+  for (int q = blockIdx.x; q < nbox; q += gridDim.x) {
+    const RasterBox b = boxes[q];
+    const RasterMap m = maps[b.map];
+    const int cells = b.bw * b.bh;
+    for (int t = threadIdx.x; t < cells; t += blockDim.x) hist[t] = 0;
+    __syncthreads();
+    const int total = b.ni * b.nj;
+    for (int t = threadIdx.x; t < total; t += blockDim.x) {
+      const int i = t / b.nj, j = t % b.nj;
+      const float x0 = (float)(i * 0.5), y0 = (float)(j * 0.5);
+      const float x = x0 * m.c + y0 * m.s;
+      const float y = -x0 * m.s + y0 * m.c;
+      const int ip = b.si + trunc_f(roundf(x)), jp = b.sj + trunc_f(roundf(y));
+      if (ip >= m.r0 && ip < m.r1 && jp > -1 && jp < m.N) atomicAdd(&hist[(ip - b.bi0) * b.bh + (jp - b.bj0)], 1);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < cells; t += blockDim.x) {
+      const int cnt = hist[t];
+      if (cnt == 0) continue;
+      const size_t cell = (size_t)(b.bi0 + t / b.bh) * m.N + (b.bj0 + t % b.bh);
+      float v = m.occ[cell];
+      for (int r = 0; r < cnt; ++r) {
+        v += b.d;
+        v = stl_max(stl_min(v, m.lp_max), m.lp_min);
+      }
+      m.occ[cell] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// scatter of a batch's staged float lists (APF obstacle lists) into the planners' buffers
+__global__ __launch_bounds__(64) void k_copy_batch(const CopyItem* __restrict__ items, int n,
+                                                   const float* __restrict__ src) {
+  for (int q = blockIdx.x; q < n; q += gridDim.x) {
+    const CopyItem it = items[q];
+    for (int t = threadIdx.x; t < it.count; t += blockDim.x) it.dst[t] = src[it.src_off + t];
+  }
+}
+
 // Grid2D::update_obstacles(lines) (Grid2D.cpp:142-194).  lp: per line {ax, ay, dx, dy,
 // nx, ny, delta, n_len, n_wid}; seq_len / seq_wid: the reference's float-accumulated
 // progress values (prog_length / prog_width) computed on the host.
@@ -1776,6 +1896,33 @@ hipError_t launch_raster_lines(float* occ, int* cnt, int N, int n45, int n2, flo
                                int r0, int r1, hipStream_t st) {
   hipLaunchKernelGGL(k_raster_lines, dim3(1), dim3(1024), 0, st, occ, cnt, N, n45, n2, res, lp, seq_len, seq_wid,
                      stride, nline, mn, mx, r0, r1);
+  return hipGetLastError();
+}
+static dim3 batch_grid(int n, size_t cells) {
+  const size_t bx = std::min<size_t>((cells / 4 + 255) / 256 + 1, 256);
+  return dim3((unsigned)bx, (unsigned)std::min(n, 65535));
+}
+hipError_t launch_decay_batch(const DecayItem* items, int n, size_t max_cells, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_decay_batch, batch_grid(n, max_cells), dim3(256), 0, st, items, n);
+  return hipGetLastError();
+}
+hipError_t launch_relocate_batch(const RelocItem* items, int n, size_t max_cells, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const dim3 g = batch_grid(n, max_cells * 4);
+  hipLaunchKernelGGL(k_relocate_claim_batch, g, dim3(256), 0, st, items, n);
+  hipLaunchKernelGGL(k_relocate_gather_batch, g, dim3(256), 0, st, items, n);
+  hipLaunchKernelGGL(k_relocate_copy_batch, batch_grid(n, max_cells), dim3(256), 0, st, items, n);
+  return hipGetLastError();
+}
+hipError_t launch_raster_boxes_batch(const RasterMap* maps, const RasterBox* boxes, int nbox, hipStream_t st) {
+  if (nbox <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_raster_boxes_batch, dim3(std::min(nbox, 65535)), dim3(256), 0, st, maps, boxes, nbox);
+  return hipGetLastError();
+}
+hipError_t launch_copy_batch(const CopyItem* items, int n, const float* src, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_copy_batch, dim3(std::min(n, 65535)), dim3(64), 0, st, items, n, src);
   return hipGetLastError();
 }
 hipError_t launch_velocity_profile(const VelParams& vp, int n, const long long* off, const float* xyh, const float* curv,

@@ -155,6 +155,47 @@ struct PlannerDev {
   SearchResult* result;
 };
 
+// ---- batched map updates (hastar_*_batch): one launch serves many planners' maps ----
+// Grid2D::update_obstacles() of one map window (Grid2D.cpp:197-208)
+struct DecayItem {
+  float* occ;        // first cell of the window
+  long long cells;   // cells in the window
+  float lp_free, lp_min, lp_max, pad;
+};
+// Grid3D::relocate_obstacles of one map (Grid3D.cpp:169-203) with its scratch
+struct RelocItem {
+  float* occ;        // map (source, then destination of the copy-back)
+  float* tmp;        // N*N scratch: the relocated map
+  int* winner;       // N*N scratch, kept at -1 between uses
+  int N;
+  float c, s, ox, oy;
+  int pad;
+};
+// one planner of a batched box raster
+struct RasterMap {
+  float* occ;
+  int N, r0, r1;     // map size and row window
+  float c, s, lp_min, lp_max;
+  int pad;
+};
+// one box (Grid2D.cpp:99-139): sub-sample origin and counts, log-odds delta, and the cell
+// window that holds every sub-sample (the layer footprint of hastar_update_boxes)
+struct RasterBox {
+  int map;           // index into the RasterMap array
+  int si, sj, ni, nj;
+  float d;
+  int bi0, bj0;      // footprint origin (cells)
+  int bw, bh;        // footprint size (cells), bw * bh <= RASTER_HIST
+  int pad0, pad1;
+};
+constexpr int RASTER_HIST = 8192;  // LDS hit counters of one box footprint (32 KiB)
+// a device-to-device copy of `count` floats (APF lists of a batch)
+struct CopyItem {
+  float* dst;
+  long long src_off;
+  int count, pad;
+};
+
 // Open-tree capacity of an inner A* search while it stays in LDS (kernel and host agree).
 constexpr int ASTAR_LDS_CAP = 1024;
 

@@ -73,6 +73,10 @@ def load_library():
     L.hastar_velocity_profile_batch.argtypes = [C.c_int, C.POINTER(HastarVelocityParams), C.c_int,
                                                 C.POINTER(C.c_longlong), fp, fp, fp, fp, C.POINTER(C.c_ubyte), fp,
                                                 C.POINTER(C.c_ubyte)]
+    hp = C.POINTER(C.c_void_p)
+    L.hastar_update_goal_batch.argtypes = [hp, C.c_int, fp, fp]
+    L.hastar_decay_batch.argtypes = [hp, C.c_int]
+    L.hastar_update_boxes_batch.argtypes = [hp, C.c_int, fp, fp, ip, C.c_float]
     L.hastar_velocity_profile_last_batch.argtypes = [C.c_int, C.POINTER(HastarVelocityParams), C.c_int, fp, fp,
                                                      C.POINTER(C.c_ubyte), fp, C.POINTER(C.c_ubyte)]
     _lib = L
@@ -389,6 +393,37 @@ def reset_batch(planners_or_buffers):
         n = len(b)
         hs = (C.c_void_p * n)(*[p.h.value for p in b])
     _check(load_library().hastar_reset_batch(hs, n))
+
+
+def _handles(planners_or_buffers):
+    b = planners_or_buffers
+    if isinstance(b, BatchBuffers):
+        return b.hs, b.n
+    return (C.c_void_p * len(b))(*[p.h.value for p in b]), len(b)
+
+
+def update_goal_batch(planners, goals, starts):
+    """update_goal of every planner in one call (hastar_update_goal_batch)."""
+    hs, n = _handles(planners)
+    _check(load_library().hastar_update_goal_batch(hs, n, fptr(_f32(goals, (n, 3))), fptr(_f32(starts, (n, 3)))))
+
+
+def decay_batch(planners):
+    """update_obstacles() of every planner in one launch (hastar_decay_batch)."""
+    hs, n = _handles(planners)
+    _check(load_library().hastar_decay_batch(hs, n))
+
+
+def update_boxes_batch(planners, boxes_list, conf_list, apf_added_radius):
+    """update_obstacles(boxes, confidence, r) of every planner (hastar_update_boxes_batch):
+    boxes_list[i] is planner i's (k_i x 4) boxes, conf_list[i] its k_i confidences."""
+    hs, n = _handles(planners)
+    counts = np.array([len(b) for b in boxes_list], np.int32)
+    B = _f32(np.concatenate([_f32(b, (-1, 4)) for b in boxes_list]) if n else np.zeros((0, 4)), (-1, 4))
+    Cf = _f32(np.concatenate([_f32(c) for c in conf_list]) if n else np.zeros(0))
+    if len(B) != counts.sum() or len(Cf) != counts.sum():
+        raise ValueError("update_boxes_batch: box and confidence counts differ")
+    _check(load_library().hastar_update_boxes_batch(hs, n, fptr(B), fptr(Cf), iptr(counts), float(apf_added_radius)))
 
 
 def find_path_batch_arrays(planners, vels, starts, cap=4096, buffers=None):

@@ -65,6 +65,26 @@ def drive(planner, proto):
     planner.reset()
 
 
+def drive_batch(gpu, planners, protos):
+    """drive() of many GPU planners through the batched map-update entry points
+    (hastar_update_goal_batch / hastar_decay_batch / hastar_update_boxes_batch): the same
+    call sequence per planner, bit for bit, in a handful of launches.  Lines (absent from the
+    synthetic workloads) go through the per-planner call."""
+    gpu.update_goal_batch(planners, [p["goal"] for p in protos], [p["start"] for p in protos])
+    cycles = protos[0]["cycles"]
+    assert all(p["cycles"] == cycles for p in protos)
+    apf_r = protos[0]["apf_r"]
+    assert all(p["apf_r"] == apf_r for p in protos)
+    for _ in range(cycles):
+        gpu.decay_batch(planners)
+        for pl, p in zip(planners, protos):
+            if len(p["lines"]):
+                pl.update_lines(p["lines"], [p["line_conf"]] * len(p["lines"]), p["line_width"])
+        gpu.update_boxes_batch(planners, [p["boxes"] for p in protos],
+                               [np.full(len(p["boxes"]), p["box_conf"], np.float32) for p in protos], apf_r)
+    gpu.reset_batch(planners)
+
+
 def replan_pairs(N, bins, K, n_pairs, seed, res=0.5, clear=8.0):
     """n_pairs start/goal pairs on an N x N grid.  Each goal is uniform in
     +-0.15 W with a uniform heading; the start lies U(0.3, 0.6) W behind it along that

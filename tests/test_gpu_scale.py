@@ -185,3 +185,61 @@ def test_velocity_profile_of_last_batch(gpu, oracle_lib):
                                                bool(flags[i] & 1), bool(flags[i] & 2))
         assert bool(feas[i]) == ok_o
         assert_bits_equal(vel[a:b], vo, f"velocity of path {i}")
+
+
+# ---------------------------------------------------------- batched map updates --------
+def test_batched_map_updates_equal_single_calls(gpu, oracle_lib):
+    """hastar_update_goal_batch / hastar_decay_batch / hastar_update_boxes_batch over planners
+    of different grid sizes, goal frames, row windows and overlapping boxes with per-box
+    confidences: every map and APF list equals the oracle's per-instance updates (Grid2D.cpp:
+    99-208, Grid3D.cpp:22-44, 102-203), and a search on a batch-built map equals the oracle's."""
+    from path_planning_pkg_amd.capi import PlannerConfig
+    rng = np.random.default_rng(23)
+    sizes = [128, 200, 256, 97, 256, 180]
+    cfgs = [PlannerConfig(grid_size=N, num_angle_bins=36) for N in sizes]
+    gs = [gpu.HybridAStar(c) for c in cfgs]
+    os_ = [oracle_lib.OraclePlanner(c) for c in cfgs]
+    goals = rng.uniform(-5, 5, (len(gs), 3)).astype(np.float32)
+    starts = np.concatenate([rng.uniform(-40, -20, (len(gs), 2)), np.zeros((len(gs), 1))], 1).astype(np.float32)
+    gs[4].set_row_window(37, 201)  # a row window applies to decay and boxes alike
+    gpu.update_goal_batch(gs, goals, starts)
+    for o, g0, s0 in zip(os_, goals, starts):
+        o.update_goal(g0, s0)
+    for cyc in range(4):
+        bl, cl = [], []
+        for i in range(len(gs)):
+            k = int(rng.integers(0, 90))
+            b = np.stack([rng.uniform(-40, 10, k), rng.uniform(-30, 20, k), rng.uniform(0.5, 9, k),
+                          rng.uniform(0.5, 9, k)], 1).astype(np.float32)
+            bl.append(b)
+            cl.append(rng.uniform(0.05, 0.97, k).astype(np.float32))
+        gpu.decay_batch(gs)
+        gpu.update_boxes_batch(gs, bl, cl, 1.5)
+        for o, b, c in zip(os_, bl, cl):
+            o.decay()
+            o.update_boxes(b, c, 1.5)
+        for i, (g, o) in enumerate(zip(gs, os_)):
+            m, ref = g.get_obstacles(), o.get_obstacles()
+            if i == 4:
+                assert_bits_equal(m[37:201], ref[37:201], f"windowed map {i} cycle {cyc}")
+            else:
+                assert_bits_equal(m, ref, f"map {i} cycle {cyc}")
+            assert_bits_equal(g.apf(), o.apf(), f"APF list {i} cycle {cyc}")
+    # a second goal change relocates every map in one batched call
+    goals2 = rng.uniform(-5, 5, (len(gs), 3)).astype(np.float32)
+    gpu.update_goal_batch(gs, goals2, starts)
+    for i, (o, g0, s0) in enumerate(zip(os_, goals2, starts)):
+        o.update_goal(g0, s0)
+        if i != 4:
+            assert_bits_equal(gs[i].get_obstacles(), o.get_obstacles(), f"relocated map {i}")
+    # the synthetic workload built with drive_batch searches like the oracle
+    from tests.scenarios import drive_batch
+    cases = [synthetic(256, 36, 40, s) for s in (1, 2, 4)]
+    gb = [gpu.HybridAStar(c) for c, _ in cases]
+    drive_batch(gpu, gb, [p for _, p in cases])
+    for g, (cfg, proto) in zip(gb, cases):
+        o = oracle_lib.OraclePlanner(cfg)
+        drive(o, proto)
+        assert_bits_equal(g.get_obstacles(), o.get_obstacles(), "drive_batch map")
+        compare_results(g.find_path(proto["vel"], proto["start"]), o.find_path(proto["vel"], proto["start"]),
+                        "search on a drive_batch map")
