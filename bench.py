@@ -1,21 +1,29 @@
 """bench.py — Hybrid A* node expansions/sec on the 1024x1024x72 grid (BASELINE.json configs[2]).
 
-Workload (one "step"): a batch of B independent planners (SURVEY.md §8d synthetic
-generator: N = 1024, 72 angle bins, K = 200 box obstacles, seed = query id; the reference's
-only motion mode: forward Dubins), each already set up in HBM (update_goal, 5 x {decay,
-boxes}); the step resets the holonomic memo of every planner (HybridAStar::reset) and runs
-ONE batched find_path launch — one wavefront per planner.
+Workload (one "step"): a batch of B independent planners per GPU (SURVEY.md §8d synthetic
+generator: N = 1024, 72 angle bins, K = 200 box obstacles, seed = query id + 1; the
+reference's only motion mode: forward Dubins), each already set up in HBM (update_goal,
+5 x {decay, boxes} through the batched map-update ABI); the step resets the holonomic memo
+of every planner (HybridAStar::reset) and runs ONE batched find_path — one wavefront per
+planner (plus resume launches for searches that outgrow their arena, if any).
 value = total pops of all planners on all ranks / wall time of the K timed steps (max over
-ranks).  One rank per GPU (torch.distributed over RCCL for the barrier/reductions only):
+ranks).  One rank per GPU (torch.distributed; RCCL for the barrier / reductions only):
 planners are sharded across ranks with no data-path collective -> weak scaling.
 
-Extra fields: plan latency of a single query (median of single-planner searches),
-roofline of the search kernel (algorithmic bytes of SURVEY.md §8d per launch / kernel time
-from HIP events on the launch stream), and the CPU oracle timed on the host (rank 0).
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment starts
+torch.distributed.run with N ranks as a child process (before anything touches a GPU) and
+exits with its status.
+
+Extra fields: the first (cold: no longest-first history) step's throughput, plan latency of
+single queries on the GPU and on one CPU core for the SAME queries, the search kernel's
+roofline (SURVEY.md §8d algorithmic bytes / kernel time from HIP events on its stream), and
+the CPU oracle timed on `cores` host threads, one private planner per thread (rank 0).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -26,6 +34,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "Hybrid A* node expansions/sec + plan latency, 1024x1024x72 grid"
 
 
 def algorithmic_bytes(st, K):
@@ -41,6 +50,12 @@ def shard_query_ids(rank, world, batch):
     return [rank * batch + i for i in range(batch)]
 
 
+def shard_global_ids(rank, world, total):
+    """A fixed global set of `total` ids dealt round-robin over the ranks (strong scaling)."""
+    assert 0 <= rank < world
+    return list(range(rank, total, world))
+
+
 def reduce_over_ranks(dist, elapsed, pops, device):
     """(max elapsed, total pops) over ranks; identity without a process group."""
     if dist is None:
@@ -53,19 +68,35 @@ def reduce_over_ranks(dist, elapsed, pops, device):
     return float(tmax[0]), float(tsum[0])
 
 
-def build_planners(gpu, cfgs, device):
-    from tests.scenarios import drive
-    planners = []
-    for cfg, proto in cfgs:
-        p = gpu.HybridAStar(cfg, device=device)
-        drive(p, proto)
-        planners.append(p)
-    return planners
+def cpu_threads():
+    """Host threads of the CPU baseline: HASTAR_CPU_THREADS, else OMP_NUM_THREADS (the GPU
+    box sets it to this job's CPU share), else the visible cores."""
+    for k in ("HASTAR_CPU_THREADS", "OMP_NUM_THREADS"):
+        v = os.environ.get(k)
+        if v and v.isdigit() and int(v) > 0:
+            return int(v)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
-def main():
+def launch_ranks(args):
+    """Start `args.gpus` ranks under torch.distributed.run (a child process; this process has
+    not touched a GPU) and return its exit status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); > 1 without WORLD_SIZE spawns them")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("HASTAR_BENCH_BATCH", "23552")),
@@ -73,7 +104,7 @@ def main():
     ap.add_argument("--grid", type=int, default=None, help="default 1024 (cfg3, cfg5) or 2048 (cfg4)")
     ap.add_argument("--bins", type=int, default=72)
     ap.add_argument("--obstacles", type=int, default=200)
-    ap.add_argument("--max-pops", type=int, default=0, help="0 = library default (262144)")
+    ap.add_argument("--max-pops", type=int, default=0, help="initial arena of a search in pops (0 = 262144)")
     ap.add_argument("--max-astar-nodes", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -83,13 +114,22 @@ def main():
                          "cfg4: 2048^2 queries with the map build row-sharded over the ranks + RCCL all-gather "
                          "(BASELINE.json configs[3]); cfg5: 20 Hz replan loop of start/goal pairs (configs[4])")
     ap.add_argument("--map-queries", type=int, default=16, help="cfg4: maps built both locally and row-sharded")
-    ap.add_argument("--pairs", type=int, default=64, help="cfg5: start/goal pairs per GPU")
-    args = ap.parse_args()
+    ap.add_argument("--pairs", type=int, default=64, help="cfg5: start/goal pairs in total, dealt over the ranks")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU work: exercises the launcher, sharding and reductions only (CPU rehearsal)")
+    args = ap.parse_args(argv)
     if args.grid is None:
         args.grid = 2048 if args.workload == "cfg4" else 1024
     if args.workload == "cfg4" and "--batch" not in sys.argv and "HASTAR_BENCH_BATCH" not in os.environ:
         args.batch = 6144  # 2048^2 maps: 32 MiB per planner; the arena pool takes the rest of the HBM
+    return args
 
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     # search arenas may take 95% of the HBM left after the planners' maps (library default 80%)
     os.environ.setdefault("HASTAR_ARENA_FRAC", "0.95")
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -100,29 +140,26 @@ def main():
     if world > 1:
         import torch.distributed as dist_mod
         dist = dist_mod
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        if args.backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(args.backend)
     device = local_rank
+    red_dev = f"cuda:{device}" if args.backend == "nccl" and not args.dry_run else "cpu"
+    if args.dry_run:
+        return run_dry(args, dist, rank, world, red_dev)
 
     from path_planning_pkg_amd import planner as gpu
-    from path_planning_pkg_amd.capi import PlannerConfig
-    from tests.scenarios import synthetic
 
     if args.workload == "cfg5":
         return run_cfg5(args, gpu, dist, torch, rank, world, device)
     B = args.batch
     map_build = map_build_phase(args, gpu, dist, torch, rank, world, device) if args.workload == "cfg4" else None
-
-    def cfg_for(q):
-        cfg, proto = synthetic(args.grid, args.bins, args.obstacles, seed=q + 1)
-        cfg.values["max_pops"] = args.max_pops
-        cfg.values["max_astar_nodes"] = args.max_astar_nodes
-        return cfg, proto
-
     qids = shard_query_ids(rank, world, B)
-    cfgs = [cfg_for(q) for q in qids]
+    t_gen = time.perf_counter()
+    cfgs = [query_case(args, q) for q in qids]
+    t_gen = time.perf_counter() - t_gen
     t_setup = time.perf_counter()
-    planners = build_planners(gpu, cfgs, device)
+    planners, setup_split = build_planners(gpu, cfgs, device)
     t_setup = time.perf_counter() - t_setup
     vels = [c[1]["vel"] for c in cfgs]
     starts = [c[1]["start"] for c in cfgs]
@@ -132,29 +169,35 @@ def main():
 
     def step():
         gpu.reset_batch(bufs)  # HybridAStar::reset() of every planner
-        br = gpu.find_path_batch_arrays(planners, vels, starts, buffers=bufs)
-        return br, br.kernel_ms
+        return gpu.find_path_batch_arrays(planners, vels, starts, buffers=bufs)
 
-    for _ in range(args.warmup):
+    # the first step is cold: the longest-first queue has no history yet
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    r0 = step()
+    cold_s = time.perf_counter() - t0
+    cold_pops = int(r0.stats["pops"].sum())
+    cold_s, cold_pops_all = reduce_over_ranks(dist, cold_s, cold_pops, f"cuda:{device}")
+    for _ in range(max(args.warmup - 1, 0)):
         step()
     if dist:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     pops = 0
-    kernel_ms = []
-    alg_bytes = []
+    kernel_ms, alg_bytes = [], []
     statuses = set()
-    oks = 0
+    oks, parks = 0, 0
     last = None
     for _ in range(args.steps):
-        res, kms = step()
-        kernel_ms.append(kms)
+        res = step()
+        kernel_ms.append(res.kernel_ms)
         st = res.stats
         pops += int(st["pops"].sum())
         alg_bytes.append(algorithmic_bytes(st, args.obstacles))
         statuses |= set(int(v) for v in np.unique(st["status"]))
         oks += int(res.ok.sum())
+        parks += int(st["parks"].sum())
         last = res
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
@@ -163,16 +206,20 @@ def main():
     out = None
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
-        value = pops_all / elapsed
         avg_kernel_ms = float(np.mean(kernel_ms))
         achieved = float(np.mean(alg_bytes)) / (avg_kernel_ms * 1e-3) / 1e9
-        # single-query plan latency (the second half of the metric)
+        vel_prof = velocity_profile_phase(gpu, last, device, vels)  # before any other find_path
+        lat_ids = list(range(min(args.latency_queries, B)))
         lat = []
-        for p, c in list(zip(planners, cfgs))[: args.latency_queries]:
-            p.reset()
-            r, kms = gpu.find_path_batch([p], [c[1]["vel"]], [c[1]["start"]], cap=8192)
+        for i in lat_ids:  # single-query plan latency (the second half of the metric)
+            planners[i].reset()
+            _, kms = gpu.find_path_batch([planners[i]], [vels[i]], [starts[i]], cap=8192)
             lat.append(kms)
-        vel_prof = velocity_profile_phase(gpu, last, device, [c[1]["vel"] for c in cfgs])
+        # the batch's longest search alone (its latency bounds the step)
+        li = int(np.argmax(last.stats["pops"]))
+        longest = {"query": qids[li], "pops": int(last.stats["pops"][li])}
+        planners[li].reset()
+        _, longest["gpu_ms_alone"] = gpu.find_path_batch([planners[li]], [vels[li]], [starts[li]], cap=8192)
         traffic = None
         pmc = ROOT / "profiles" / "pmc_search_summary.json"
         if pmc.exists():
@@ -183,8 +230,8 @@ def main():
             except (ValueError, OSError):
                 traffic = None
         out = {
-            "metric": "Hybrid A* node expansions/sec + plan latency, 1024x1024x72 grid",
-            "value": value,
+            "metric": METRIC,
+            "value": pops_all / elapsed,
             "unit": "expansions/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -194,33 +241,87 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (SURVEY.md §8d generator; seeds = query ids)",
+            "data": "synthetic (SURVEY.md §8d generator; seeds = query ids + 1)",
             "config": {"workload": f"{args.workload}: {args.grid}x{args.grid}x{args.bins} grid, {args.obstacles} box "
                                    f"obstacles, batch of {B} independent queries per GPU, forward Dubins"
                                    + (", map build row-sharded over the ranks + RCCL all-gather (map_build)"
                                       if map_build else ""),
                        "grid": args.grid, "angle_bins": args.bins, "obstacles": args.obstacles,
                        "queries_per_gpu": B, "global_batch": B * world, "parallelism": f"query-sharded x{world}"},
-            "plan_latency_ms": float(np.median(lat)) if lat else None,
+            "kernel_only_value": pops_all / elapsed * ms_per_step / avg_kernel_ms,
+            "cold_first_step": {"value": cold_pops_all / cold_s, "ms": cold_s * 1e3,
+                                "note": "first launch of the batch: no longest-first history"},
+            "plan_latency_ms": {"gpu_median": float(np.median(lat)) if lat else None, "queries": [qids[i] for i in lat_ids],
+                                "gpu": lat},
+            "longest_query": longest,
             "pops_per_step": pops_all / args.steps,
             "success_rate": oks / (B * args.steps),
             "search_status": sorted(statuses),
+            "parks_per_step": parks / args.steps,
             "setup_s_per_gpu": t_setup,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+            "setup_split_s": dict(setup_split, inputs_generated_s=t_gen),
+            "roofline": {"bound": "latency", "roof": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                          "kernel": "hastar_search_kernel", "kernel_ms": avg_kernel_ms,
-                         "alg_bytes_per_launch": float(np.mean(alg_bytes))},
+                         "alg_bytes_per_launch": float(np.mean(alg_bytes)),
+                         "note": "dependent per-wave round trips bound the search, not HBM bandwidth "
+                                 "(SQ/TCC counters in profiles/, DESIGN.md §4.1)"},
         }
         if map_build:
             out["map_build"] = map_build
         out["velocity_profile"] = vel_prof
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps)
+            cb = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps, lat_ids)
+            out["cpu_baseline"] = cb
+            out["plan_latency_ms"]["cpu_same_queries_median"] = cb.pop("latency_same_queries_ms", None)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
     if out is not None:
         print(json.dumps(out))
+
+
+def query_case(args, q):
+    from tests.scenarios import synthetic
+    cfg, proto = synthetic(args.grid, args.bins, args.obstacles, seed=q + 1)
+    cfg.values["max_pops"] = args.max_pops
+    cfg.values["max_astar_nodes"] = args.max_astar_nodes
+    return cfg, proto
+
+
+def build_planners(gpu, cfgs, device):
+    """Create the planners and run the fixture protocol on all of them through the batched
+    map-update ABI (tests/scenarios.py::drive_batch)."""
+    import torch
+    from tests.scenarios import drive_batch
+    t0 = time.perf_counter()
+    planners = [gpu.HybridAStar(cfg, device=device) for cfg, _ in cfgs]
+    t1 = time.perf_counter()
+    drive_batch(gpu, planners, [proto for _, proto in cfgs])
+    torch.cuda.synchronize(device)
+    t2 = time.perf_counter()
+    return planners, {"create_s": t1 - t0, "map_updates_s": t2 - t1}
+
+
+def run_dry(args, dist, rank, world, red_dev):
+    """--dry-run: the launcher / sharding / reduction path without GPU work (each 'query'
+    counts one pop), so a CPU box can rehearse `bench.py --gpus N`."""
+    ids = shard_global_ids(rank, world, args.pairs) if args.workload == "cfg5" else shard_query_ids(rank, world, args.batch)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    elapsed, pops_all = reduce_over_ranks(dist, time.perf_counter() - t0, len(ids), red_dev)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": pops_all / elapsed, "unit": "expansions/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3,
+                          "higher_is_better": True, "scaling": "strong" if args.workload == "cfg5" else "weak",
+                          "vs_baseline": None, "dtype": "f32", "data": "dry run (no GPU work)",
+                          "config": {"workload": args.workload, "units_total": int(pops_all),
+                                     "parallelism": f"x{world}"}}))
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 # VelocityGenerator parameters for the post-search stage (synthetic; the reference's
@@ -229,12 +330,25 @@ VEL_PARAMS = (10.0, 3.0, 2.5, 1.5, 3.0)
 
 
 def velocity_profile_phase(gpu, last, device, vels):
-    """VelocityGenerator<float> over every successful path of the last timed step
-    (SURVEY §8(f) rank 3): one packed hastar_velocity_profile_batch call, timed after a
-    warm-up call.  Host buffers in and out, so the time is PCIe-inclusive."""
+    """VelocityGenerator<float> over every path of the last timed step,
+    two ways: (a) device-resident — hastar_velocity_profile_last_batch profiles the paths where
+    the batch packed them in HBM (local_planner.cpp:316-323 profiles the search's own output),
+    velocities back to the host; (b) host buffers in and out (PCIe-inclusive, paths uploaded).
+    (b) is compared with the oracle bit for bit, (a) with (b).  Must run before any other
+    find_path call on the device (it would replace the last batch)."""
     idx = np.nonzero(last.ok & (last.lens > 0))[0]
     if len(idx) == 0:
         return None
+    n_all = len(last.lens)
+    vg = gpu.VelocityGenerator(*VEL_PARAMS, device=device)
+    v0a = np.asarray(vels, np.float32)
+    vma = np.full(n_all, VEL_PARAMS[0], np.float32)
+    fla = np.full(n_all, 2, np.uint8)
+    lens_all = last.lens.astype(np.int64).copy()
+    vg.profile_last_batch(lens_all, v0a, vma, fla)
+    t0 = time.perf_counter()
+    feas_a, vel_a = vg.profile_last_batch(lens_all, v0a, vma, fla)
+    ms_dev = (time.perf_counter() - t0) * 1e3
     lens = last.lens[idx].astype(np.int64)
     off = np.zeros(len(idx) + 1, np.int64)
     np.cumsum(lens, out=off[1:])
@@ -243,7 +357,6 @@ def velocity_profile_phase(gpu, last, device, vels):
     v0 = np.asarray([vels[i] for i in idx], np.float32)
     vm = np.full(len(idx), VEL_PARAMS[0], np.float32)
     flags = np.full(len(idx), 2, np.uint8)  # stop_at_goal
-    vg = gpu.VelocityGenerator(*VEL_PARAMS, device=device)
     vg.profile_packed(off, X, K, v0, vm, flags)
     t0 = time.perf_counter()
     feas, vel = vg.profile_packed(off, X, K, v0, vm, flags)
@@ -259,7 +372,14 @@ def velocity_profile_phase(gpu, last, device, vels):
         vg_ = vel[a:b]
         nan = np.isnan(vo) & np.isnan(vg_)  # NaN payloads are not part of the contract
         same = same and ok_o == bool(feas[j]) and bool((nan | (vo.view(np.uint32) == vg_.view(np.uint32))).all())
-    return {"paths": int(len(idx)), "points": int(off[-1]), "ms_pcie_inclusive": ms,
+    # (a) vs (b): the device-resident profile of every successful path, bit for bit
+    off_all = np.zeros(n_all + 1, np.int64)
+    np.cumsum(lens_all, out=off_all[1:])
+    same_dev = bool(all(bool(feas_a[i]) == bool(feas[j]) and np.array_equal(
+        vel_a[off_all[i]:off_all[i + 1]].view(np.uint32), vel[off[j]:off[j + 1]].view(np.uint32))
+        for j, i in enumerate(idx)))
+    return {"paths": int(len(idx)), "points": int(off[-1]), "ms_device_resident": ms_dev,
+            "device_resident_equals_host_path": same_dev, "ms_pcie_inclusive": ms,
             "paths_per_s": len(idx) / (ms * 1e-3), "feasible_rate": float(feas.mean()),
             "cpu_oracle_ms": cpu_s * 1e3, "cpu_oracle_cores": 1, "parity_with_oracle": bool(same),
             "params": dict(zip(("max_velocity", "coast_velocity", "max_lat_acc", "max_long_acc", "max_long_dec"),
@@ -317,27 +437,29 @@ def map_build_phase(args, gpu, dist, torch, rank, world, device):
 
 def run_cfg5(args, gpu, dist, torch, rank, world, device):
     """BASELINE.json configs[4] / SURVEY.md §8d cfg5: the local planner's replan loop for
-    `pairs` start/goal pairs per GPU (pair ids rank*pairs ...; weak scaling, no exchange).
-    One step = one 20 Hz tick of every pair: a batched find_path WITHOUT reset (memo and
-    stale node-map values carry over, local_planner.cpp:316), then free-space decay and the
-    boxes moved by their velocity (local_planner.cpp:241,288).  value = pops / tick wall
-    (max over ranks); the tick wall includes the map upkeep."""
-    from tests.scenarios import drive, replan_pairs, replan_tick, replan_tick_inputs
-    P = args.pairs
+    `pairs` start/goal pairs IN TOTAL, dealt round-robin over the ranks (strong scaling, no
+    exchange; pair id q uses seed 1000 + q).  One step = one 20 Hz tick of every pair: a
+    batched find_path WITHOUT reset (memo and stale node-map values carry over,
+    local_planner.cpp:316), then free-space decay and the boxes moved by their velocity
+    (local_planner.cpp:241,288).  value = pops / tick wall (max over ranks); the tick wall
+    includes the map upkeep."""
+    from tests.scenarios import drive_batch, replan_pairs, replan_tick_inputs
+    ids = shard_global_ids(rank, world, args.pairs)
     pairs = []
-    for q in shard_query_ids(rank, world, P):  # one generator draw per pair id
+    for q in ids:  # one generator draw per pair id
         pairs += replan_pairs(args.grid, args.bins, args.obstacles, 1, seed=1000 + q)
     t_setup = time.perf_counter()
     planners = []
     for cfg, proto, _ in pairs:
         cfg.values["max_pops"] = args.max_pops
         cfg.values["max_astar_nodes"] = args.max_astar_nodes
-        p = gpu.HybridAStar(cfg, device=device)
-        drive(p, proto)
-        planners.append(p)
+        planners.append(gpu.HybridAStar(cfg, device=device))
+    drive_batch(gpu, planners, [proto for _, proto, _ in pairs])
     t_setup = time.perf_counter() - t_setup
     bufs = gpu.BatchBuffers(planners, cap=8192)
     vels = [proto["vel"] for _, proto, _ in pairs]
+    conf = [np.full(len(proto["boxes"]), proto["box_conf"], np.float32) for _, proto, _ in pairs]
+    apf_r = pairs[0][1]["apf_r"] if pairs else 2.5
     tick = [0]
 
     def step():
@@ -345,8 +467,9 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
         starts = [replan_tick_inputs(proto, v, t)[0] for _, proto, v in pairs]
         br = gpu.find_path_batch_arrays(planners, vels, starts, buffers=bufs)
         st = br.stats.copy()
-        for p, (_, proto, v) in zip(planners, pairs):
-            replan_tick(p, proto, v, t)
+        # the tick's map upkeep (local_planner.cpp:241,288), batched: decay + moved boxes
+        gpu.decay_batch(bufs)
+        gpu.update_boxes_batch(bufs, [replan_tick_inputs(proto, v, t + 1)[1] for _, proto, v in pairs], conf, apf_r)
         tick[0] += 1
         return st, br.kernel_ms, int(br.ok.sum())
 
@@ -371,20 +494,22 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
         avg_k = float(np.mean(kms))
         achieved = float(np.mean(alg)) / (avg_k * 1e-3) / 1e9
         out = {
-            "metric": "Hybrid A* node expansions/sec + plan latency, 1024x1024x72 grid",
+            "metric": METRIC,
             "value": pops_all / elapsed, "unit": "expansions/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (SURVEY.md §8d cfg5 generator; pair ids seed the boxes, goals and box velocities)",
             "config": {"workload": f"cfg5: {args.grid}x{args.grid}x{args.bins} grid, {args.obstacles} moving boxes, "
-                                   f"{P} start/goal pairs per GPU replanned every 50 ms tick without reset",
-                       "grid": args.grid, "angle_bins": args.bins, "obstacles": args.obstacles, "pairs_per_gpu": P,
-                       "global_batch": P * world, "parallelism": f"pair-sharded x{world}"},
+                                   f"{args.pairs} start/goal pairs in total replanned every 50 ms tick without reset",
+                       "grid": args.grid, "angle_bins": args.bins, "obstacles": args.obstacles,
+                       "pairs_total": args.pairs, "pairs_rank0": len(ids), "global_batch": args.pairs,
+                       "parallelism": f"pair-sharded x{world}"},
             "replan_latency_ms": avg_k, "tick_ms": elapsed / args.steps * 1e3,
-            "tick_budget_ms": 50.0, "success_rate": oks / (P * args.steps), "setup_s_per_gpu": t_setup,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": "hastar_search_kernel",
-                         "kernel_ms": avg_k, "alg_bytes_per_launch": float(np.mean(alg))},
+            "tick_budget_ms": 50.0, "success_rate": oks / max(len(ids) * args.steps, 1), "setup_s_per_gpu": t_setup,
+            "roofline": {"bound": "latency", "roof": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                         "kernel": "hastar_search_kernel", "kernel_ms": avg_k,
+                         "alg_bytes_per_launch": float(np.mean(alg))},
         }
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_cfg5(pairs, args.cpu_seconds, args.warmup + args.steps)
@@ -396,10 +521,13 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
 
 
 def cpu_baseline_cfg5(pairs, budget_s, ticks):
-    """The oracle replaying the same pairs' replan loops (1 thread, find_path timed only)."""
+    """The oracle replaying the same pairs' replan loops (1 thread per pair, find_path timed
+    only): a tick's pairs are independent, so the CPU's tick takes as long as its slowest pair
+    when it has a core per pair; reported as the single-thread rate and that tick time."""
     from oracle.pyoracle import OraclePlanner
     from tests.scenarios import drive, replan_tick, replan_tick_inputs
     pops, wall, n = 0, 0.0, 0
+    tick_max = np.zeros(ticks)
     for cfg, proto, v in pairs:
         o = OraclePlanner(cfg)
         drive(o, proto)
@@ -407,50 +535,66 @@ def cpu_baseline_cfg5(pairs, budget_s, ticks):
             r = o.find_path(proto["vel"], replan_tick_inputs(proto, v, t)[0])
             pops += r["stats"]["pops"]
             wall += r["wall_ms"] * 1e-3
+            tick_max[t] = max(tick_max[t], r["wall_ms"])
             replan_tick(o, proto, v, t)
         o.close()
         n += 1
         if wall >= budget_s:
             break
     return {"value": pops / wall if wall > 0 else None, "unit": "expansions/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} pairs x {ticks} ticks (same call sequence as the GPU run), find_path only, "
-                      f"1 thread (oracle/hastar_oracle.cpp)"}
+            "sample": f"first {n} pairs of rank 0 x {ticks} ticks (same call sequence as the GPU run), find_path only, "
+                      f"1 thread (oracle/hastar_oracle.cpp)",
+            "tick_ms_one_core_per_pair": float(tick_max.mean()) if n else None}
 
 
-def cpu_baseline(cfgs, gpu_results, budget_s, replans):
-    """The oracle (CPU restatement, 'port') on the host: single thread, find_path only,
-    as the reference harness times it (test_hybrid_astar.cpp:123-126).  Each sampled query
-    replays the GPU planner's exact call sequence — the map drive, then `replans` x
-    (reset + find_path), warm-up and timed steps alike (the node map's f values persist
-    across reset, HybridAStar.cpp:49-52, so later replans differ from the first) — and
-    every replan is timed.  The last replan is compared with the GPU's last timed step."""
-    from oracle.pyoracle import OraclePlanner
+def cpu_baseline(cfgs, gpu_results, budget_s, replans, lat_ids):
+    """The oracle (CPU restatement, 'port') on `cpu_threads()` host threads, one private
+    planner per thread at a time (BASELINE.md "Plan for the CPU baseline"), find_path timed
+    only, as the reference harness times it (test_hybrid_astar.cpp:123-126).  Each sampled
+    query replays the GPU planner's exact call sequence — the map drive, then `replans` x
+    (reset + find_path), warm-up and timed steps alike (the node map's f values persist across
+    reset, HybridAStar.cpp:49-52, so later replans differ from the first).  Queries are taken
+    in the GPU batch's order, in chunks of 16 per thread, until the chunks' parallel wall time
+    reaches the budget.  value = pops / parallel wall (chunk tails included).  Each query's
+    last replan is compared with the GPU's last timed step (pop digest, success, cost bits)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle.pyoracle import OraclePlanner, run_batch_threads
     from tests.scenarios import drive
-    pops = 0
-    wall = 0.0
-    n = 0
-    plans = 0
-    parity = True
-    for i, (cfg, proto) in enumerate(cfgs):
-        o = OraclePlanner(cfg)
-        drive(o, proto)
-        for _ in range(replans):
-            o.reset()
-            r = o.find_path(proto["vel"], proto["start"])
-            pops += r["stats"]["pops"]
-            wall += r["wall_ms"] * 1e-3
-            plans += 1
-        n += 1
-        g = gpu_results.result(i)
-        parity &= (r["stats"]["pop_digest"] == g["stats"]["pop_digest"] and r["ok"] == g["ok"]
-                   and np.float32(r["cost"]).tobytes() == np.float32(g["cost"]).tobytes())
-        o.close()
-        if wall >= budget_s:
-            break
-    return {"value": pops / wall if wall > 0 else None, "unit": "expansions/s", "cores": 1, "kind": "port",
+    T = cpu_threads()
+    chunk = 16 * T
+    pops, wall, plans, plan_s = 0, 0.0, 0, 0.0
+    n, parity, lat = 0, True, []
+
+    def make(c):
+        o = OraclePlanner(c[0])
+        drive(o, c[1])
+        return o
+
+    with ThreadPoolExecutor(T) as ex:
+        while n < len(cfgs) and wall < budget_s:
+            sub = cfgs[n:n + chunk]
+            ors = list(ex.map(make, sub))
+            r = run_batch_threads(ors, [c[1]["vel"] for c in sub], [c[1]["start"] for c in sub], replans, T)
+            pops += r["pops"]
+            wall += r["wall_s"]
+            plans += r["plans"]
+            plan_s += r["plan_s_sum"]
+            for j in range(len(sub)):
+                g = gpu_results.result(n + j)
+                parity &= (int(r["digest"][j]) == g["stats"]["pop_digest"] and bool(r["ok"][j]) == g["ok"]
+                           and np.float32(r["cost"][j]).tobytes() == np.float32(g["cost"]).tobytes())
+                if n + j in lat_ids:
+                    lat.append(float(np.median(r["plan_ms"][j])))
+            for o in ors:
+                o.close()
+            n += len(sub)
+    return {"value": pops / wall if wall > 0 else None, "unit": "expansions/s", "cores": T, "kind": "port",
             "sample": f"first {n} queries of the GPU batch x {replans} replans each (same call sequence as the GPU "
-                      f"run), find_path only, 1 thread (oracle/hastar_oracle.cpp)",
-            "mean_plan_ms": wall / plans * 1e3 if plans else None, "parity_with_gpu": bool(parity)}
+                      f"run), find_path only, {T} threads with one private planner each (oracle/hastar_oracle.cpp, "
+                      f"-O3)",
+            "per_core_value": pops / plan_s if plan_s > 0 else None,
+            "mean_plan_ms": plan_s / plans * 1e3 if plans else None, "parity_with_gpu": bool(parity),
+            "latency_same_queries_ms": float(np.median(lat)) if lat else None}
 
 
 if __name__ == "__main__":

@@ -1291,7 +1291,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
 // pulls planner indices (in `order`, longest-expected-first when the host knows) from a
 // device counter until the queue is drained, so early finishers take the next planner.
 // resume = 1: wave b continues parked planner order[b] in arena b (no queue).
-__global__ __launch_bounds__(64, HASTAR_WAVES_PER_EU) void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HASTAR_WAVES_PER_EU))) void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners,
                                                            const SlotArena* __restrict__ arenas,
                                                            const int* __restrict__ order, int* __restrict__ next,
                                                            long long hard_pops, int n_prio, int iso, int resume) {

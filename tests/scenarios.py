@@ -31,10 +31,9 @@ def harness():
     return cfg, proto, g
 
 
-def synthetic(N, bins, K, seed, res=0.5, clear=8.0):
-    """SURVEY.md §8d synthetic case (harness vehicle parameters)."""
-    W = N * res
-    rng = np.random.default_rng(seed)
+def _synthetic_boxes_loop(W, K, rng, clear):
+    """The generator's definition, one candidate at a time (kept as the test's reference for
+    the vectorised draw below)."""
     boxes = []
     start = np.array([-0.6 * W, 0.0])
     goal = np.array([0.0, 0.0])
@@ -46,6 +45,34 @@ def synthetic(N, bins, K, seed, res=0.5, clear=8.0):
         if math.hypot(cx - start[0], cy - start[1]) < clear + r or math.hypot(cx - goal[0], cy - goal[1]) < clear + r:
             continue
         boxes.append([cx, cy, sx, sy])
+    return boxes
+
+
+def _synthetic_boxes(W, K, rng, clear):
+    """Vectorised draw of the same candidates: every candidate consumes 4 doubles of the
+    stream in the order (sx, sy, cx, cy) and numpy's uniform(a, b) is a + (b - a) * u, so
+    drawing blocks of candidates and keeping the first K accepted gives the loop's boxes."""
+    out = []
+    while len(out) < K:
+        u = rng.random((2 * K + 16, 4))
+        sx = 1.0 + (6.0 - 1.0) * u[:, 0]
+        sy = 1.0 + (6.0 - 1.0) * u[:, 1]
+        cx = -0.8 * W + (0.2 * W - -0.8 * W) * u[:, 2]
+        cy = -0.5 * W + (0.5 * W - -0.5 * W) * u[:, 3]
+        r = np.hypot(sx, sy) / 2
+        ok = ~((np.hypot(cx - (-0.6 * W), cy - 0.0) < clear + r) | (np.hypot(cx - 0.0, cy - 0.0) < clear + r))
+        for k in np.nonzero(ok)[0]:
+            out.append([cx[k], cy[k], sx[k], sy[k]])
+            if len(out) == K:
+                break
+    return out
+
+
+def synthetic(N, bins, K, seed, res=0.5, clear=8.0):
+    """SURVEY.md §8d synthetic case (harness vehicle parameters)."""
+    W = N * res
+    rng = np.random.default_rng(seed)
+    boxes = _synthetic_boxes(W, K, rng, clear)
     cfg = PlannerConfig(grid_size=N, num_angle_bins=bins, steering=steering_from_degrees([-30, -15, 0, 15, 30]))
     proto = dict(goal=[0.0, 0.0, 0.0], start=[float(-0.6 * W), 0.0, 0.0], vel=2.0, cycles=5,
                  lines=np.zeros((0, 4), np.float32), line_conf=0.6, line_width=1.25,

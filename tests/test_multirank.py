@@ -141,3 +141,35 @@ def test_two_rank_row_sharded_map_build():
         assert p.exitcode == 0
     for _, m, full in out:
         assert m == ref.map.tobytes() and full == ref.map.tobytes()
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus2_launcher_dry_run():
+    """`bench.py --gpus 2` without WORLD_SIZE starts two ranks itself (torch.distributed.run
+    as a child process) and rank 0 prints one JSON line with n_gpus = 2; --dry-run skips the
+    GPU work and --backend gloo runs the reductions on CPU (the driver's N > 1 path)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dry-run", "--backend", "gloo",
+                          "--batch", "5", "--steps", "2", "--warmup", "1"], capture_output=True, text=True,
+                         timeout=280, env=env, cwd=str(ROOT))
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["units_total"] == 10 and rec["steps"] == 2
+    # cfg5: 64 global pairs dealt over the ranks (strong scaling)
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dry-run", "--backend", "gloo",
+                          "--workload", "cfg5", "--pairs", "64"], capture_output=True, text=True, timeout=280,
+                         env=env, cwd=str(ROOT))
+    assert out.returncode == 0, out.stderr[-2000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["n_gpus"] == 2 and rec["config"]["units_total"] == 64 and rec["scaling"] == "strong"
+
+
+def test_global_pair_sharding():
+    sys.path.insert(0, str(ROOT))
+    import bench
+    parts = [bench.shard_global_ids(r, 8, 64) for r in range(8)]
+    assert sorted(sum(parts, [])) == list(range(64)) and all(len(p) == 8 for p in parts)

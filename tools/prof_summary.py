@@ -62,6 +62,42 @@ def pmc(args):
     print(json.dumps({k: out[k] for k in ("fetch_size_kib", "write_size_kib", "hbm_bytes_per_launch")}))
 
 
+def counters(args):
+    """Every counter of the given rocprofv3 --pmc pass directories, summed over the search
+    kernel's dispatch `--dispatch` (per-XCD / per-instance rows are added up)."""
+    out = {"kernel": KERNEL, "batch": args.batch, "grid": args.grid, "dispatch_index": args.dispatch, "counters": {}}
+    for d in args.dirs:
+        per = {}
+        for r in rows(d, "counter_collection.csv"):
+            if KERNEL not in r["Kernel_Name"]:
+                continue
+            key = int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0)
+            per.setdefault(r["Counter_Name"], {}).setdefault(key, 0.0)
+            per[r["Counter_Name"]][key] += float(r["Counter_Value"])
+        for name, vals in per.items():
+            ks = sorted(vals)
+            out["counters"][name] = vals[ks[args.dispatch]]
+    c = out["counters"]
+    der = {}
+    if c.get("SQ_WAVE_CYCLES"):
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
+            if k in c:
+                der[k.lower() + "_frac_of_wave_cycles"] = c[k] / c["SQ_WAVE_CYCLES"]
+    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c and c["TCC_HIT_sum"] + c["TCC_MISS_sum"] > 0:
+        der["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    if c.get("SQ_WAVES") and c.get("SQ_WAVE_CYCLES"):
+        der["mean_wave_lifetime_cycles"] = 4.0 * c["SQ_WAVE_CYCLES"] / c["SQ_WAVES"]  # quad-cycles -> cycles
+    insts = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD",
+                                        "SQ_INSTS_VMEM_WR", "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH"))
+    if insts:
+        der["insts_counted"] = insts
+    out["derived"] = der
+    out["note"] = ("SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles (MI355X_MICROARCH.md); "
+                   "WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES")
+    Path(args.out).write_text(json.dumps(out, indent=1))
+    print(json.dumps(der))
+
+
 ap = argparse.ArgumentParser()
 sub = ap.add_subparsers(dest="cmd", required=True)
 t = sub.add_parser("trace")
@@ -76,5 +112,11 @@ p.add_argument("out")
 p.add_argument("--batch", type=int, required=True)
 p.add_argument("--grid", type=int, default=1024)
 p.add_argument("--dispatch", type=int, default=-1)
+c = sub.add_parser("counters")
+c.add_argument("out")
+c.add_argument("dirs", nargs="+")
+c.add_argument("--batch", type=int, required=True)
+c.add_argument("--grid", type=int, default=1024)
+c.add_argument("--dispatch", type=int, default=1)
 a = ap.parse_args()
-trace(a) if a.cmd == "trace" else pmc(a)
+{"trace": trace, "pmc": pmc, "counters": counters}[a.cmd](a)
