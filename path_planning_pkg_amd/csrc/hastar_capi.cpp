@@ -30,6 +30,7 @@
 
 #include "../../include/hastar.h"
 #include "../../include/hastar_test.h"
+#include "../../include/hastar_units.h"
 #include "glibc_mathf.h"
 #include "hastar_kernels.h"
 #include "hastar_layout.h"
@@ -1662,6 +1663,124 @@ int hastar_velocity_profile_last_batch(int device, const hastar_velocity_params*
   HIPCHK(hipMemcpyAsync(feasible, d_feas, n, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   return HASTAR_OK;
+}
+
+// ------------------------------------------- AStar<float> / Grid2D<float> on a handle ---
+// The reference's AStar class owns a plain Grid2D (AStar.h:63-66 without
+// STORE_GRID_AS_REFERENCE): its goal change only re-orients the frame (no relocation,
+// Grid2D.cpp:260-266) and its start cell truncates the rotated offset before adding the
+// goal cell (Grid2D.cpp:270-290).  These entry points give a planner handle those
+// semantics; map updates, reset and get_obstacles are the planner's own.
+int hastar_grid2d_update_goal_heading(hastar_handle h, const float goal[2], const float start[2]) {
+  if (!h || !goal || !start) return fail(HASTAR_EINVAL, "null argument");
+  h->goal2x = goal[0];
+  h->goal2y = goal[1];
+  h->grid_heading = g_atan2f(goal[1] - start[1], goal[0] - start[0]);
+  PlannerDev& D = h->desc;
+  D.goal_cx = D.n45;
+  D.goal_cy = D.n2;
+  D.grid_heading = h->grid_heading;
+  h->goal_set = true;
+  return HASTAR_OK;
+}
+
+static float euclid_h_host(const PlannerDev& P, int i, int j) {  // Grid2D.cpp:303-316, as euclid_h
+  const float dx = (float)(P.n45 - i) * P.res;
+  const float dx2 = dx * dx;
+  const float dy = (float)(P.n2 - j) * P.res;
+  const float dy2 = dy * dy;
+  return std::sqrt(dx2 + dy2);
+}
+
+// Node2D::soft_reset of cell (i, j) (Grid2D.cpp:294-299): its f becomes its h
+int hastar_grid2d_set_start_node_grid(hastar_handle h, int i, int j) {
+  if (!h) return fail(HASTAR_EINVAL, "null handle");
+  const PlannerDev& D = h->desc;
+  if (i < 0 || i >= D.N || j < 0 || j >= D.N) return fail(HASTAR_EINVAL, "cell outside the grid");
+  HIPCHK(hipSetDevice(h->device));
+  const float f = euclid_h_host(D, i, j);
+  HIPCHK(hipMemcpyAsync(D.nm_f + (size_t)i * D.N + j, &f, sizeof(float), hipMemcpyHostToDevice, h->dc->stream));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
+  return HASTAR_OK;
+}
+
+// Grid2D::set_start_node(start) (Grid2D.cpp:270-290): cell[0..1] = the start cell
+int hastar_grid2d_set_start_node(hastar_handle h, const float start[2], int cell[2]) {
+  if (!h || !start || !cell) return fail(HASTAR_EINVAL, "null argument");
+  const PlannerDev& D = h->desc;
+  const float gh = h->grid_heading, c = g_cosf(gh), s = g_sinf(gh);
+  const float dx = start[0] - h->goal2x, dy = start[1] - h->goal2y;
+  const float rx = dx * c + dy * s, ry = -dx * s + dy * c;
+  int i = gmath::x86_trunc_int(rx / D.res) + D.n45, j = gmath::x86_trunc_int(ry / D.res) + D.n2;
+  if (!(i > -1 && i < D.N && j > -1 && j < D.N)) i = j = 0;
+  cell[0] = i;
+  cell[1] = j;
+  return hastar_grid2d_set_start_node_grid(h, i, j);
+}
+
+// Grid2D::get_node_total_cost (Grid2D.cpp:229-233)
+int hastar_grid2d_node_cost(hastar_handle h, int i, int j, float* f) {
+  if (!h || !f) return fail(HASTAR_EINVAL, "null argument");
+  const PlannerDev& D = h->desc;
+  if (i < 0 || i >= D.N || j < 0 || j >= D.N) return fail(HASTAR_EINVAL, "cell outside the grid");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemcpyAsync(f, D.nm_f + (size_t)i * D.N + j, sizeof(float), hipMemcpyDeviceToHost, h->dc->stream));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
+  return HASTAR_OK;
+}
+
+// One holonomic search on the device (k_astar_query).  mode: 1 memo test of the start,
+// 2 get_cost_only, 4 path (cap points of xy, world frame, goal's predecessor first).
+static int astar_run(hastar_handle h, int si, int sj, int mode, const float goal_w[2], float* cost, float* xy, int cap,
+                     int* n) {
+  const PlannerDev& D = h->desc;
+  if (si < 0 || si >= D.N || sj < 0 || sj >= D.N) return fail(HASTAR_EINVAL, "cell outside the grid");
+  if (!h->goal_set) return fail(HASTAR_EINVAL, "update_goal / update_goal_start must come first");
+  HIPCHK(hipSetDevice(h->device));
+  DeviceCtx& DC = *h->dc;
+  std::lock_guard<std::mutex> lk(DC.mu);
+  if (int rc = arenas_acquire(DC, h->areq, 1)) return rc;
+  const int pcap = std::max(cap, 1);
+  const size_t bytes = align256(sizeof(PlannerDev)) + 256 + align256((size_t)pcap * 2 * sizeof(float)) + 256;
+  if (int rc = stage_acquire(DC, bytes)) return rc;
+  char* q = DC.stage;
+  PlannerDev* d_desc = reinterpret_cast<PlannerDev*>(q);
+  float* d_cost = reinterpret_cast<float*>(q + align256(sizeof(PlannerDev)));
+  int* d_n = reinterpret_cast<int*>(q + align256(sizeof(PlannerDev)) + 16);
+  float* d_xy = reinterpret_cast<float*>(q + align256(sizeof(PlannerDev)) + 256);
+  HIPCHK(hipMemcpyAsync(d_desc, &D, sizeof(PlannerDev), hipMemcpyHostToDevice, DC.stream));
+  const float ang = -h->grid_heading;
+  HIPCHK(launch_astar_query(d_desc, DC.d_arenas, si, sj, mode, goal_w ? goal_w[0] : 0.0f, goal_w ? goal_w[1] : 0.0f,
+                            g_cosf(ang), g_sinf(ang), d_cost, d_xy, cap, d_n, DC.stream));
+  int nn = 0;
+  HIPCHK(hipMemcpyAsync(cost, d_cost, sizeof(float), hipMemcpyDeviceToHost, DC.stream));
+  HIPCHK(hipMemcpyAsync(&nn, d_n, sizeof(int), hipMemcpyDeviceToHost, DC.stream));
+  HIPCHK(hipStreamSynchronize(DC.stream));
+  if (nn == -2) return fail(HASTAR_EOVERFLOW, "holonomic search outgrew its open-set arena (max_astar_nodes)");
+  if (n) *n = nn;
+  if (nn == -1) return fail(HASTAR_ENOSPC, "path buffer too small");
+  if (nn > 0 && xy) HIPCHK(hipMemcpy(xy, d_xy, (size_t)nn * 2 * sizeof(float), hipMemcpyDeviceToHost));
+  return HASTAR_OK;
+}
+
+// AStar::find_path(int, int) (AStar.cpp:100-113): memo test, then a cost-only search
+int hastar_astar_cost(hastar_handle h, int i, int j, float* cost) {
+  if (!h || !cost) return fail(HASTAR_EINVAL, "null argument");
+  return astar_run(h, i, j, 1 | 2, nullptr, cost, nullptr, 0, nullptr);
+}
+
+// AStar::find_path(goal, start, get_cost_only) and find_path(goal, start, path)
+// (AStar.cpp:70-97): re-orient the frame (no relocation), soft-reset the start cell, search.
+// With path != NULL (cap points), *n points of the predecessor chain follow the goal (the
+// reference's path = goal, then these).
+int hastar_astar_find_path(hastar_handle h, const float goal[2], const float start[2], int cost_only, float* cost,
+                           float* xy, int cap, int* n) {
+  if (!h || !goal || !start || !cost) return fail(HASTAR_EINVAL, "null argument");
+  if (int rc = hastar_grid2d_update_goal_heading(h, goal, start)) return rc;
+  int cell[2];
+  if (int rc = hastar_grid2d_set_start_node(h, start, cell)) return rc;
+  const int mode = cost_only ? 2 : (xy ? 4 : 0);
+  return astar_run(h, cell[0], cell[1], mode, goal, cost, xy, cap, n);
 }
 
 // ---------------------------------------------------------------- test hooks --------

@@ -9,6 +9,9 @@ hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_ar
 hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, const int* d_order,
                          long long hard_pops, hipStream_t st);
 int search_slots_per_cu();
+hipError_t launch_astar_query(const PlannerDev* d_desc, const SlotArena* d_arena, int si, int sj, int mode, float gwx,
+                              float gwy, float rc, float rs, float* out_cost, float* xy, int cap, int* out_n,
+                              hipStream_t st);
 hipError_t launch_gather_paths(const PlannerDev* d_descs, const long long* d_off, const int* d_len, int n, float* xyh,
                                float* curv, hipStream_t st);
 hipError_t launch_init_nodemap(const PlannerDev& P, hipStream_t st);

@@ -55,6 +55,7 @@ struct SearchCtx {
   uint32_t gen3, gen2;
   long long pops, succ, apops, asearch, shots, amigr, apops_g;
   int status;
+  bool cost_only;   // AStar::a_star_search(get_cost_only): memo exits + memoise (always, inside the search)
 #ifdef HASTAR_STAMPS
   unsigned long long cyc[NSTAMP];
 #endif
@@ -500,11 +501,11 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     if (G) c.apops_g++;
     if (tx == P.goal_cx && ty == P.goal_cy) {
       const float fgoal = g0 + euclid_h(P, tx, ty);  // the record's f (Node2D: f = g + h)
-      memoise(c, fgoal, ci);
+      if (c.cost_only) memoise(c, fgoal, ci);
       *result = fgoal;
       return true;
     }
-    const uint64_t vmask = __ballot(valid), vismask = __ballot(vis), cmask = __ballot(closed);
+    const uint64_t vmask = __ballot(valid), vismask = c.cost_only ? __ballot(vis) : 0ull, cmask = __ballot(closed);
     if (!G) STAMP_ADD(8, t_pop);
     for (int k = 0; k < nact; ++k) {
       if (!((vmask >> k) & 1ull)) continue;
@@ -624,7 +625,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     }
     // consume every probe before the first store of this pop, so that no later register
     // reuse has to wait on a store (vmcnt counts loads and stores in issue order)
-    const uint64_t vmask = __ballot(valid), vismask = __ballot(vis), cmask = __ballot(closed);
+    const uint64_t vmask = __ballot(valid), vismask = c.cost_only ? __ballot(vis) : 0ull, cmask = __ballot(closed);
     nf = __builtin_amdgcn_readfirstlane(0) + nf;  // keep nf live in a VGPR (no-op)
     tr.unlink(b);
     free_lds(c, tr, b);
@@ -645,7 +646,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     c.apops++;
     if (tx == P.goal_cx && ty == P.goal_cy) {
       const float fgoal = g0 + euclid_h(P, tx, ty);  // the record's f (Node2D: f = g + h)
-      memoise(c, fgoal, ci);
+      if (c.cost_only) memoise(c, fgoal, ci);
       *result = fgoal;
       return true;
     }
@@ -758,13 +759,14 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
   return true;
 }
 
-// AStar::find_path(int, int) (AStar.cpp:100-113)
-__device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, int sj) {
+// AStar::find_path(int, int) (AStar.cpp:100-113); check_start = false: a_star_search from
+// the soft-reset start node without the memo test of the start (AStar.cpp:88-95)
+__device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, int sj, bool check_start = true) {
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
   const size_t s_cell = (size_t)si * P.N + sj;
-  if ((gp(P.visited)[s_cell >> 5] >> (s_cell & 31)) & 1u) return gp(P.nm_f)[s_cell];
+  if (check_start && ((gp(P.visited)[s_cell >> 5] >> (s_cell & 31)) & 1u)) return gp(P.nm_f)[s_cell];
   const float h0 = euclid_h(P, si, sj);
   gp(P.nm_f)[s_cell] = h0;  // Grid2D::set_start_node_grid -> Node2D::soft_reset
   c.asearch++;
@@ -1301,6 +1303,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HASTAR_WAVES
   c.A = arenas + blockIdx.x;
   const SlotArena& A = *c.A;
   c.lane = threadIdx.x;
+  c.cost_only = true;
   c.gen3 = gp(A.gens)[0];
   c.gen2 = gp(A.gens)[1];
   if (resume) {
@@ -1358,6 +1361,62 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HASTAR_WAVES
     gp(A.gens)[0] = c.gen3;
     gp(A.gens)[1] = c.gen2;
   }
+}
+
+// ------------------------------------------------- AStar<float> on its own (AStar.h) --
+// The holonomic search of planner *P outside a Hybrid A* search (the reference's AStar
+// class, used by utils/astar/test_astar.cpp): mode bit 0 = memo test of the start
+// (find_path(int, int), AStar.cpp:100-113), bit 1 = get_cost_only (memo exits and the
+// memo write-back), bit 2 = return the closed-record chain from the goal's predecessor
+// (reconstruct_path, AStar.cpp:189-205), as world coordinates: the goal's predecessor
+// first, each ((x - gx) * res, (y - gy) * res) rotated by -heading plus the goal position.
+__global__ __launch_bounds__(64) void k_astar_query(const PlannerDev* __restrict__ P, const SlotArena* __restrict__ arena,
+                                                    int si, int sj, int mode, float gwx, float gwy, float rc, float rs,
+                                                    float* out_cost, float* xy, int cap, int* out_n) {
+  __shared__ AStarLds alds;
+  SearchCtx c;
+  c.P = P;
+  c.A = arena;
+  c.lane = threadIdx.x;
+  c.cost_only = (mode & 2) != 0;
+  c.gen2 = gp(arena->gens)[1];
+  c.asearch = c.apops = c.amigr = c.apops_g = 0;
+  c.status = 0;
+  const float r = holonomic(c, alds, si, sj, (mode & 1) != 0);
+  int n = 0;
+  if ((mode & 4) && r < FLT_MAX && c.status == 0) {
+    const PlannerDev& Pd = *P;
+    const GAS Cell2* cells = gp(arena->cell2);
+    const int goal = Pd.goal_cx * Pd.N + Pd.goal_cy;
+    // the predecessor chain of the goal's closed record (cell indices)
+    int cur = cells[goal].prev;
+    while (cur != NIL) {
+      if (n >= cap) {
+        n = -1;
+        break;
+      }
+      if (c.lane == 0) {
+        const int dx = cur / Pd.N - Pd.goal_cx, dy = cur % Pd.N - Pd.goal_cy;
+        const float x = (float)dx * Pd.res, y = (float)dy * Pd.res;
+        xy[2 * n] = x * rc + y * rs + gwx;
+        xy[2 * n + 1] = -x * rs + y * rc + gwy;
+      }
+      ++n;
+      cur = cells[cur].prev;
+    }
+  }
+  if (c.lane == 0) {
+    *out_cost = c.status == 0 ? r : FLT_MAX;
+    *out_n = c.status == 0 ? n : -2;
+    gp(arena->gens)[1] = c.gen2;
+  }
+}
+hipError_t launch_astar_query(const PlannerDev* d_desc, const SlotArena* d_arena, int si, int sj, int mode, float gwx,
+                              float gwy, float rc, float rs, float* out_cost, float* xy, int cap, int* out_n,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(k_astar_query, dim3(1), dim3(64), 0, st, d_desc, d_arena, si, sj, mode, gwx, gwy, rc, rs, out_cost,
+                     xy, cap, out_n);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ map kernels -------

@@ -18,10 +18,17 @@ python3 tools/prof_summary.py trace $R/trace $OUT/trace_summary.json --warmup 1 
 find $R/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 B=$(python3 -c "import json;print(json.load(open('$OUT/bench.json'))['config']['queries_per_gpu'])")
 ARGS="--steps 1 --warmup 1 --no-cpu-baseline --latency-queries 0"
-pass() {  # pass <name> <counters...>
+timeout -s KILL 120 rocprofv3 -L > $OUT/avail_counters.txt 2>&1 || true
+pass() {  # pass <name> <counters...>: counters this device does not list are dropped
   local name=$1; shift
-  echo "pmc pass $name: $*"
-  timeout -s KILL 400 rocprofv3 --pmc "$@" --output-format csv --kernel-include-regex hastar_search_kernel -d $R/$name -o pmc -- python3 bench.py $ARGS > $OUT/pmc_$name.log 2>&1 || { tail -5 $OUT/pmc_$name.log; exit 1; }
+  local use=()
+  for c in "$@"; do
+    base=${c%_sum}
+    if grep -qw "$base" $OUT/avail_counters.txt; then use+=("$c"); else echo "  (counter $c not listed: skipped)"; fi
+  done
+  [ ${#use[@]} -eq 0 ] && return 0
+  echo "pmc pass $name: ${use[*]}"
+  timeout -s KILL 400 rocprofv3 --pmc "${use[@]}" --output-format csv --kernel-include-regex hastar_search_kernel -d $R/$name -o pmc -- python3 bench.py $ARGS > $OUT/pmc_$name.log 2>&1 || { tail -5 $OUT/pmc_$name.log; exit 1; }
 }
 pass FETCH FETCH_SIZE
 pass WRITE WRITE_SIZE
