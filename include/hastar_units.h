@@ -17,6 +17,9 @@
 extern "C" {
 #endif
 
+/* Last error message of the unit calls of this thread (static storage). */
+const char* hastar_units_last_error(void);
+
 /* Node3D<T> fields the vehicle model reads / writes (Node3D.h:17-24) */
 typedef struct hastar_node3_f32 {
   float x, y, heading, g, vmin_sqr;
@@ -83,6 +86,8 @@ int hastar_grid2d_update_goal_heading(hastar_handle h, const float goal[2], cons
 int hastar_grid2d_set_start_node(hastar_handle h, const float start[2], int cell[2]);
 /* Grid2D::set_start_node_grid(i, j) (Grid2D.cpp:294-299) */
 int hastar_grid2d_set_start_node_grid(hastar_handle h, int i, int j);
+/* AStar::update_goal_node(goal_node) (AStar.cpp:24-28): the goal cell of later searches */
+int hastar_astar_set_goal_cell(hastar_handle h, int i, int j);
 /* Grid2D::get_node_total_cost(i, j) (Grid2D.cpp:229-233): the node map's f (memo / stale) */
 int hastar_grid2d_node_cost(hastar_handle h, int i, int j, float* f);
 /* AStar::find_path(i, j) (AStar.cpp:100-113): memoised cost-to-goal of cell (i, j) */

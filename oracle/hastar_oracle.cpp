@@ -492,6 +492,29 @@ template <class T> struct Planner {
     astar_goal = {n45, n2, 0, nm_f[(size_t)n45 * N + n2], nullptr};
   }
   void reset() { std::fill(visited.begin(), visited.end(), 0); }
+  // ---- the stand-alone AStar's plain Grid2D (AStar.h without STORE_GRID_AS_REFERENCE) ----
+  // Grid2D::update_goal_heading (Grid2D.cpp:260-266): no relocation
+  void goal_2d(const P2<T>& g, const P2<T>& s) {
+    goal2 = g;
+    grid_heading = std::atan2(g.y - s.y, g.x - s.x);
+    astar_goal = {n45, n2, 0, nm_f[(size_t)n45 * N + n2], nullptr};
+  }
+  // Grid2D::set_start_node (Grid2D.cpp:270-290)
+  std::pair<int, int> start_2d(const P2<T>& s) {
+    P2<T> rel = rot2<T>(s.x - goal2.x, s.y - goal2.y, grid_heading);
+    int i = static_cast<int>(rel.x / res) + n45, j = static_cast<int>(rel.y / res) + n2;
+    if (!inside(i, j)) i = j = 0;
+    nm_f[(size_t)i * N + j] = nm_h[(size_t)i * N + j];
+    return {i, j};
+  }
+  // AStar::reconstruct_path (AStar.cpp:189-205): world points of the goal's predecessors
+  void path_2d(const P2<T>& goal, std::vector<P2<T>>& out) const {
+    for (const N2<T>* p = astar_goal.prev; p; p = p->prev) {
+      P2<T> rel{(p->x - astar_goal.x) * res, (p->y - astar_goal.y) * res};
+      P2<T> w = rot2<T>(rel.x, rel.y, -grid_heading);
+      out.push_back({w.x + goal.x, w.y + goal.y});
+    }
+  }
 
 #ifdef ORC_SHAPE_STATS
   // Analysis build only (tools/astar_shape_stats.py): how often the open tree's shape can
@@ -528,6 +551,10 @@ template <class T> struct Planner {
   // AStar::find_path(int, int) (AStar.cpp:100-113) + a_star_search (118-186)
   T holonomic(int si, int sj) {
     if (visited[(size_t)si * N + sj]) return nm_f[(size_t)si * N + sj];
+    return a_star(si, sj, true);
+  }
+  // AStar::a_star_search(start, get_cost_only) (AStar.cpp:118-186) from the soft-reset start
+  T a_star(int si, int sj, bool cost_only) {
     nm_f[(size_t)si * N + sj] = nm_h[(size_t)si * N + sj];  // Node2D::soft_reset
     st.astar_searches++;
     cl2.clear();
@@ -543,7 +570,7 @@ template <class T> struct Planner {
       st.astar_pops++;
       if (cur->x == astar_goal.x && cur->y == astar_goal.y) {
         astar_goal = *cur;
-        memoise(astar_goal.f, &astar_goal);
+        if (cost_only) memoise(astar_goal.f, &astar_goal);
         return astar_goal.f;
       }
       const T g0 = cur->g;
@@ -551,7 +578,7 @@ template <class T> struct Planner {
         int i = cur->x + act_dx[k], j = cur->y + act_dy[k];
         if (!inside(i, j) || !(occ[(size_t)i * N + j] < thr)) continue;  // Grid2D::get_neighbors
         const size_t c = (size_t)i * N + j;
-        if (visited[c]) {
+        if (cost_only && visited[c]) {
           T tot = nm_f[c] + g0 + act_cost[k];
           memoise(tot, cur);
           return tot;
@@ -1014,6 +1041,65 @@ extern "C" void orc_libm(int fn, const float* a, const float* b, float* out, int
 }
 
 extern "C" void orc_set_max_pops(long long n) { orc::g_max_pops = n; }
+
+// The stand-alone AStar<float> (utils/astar/test_astar.cpp) on a planner's plain Grid2D.
+extern "C" void orc_grid2d_goal(void* h, const float g[2], const float s[2]) {
+  static_cast<OP*>(h)->goal_2d({g[0], g[1]}, {s[0], s[1]});
+}
+extern "C" void orc_grid2d_start(void* h, const float s[2], int cell[2]) {
+  auto c = static_cast<OP*>(h)->start_2d({s[0], s[1]});
+  cell[0] = c.first;
+  cell[1] = c.second;
+}
+extern "C" float orc_astar_cost(void* h, int i, int j) { return static_cast<OP*>(h)->holonomic(i, j); }
+// AStar::find_path(goal, start, path / cost_only): returns the cost; *n path points after the goal
+extern "C" float orc_astar_find_path(void* h, const float g[2], const float s[2], int cost_only, float* xy, int cap,
+                                     int* n) {
+  auto* P = static_cast<OP*>(h);
+  P->goal_2d({g[0], g[1]}, {s[0], s[1]});
+  auto c = P->start_2d({s[0], s[1]});
+  const float cost = P->a_star(c.first, c.second, cost_only != 0);
+  std::vector<orc::P2<float>> pts;
+  if (!cost_only && cost < std::numeric_limits<float>::max()) P->path_2d({g[0], g[1]}, pts);
+  *n = (int)pts.size();
+  for (int k = 0; k < (int)pts.size() && k < cap; ++k) {
+    xy[2 * k] = pts[k].x;
+    xy[2 * k + 1] = pts[k].y;
+  }
+  return cost;
+}
+// VehicleModel<float>::simulate_action over an action list from the harness start node
+extern "C" int orc_vehicle_chain_f(float ts, float a_lat, float wheelbase, float rear_to_cg, int bins, int na,
+                                   const float* steer, const float* w, int nsteer, float vmin0, const int* actions,
+                                   int nact, float* xy_out) {
+  std::vector<float> sv(steer, steer + nsteer), wv(w, w + nsteer);
+  orc::Motion<float> m(ts, a_lat, wheelbase, rear_to_cg, bins, na, sv, wv);
+  float x = 0, y = 0, h = 0, vmin = vmin0;
+  int bin = orc::heading_bin<float>(0.0f, (float)(5.0 * M_PI / 180.0));
+  xy_out[0] = x;
+  xy_out[1] = y;
+  int n = 1;
+  for (int k = 0; k < nact; ++k) {
+    int a = actions[k];
+    float vm = 0;
+    if (vmin > 1.0) {
+      float lat = vmin * m.curv_abs[a];
+      if (lat > m.a_lat) break;
+      float al = std::sqrt(1.0 - ((lat * lat) / m.a_lat2));
+      vm = vmin - 2 * al * m.ts;
+    }
+    const auto& o = m.offset(a, bin);
+    x = x + o.x;
+    y = y + o.y;
+    h = orc::wrap_pi<float>(h + m.dth[a]);
+    bin = orc::heading_bin<float>(h, m.prec);
+    vmin = vm;
+    xy_out[2 * n] = x;
+    xy_out[2 * n + 1] = y;
+    ++n;
+  }
+  return n;
+}
 
 // CPU baseline (bench.py cpu_baseline): `threads` std::threads, each taking whole planners
 // from a shared counter (one private planner per thread at a time, as BASELINE.md's plan

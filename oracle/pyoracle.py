@@ -55,6 +55,14 @@ def lib():
         L.orc_libm.argtypes = [C.c_int, fp, fp, fp, C.c_int]
         L.orc_velocity_profile.argtypes = [fp, C.c_float, C.c_float, fp, fp, C.c_int, C.c_int, C.c_int, fp]
         L.orc_set_max_pops.argtypes = [C.c_longlong]
+        L.orc_grid2d_goal.argtypes = [vp, fp, fp]
+        L.orc_grid2d_start.argtypes = [vp, fp, ip]
+        L.orc_astar_cost.restype = C.c_float
+        L.orc_astar_cost.argtypes = [vp, C.c_int, C.c_int]
+        L.orc_astar_find_path.restype = C.c_float
+        L.orc_astar_find_path.argtypes = [vp, fp, fp, C.c_int, fp, C.c_int, ip]
+        L.orc_vehicle_chain_f.argtypes = [C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, fp, fp,
+                                          C.c_int, C.c_float, ip, C.c_int, fp]
         L.orc_run_batch_threads.argtypes = [C.POINTER(C.c_void_p), C.c_int, fp, fp, C.c_int, C.c_int, dp, dp,
                                             C.POINTER(C.c_ulonglong), fp, ip]
         _lib = L
@@ -135,6 +143,24 @@ class OraclePlanner:
         n = ln.value
         return dict(cost=cost.value, ok=bool(ok.value), path=xyh[:n].copy(), curvature=curv[:n].copy(),
                     stats=st.as_dict(), wall_ms=wall.value)
+
+    # ---- the stand-alone AStar<float> on this planner's plain Grid2D (AStar.h)
+    def astar_goal_start(self, goal, start):
+        """AStar::update_goal_start: re-orient (no relocation), soft-reset the start cell."""
+        lib().orc_grid2d_goal(self.h, fptr(_f32(goal)), fptr(_f32(start)))
+        cell = np.zeros(2, np.int32)
+        lib().orc_grid2d_start(self.h, fptr(_f32(start)), iptr(cell))
+        return int(cell[0]), int(cell[1])
+
+    def astar_cost(self, i, j):
+        return lib().orc_astar_cost(self.h, int(i), int(j))
+
+    def astar_find_path(self, goal, start, cost_only=False, cap=1 << 14):
+        xy = np.zeros((cap, 2), np.float32)
+        n = C.c_int(0)
+        c = lib().orc_astar_find_path(self.h, fptr(_f32(goal)), fptr(_f32(start)), int(bool(cost_only)), fptr(xy), cap,
+                                      C.byref(n))
+        return c, xy[:n.value].copy()
 
     def closed_keys(self, cap=1 << 20):
         out = np.empty((cap, 3), np.int32)
@@ -229,6 +255,16 @@ def run_batch_threads(planners, vels, starts, replans, threads):
                                 iptr(ok))
     return dict(pops=int(out[0]), wall_s=float(out[1]), plan_s_sum=float(out[2]), plans=int(out[3]), plan_ms=per,
                 digest=dig, cost=cost, ok=ok.astype(bool))
+
+
+def vehicle_chain_f(ts, a_lat, wheelbase, rear_to_cg, bins, na, steering, weights, vmin0, actions):
+    st = _f32(steering)
+    w = _f32(weights)
+    acts = np.ascontiguousarray(actions, np.int32)
+    out = np.empty((len(acts) + 1, 2), np.float32)
+    n = lib().orc_vehicle_chain_f(ts, a_lat, wheelbase, rear_to_cg, bins, na, fptr(st), fptr(w), len(st), vmin0,
+                                  iptr(acts), len(acts), fptr(out))
+    return out[:n].copy()
 
 
 def velocity_profile(params, vel_init, max_velocity_curr, xyh, curv, coast_to_goal, stop_at_goal=False):

@@ -1718,6 +1718,15 @@ int hastar_grid2d_set_start_node(hastar_handle h, const float start[2], int cell
   return hastar_grid2d_set_start_node_grid(h, i, j);
 }
 
+// AStar::update_goal_node (AStar.cpp:24-28): searches end at this cell
+int hastar_astar_set_goal_cell(hastar_handle h, int i, int j) {
+  if (!h) return fail(HASTAR_EINVAL, "null handle");
+  if (i < 0 || i >= h->desc.N || j < 0 || j >= h->desc.N) return fail(HASTAR_EINVAL, "cell outside the grid");
+  h->desc.goal_cx = i;
+  h->desc.goal_cy = j;
+  return HASTAR_OK;
+}
+
 // Grid2D::get_node_total_cost (Grid2D.cpp:229-233)
 int hastar_grid2d_node_cost(hastar_handle h, int i, int j, float* f) {
   if (!h || !f) return fail(HASTAR_EINVAL, "null argument");
