@@ -98,6 +98,23 @@ int hastar_astar_cost(hastar_handle h, int i, int j, float* cost);
 int hastar_astar_find_path(hastar_handle h, const float goal[2], const float start[2], int cost_only, float* cost,
                            float* xy, int cap, int* n);
 
+/* Grid2D::clear_obstacles() (Grid2D.cpp:66-71) */
+int hastar_grid2d_clear(hastar_handle h);
+
+/* ---- Grid3D<float> (Grid3D.h:14-46) on a planner handle: the map, goal frame, APF list
+ * and motion tables are the planner's (hastar_update_goal = update_goal_heading with the
+ * relocation, hastar_update_boxes / _lines / hastar_decay = update_obstacles) ---- */
+/* Grid3D::set_start_node(start) (Grid3D.cpp:127-160): the node and its cell (soft-reset) */
+int hastar_grid3d_set_start_node(hastar_handle h, const float start[3], hastar_node3_f32* node, int cell[2]);
+/* the goal node Grid3D::update_goal_heading returned at the last hastar_update_goal */
+int hastar_grid3d_goal_node(hastar_handle h, hastar_node3_f32* node);
+/* Grid3D::get_neighbors(node, neighbors) (Grid3D.cpp:47-74): successors inside the grid and
+ * below the threshold, with the APF field added to g; cells = their (i, j). */
+int hastar_grid3d_neighbors(hastar_handle h, const hastar_node3_f32* node, int cap, hastar_node3_f32* out, int* cells,
+                            int* count, int* neglect);
+/* Grid3D::check_path(path) (Grid3D.cpp:78-93) over n poses (n x 3) */
+int hastar_grid3d_check_path(hastar_handle h, const float* xyh, int n, int* is_free);
+
 #ifdef __cplusplus
 }
 #endif

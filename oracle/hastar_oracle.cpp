@@ -1068,6 +1068,40 @@ extern "C" float orc_astar_find_path(void* h, const float g[2], const float s[2]
   }
   return cost;
 }
+// Grid3D::get_neighbors (Grid3D.cpp:47-74) of one node: out n x {x, y, h, g, vmin, ci, bin}
+// (ci / bin as float-encoded ints), cells n x 2; returns the count, *neglect the flag
+extern "C" int orc_grid3d_neighbors(void* h, const float nd[5], int ci, int bin, float* out, int* cells, int cap,
+                                    int* neglect) {
+  auto* P = static_cast<OP*>(h);
+  orc::N3<float> n{};
+  n.pose = {nd[0], nd[1], nd[2]};
+  n.g = nd[3];
+  n.vmin = nd[4];
+  n.ci = ci;
+  n.bin = bin;
+  std::vector<orc::N3<float>> nb;
+  *neglect = P->expand(n, nb) ? 1 : 0;
+  for (int k = 0; k < (int)nb.size() && k < cap; ++k) {
+    float* o = out + 7 * k;
+    o[0] = nb[k].pose.x;
+    o[1] = nb[k].pose.y;
+    o[2] = nb[k].pose.h;
+    o[3] = nb[k].g;
+    o[4] = nb[k].vmin;
+    std::memcpy(&o[5], &nb[k].ci, 4);
+    std::memcpy(&o[6], &nb[k].bin, 4);
+    cells[2 * k] = nb[k].cx;
+    cells[2 * k + 1] = nb[k].cy;
+  }
+  return (int)nb.size();
+}
+// Grid3D::check_path (Grid3D.cpp:78-93)
+extern "C" int orc_check_path(void* h, const float* xyh, int n) {
+  std::vector<orc::P3<float>> p(n);
+  for (int k = 0; k < n; ++k) p[k] = {xyh[3 * k], xyh[3 * k + 1], xyh[3 * k + 2]};
+  return static_cast<OP*>(h)->free_path(p) ? 1 : 0;
+}
+
 // VehicleModel<float>::simulate_action over an action list from the harness start node
 extern "C" int orc_vehicle_chain_f(float ts, float a_lat, float wheelbase, float rear_to_cg, int bins, int na,
                                    const float* steer, const float* w, int nsteer, float vmin0, const int* actions,

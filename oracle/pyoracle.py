@@ -61,6 +61,8 @@ def lib():
         L.orc_astar_cost.argtypes = [vp, C.c_int, C.c_int]
         L.orc_astar_find_path.restype = C.c_float
         L.orc_astar_find_path.argtypes = [vp, fp, fp, C.c_int, fp, C.c_int, ip]
+        L.orc_grid3d_neighbors.argtypes = [vp, fp, C.c_int, C.c_int, fp, ip, C.c_int, ip]
+        L.orc_check_path.argtypes = [vp, fp, C.c_int]
         L.orc_vehicle_chain_f.argtypes = [C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, fp, fp,
                                           C.c_int, C.c_float, ip, C.c_int, fp]
         L.orc_run_batch_threads.argtypes = [C.POINTER(C.c_void_p), C.c_int, fp, fp, C.c_int, C.c_int, dp, dp,
@@ -161,6 +163,19 @@ class OraclePlanner:
         c = lib().orc_astar_find_path(self.h, fptr(_f32(goal)), fptr(_f32(start)), int(bool(cost_only)), fptr(xy), cap,
                                       C.byref(n))
         return c, xy[:n.value].copy()
+
+    def grid3d_neighbors(self, node):
+        """Grid3D::get_neighbors of node = (x, y, h, g, vmin, ci, bin): (rows n x 7 as
+        (x, y, h, g, vmin) floats + (ci, bin) ints, cells n x 2, neglect)."""
+        out = np.zeros((64, 7), np.float32)
+        cells = np.zeros((64, 2), np.int32)
+        ng = C.c_int(0)
+        n = lib().orc_grid3d_neighbors(self.h, fptr(_f32(node[:5])), int(node[5]), int(node[6]), fptr(out), iptr(cells),
+                                       64, C.byref(ng))
+        return out[:n].copy(), cells[:n].copy(), bool(ng.value)
+
+    def check_path(self, xyh):
+        return bool(lib().orc_check_path(self.h, fptr(_f32(xyh, (-1, 3))), len(xyh)))
 
     def closed_keys(self, cap=1 << 20):
         out = np.empty((cap, 3), np.int32)

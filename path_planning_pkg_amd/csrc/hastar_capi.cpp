@@ -1718,6 +1718,118 @@ int hastar_grid2d_set_start_node(hastar_handle h, const float start[2], int cell
   return hastar_grid2d_set_start_node_grid(h, i, j);
 }
 
+// ---- Grid3D<float> on a handle (Grid3D.h:14-46) ----
+// Grid3D::set_start_node (Grid3D.cpp:127-160): the start node in the grid frame and its
+// cell, whose node is soft-reset; default action, velocity 0 (find_path sets its own)
+int hastar_grid3d_set_start_node(hastar_handle h, const float start[3], hastar_node3_f32* node, int cell[2]) {
+  if (!h || !start || !node || !cell) return fail(HASTAR_EINVAL, "null argument");
+  if (!h->goal_set) return fail(HASTAR_EINVAL, "update_goal must come first");
+  prepare_start(h, 0.0f, start);
+  const PlannerDev& D = h->desc;
+  node->x = D.start_x;
+  node->y = D.start_y;
+  node->heading = D.start_h;
+  node->g = 0.0f;
+  node->vmin_sqr = 0.0f;
+  node->curvature_index = D.start_ci;
+  node->angle_bin = D.start_bin;
+  cell[0] = D.start_cx;
+  cell[1] = D.start_cy;
+  return hastar_grid2d_set_start_node_grid(h, D.start_cx, D.start_cy);
+}
+
+// the goal node of Grid3D::update_goal_heading (Grid3D.cpp:115-123)
+int hastar_grid3d_goal_node(hastar_handle h, hastar_node3_f32* node) {
+  if (!h || !node) return fail(HASTAR_EINVAL, "null argument");
+  const PlannerDev& D = h->desc;
+  node->x = D.goal_x;
+  node->y = D.goal_y;
+  node->heading = D.goal_h;
+  node->g = 0.0f;
+  node->vmin_sqr = 0.0f;
+  node->curvature_index = 0;
+  node->angle_bin = D.goal_bin;
+  return HASTAR_OK;
+}
+
+// Grid3D::get_neighbors (Grid3D.cpp:47-74) of one node on the device
+int hastar_grid3d_neighbors(hastar_handle h, const hastar_node3_f32* node, int cap, hastar_node3_f32* out, int* cells,
+                            int* count, int* neglect) {
+  if (!h || !node || !count || !neglect || cap < 0 || (cap > 0 && (!out || !cells)))
+    return fail(HASTAR_EINVAL, "bad argument");
+  const PlannerDev& D = h->desc;
+  if (node->angle_bin < 0 || node->angle_bin > D.bins || node->curvature_index < 0 || node->curvature_index >= D.nsteer)
+    return fail(HASTAR_EINVAL, "node angle bin / curvature index out of range");
+  HIPCHK(hipSetDevice(h->device));
+  DeviceCtx& DC = *h->dc;
+  std::lock_guard<std::mutex> lk(DC.mu);
+  const int oc = std::max(cap, 1);
+  const size_t b_desc = align256(sizeof(PlannerDev)), b_out = align256((size_t)oc * 7 * sizeof(float));
+  const size_t b_cells = align256((size_t)oc * 2 * sizeof(int));
+  if (int rc = stage_acquire(DC, b_desc + b_out + b_cells + 256)) return rc;
+  char* q = DC.stage;
+  PlannerDev* d_desc = reinterpret_cast<PlannerDev*>(q);
+  float* d_out = reinterpret_cast<float*>(q + b_desc);
+  int* d_cells = reinterpret_cast<int*>(q + b_desc + b_out);
+  int* d_cnt = reinterpret_cast<int*>(q + b_desc + b_out + b_cells);
+  HIPCHK(hipMemcpyAsync(d_desc, &D, sizeof(PlannerDev), hipMemcpyHostToDevice, DC.stream));
+  const float nd[5] = {node->x, node->y, node->heading, node->g, node->vmin_sqr};
+  HIPCHK(launch_grid3d_neighbors(d_desc, nd, node->curvature_index, node->angle_bin, d_out, d_cells, cap, d_cnt,
+                                 d_cnt + 1, DC.stream));
+  int cn[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(cn, d_cnt, sizeof(cn), hipMemcpyDeviceToHost, DC.stream));
+  HIPCHK(hipStreamSynchronize(DC.stream));
+  *count = cn[0];
+  *neglect = cn[1];
+  const int k = std::min(cn[0], cap);
+  if (k > 0) {
+    std::vector<float> o((size_t)k * 7);
+    HIPCHK(hipMemcpy(o.data(), d_out, o.size() * sizeof(float), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cells, d_cells, (size_t)k * 2 * sizeof(int), hipMemcpyDeviceToHost));
+    for (int i = 0; i < k; ++i) {
+      const float* r = &o[(size_t)7 * i];
+      out[i].x = r[0];
+      out[i].y = r[1];
+      out[i].heading = r[2];
+      out[i].g = r[3];
+      out[i].vmin_sqr = r[4];
+      std::memcpy(&out[i].curvature_index, &r[5], 4);
+      std::memcpy(&out[i].angle_bin, &r[6], 4);
+    }
+  }
+  if (cn[0] > cap) return fail(HASTAR_ENOSPC, "neighbor buffer too small (*count = required)");
+  return HASTAR_OK;
+}
+
+// Grid3D::check_path (Grid3D.cpp:78-93): *is_free = 1 when every sample's rounded cell is
+// inside the grid and below the threshold
+int hastar_grid3d_check_path(hastar_handle h, const float* xyh, int n, int* is_free) {
+  if (!h || !is_free || n < 0 || (n > 0 && !xyh)) return fail(HASTAR_EINVAL, "bad argument");
+  HIPCHK(hipSetDevice(h->device));
+  DeviceCtx& DC = *h->dc;
+  std::lock_guard<std::mutex> lk(DC.mu);
+  const size_t b_desc = align256(sizeof(PlannerDev)), b_path = align256((size_t)std::max(n, 1) * 3 * sizeof(float));
+  if (int rc = stage_acquire(DC, b_desc + b_path + 256)) return rc;
+  char* q = DC.stage;
+  PlannerDev* d_desc = reinterpret_cast<PlannerDev*>(q);
+  float* d_path = reinterpret_cast<float*>(q + b_desc);
+  int* d_free = reinterpret_cast<int*>(q + b_desc + b_path);
+  HIPCHK(hipMemcpyAsync(d_desc, &h->desc, sizeof(PlannerDev), hipMemcpyHostToDevice, DC.stream));
+  if (n > 0) HIPCHK(hipMemcpyAsync(d_path, xyh, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, DC.stream));
+  HIPCHK(launch_grid3d_check_path(d_desc, d_path, n, d_free, DC.stream));
+  HIPCHK(hipMemcpyAsync(is_free, d_free, sizeof(int), hipMemcpyDeviceToHost, DC.stream));
+  HIPCHK(hipStreamSynchronize(DC.stream));
+  return HASTAR_OK;
+}
+
+// Grid2D::clear_obstacles (Grid2D.cpp:66-71): every log-odds cell back to 0
+int hastar_grid2d_clear(hastar_handle h) {
+  if (!h) return fail(HASTAR_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemsetAsync(h->desc.occ, 0, (size_t)h->desc.N * h->desc.N * sizeof(float), h->dc->stream));
+  return HASTAR_OK;
+}
+
 // AStar::update_goal_node (AStar.cpp:24-28): searches end at this cell
 int hastar_astar_set_goal_cell(hastar_handle h, int i, int j) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");

@@ -1419,6 +1419,76 @@ hipError_t launch_astar_query(const PlannerDev* d_desc, const SlotArena* d_arena
   return hipGetLastError();
 }
 
+// ------------------------------------------------------ Grid3D<float> on its own ------
+// Grid3D::get_neighbors (Grid3D.cpp:47-74) of one node: VehicleModel successors
+// (VehicleModel.cpp:63-105) kept when their truncated cell is inside the grid and below the
+// occupancy threshold, each with the APF field added to g and f (Grid3D.cpp:206-227).
+// out: the kept successors (x, y, heading, g, vmin_sqr | curvature index, bin), cells: their
+// (i, j); *count, *neglect = the model's returned flag.  One wavefront.
+__global__ __launch_bounds__(64) void k_grid3d_neighbors(const PlannerDev* __restrict__ Pp, float nx, float ny, float nh,
+                                                         float ng, float nvm, int nci, int nbin, float* out, int* cells,
+                                                         int cap, int* count, int* neglect) {
+  __shared__ ApfStage apfs;
+  const PlannerDev& P = *Pp;
+  const int lane = threadIdx.x;
+  apf_stage(P, apfs, lane);
+  wave_lds_sync();
+  int lo = nci - P.na;
+  lo = lo < 0 ? 0 : lo;
+  const bool slow = nvm < 1.0f;
+  int c = 0;
+  for (int a = lo; a < lo + 2 * P.na + 1 && a < P.nsteer; ++a) {
+    float vm = 0.0f;
+    if (!slow) {
+      const float lat = nvm * gp(P.curv_abs)[a];
+      if (lat > P.a_lat) continue;
+      const float al = (float)sqrt(1.0 - (double)((lat * lat) / P.a_lat2));
+      vm = nvm - 2.0f * al * P.ts;
+    }
+    const GAS float* ofs = &gp(P.off)[2 * ((size_t)a * (P.bins + 1) + nbin)];
+    const float sx = nx + ofs[0], sy = ny + ofs[1];
+    const float sh = wrap_pi_f(nh + gp(P.dth)[a]);
+    const int cx = trunc_f(sx / P.res), cy = trunc_f(sy / P.res);
+    if (!(cx > -1 && cx < P.N && cy > -1 && cy < P.N)) continue;
+    if (!(gp(P.occ)[(size_t)cx * P.N + cy] < P.thr)) continue;
+    const float fc = apf_field(P, apfs, sx, sy, sh, lane);
+    if (lane == 0 && c < cap) {
+      const float g = ng + gp(P.act_cost)[a];
+      float* o = out + 7 * c;
+      o[0] = sx;
+      o[1] = sy;
+      o[2] = sh;
+      o[3] = g + fc;  // _cost_g += field (Grid3D.cpp:66-67)
+      o[4] = vm;
+      o[5] = __int_as_float(a);
+      o[6] = __int_as_float(heading_bin(sh, P.prec));
+      cells[2 * c] = cx;
+      cells[2 * c + 1] = cy;
+    }
+    ++c;
+  }
+  if (lane == 0) {
+    *count = c;
+    *neglect = slow ? 1 : 0;
+  }
+}
+// Grid3D::check_path (Grid3D.cpp:78-93) of one sampled path
+__global__ __launch_bounds__(64) void k_grid3d_check_path(const PlannerDev* __restrict__ Pp, const float* xyh, int n,
+                                                          int* is_free) {
+  const bool ok = path_is_free(*Pp, gp(xyh), n, threadIdx.x);
+  if (threadIdx.x == 0) *is_free = ok ? 1 : 0;
+}
+hipError_t launch_grid3d_neighbors(const PlannerDev* d_desc, const float node[5], int nci, int nbin, float* out,
+                                   int* cells, int cap, int* count, int* neglect, hipStream_t st) {
+  hipLaunchKernelGGL(k_grid3d_neighbors, dim3(1), dim3(64), 0, st, d_desc, node[0], node[1], node[2], node[3], node[4],
+                     nci, nbin, out, cells, cap, count, neglect);
+  return hipGetLastError();
+}
+hipError_t launch_grid3d_check_path(const PlannerDev* d_desc, const float* xyh, int n, int* is_free, hipStream_t st) {
+  hipLaunchKernelGGL(k_grid3d_check_path, dim3(1), dim3(64), 0, st, d_desc, xyh, n, is_free);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ map kernels -------
 // Grid2D ctor + compute_heuristic (Grid2D.cpp:7-62, 303-316): _node_map f = h.
 // Batched result hand-back: planner i's path (len_i points, when it fits the caller's

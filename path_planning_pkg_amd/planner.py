@@ -73,6 +73,9 @@ def load_library():
     L.hastar_velocity_profile_batch.argtypes = [C.c_int, C.POINTER(HastarVelocityParams), C.c_int,
                                                 C.POINTER(C.c_longlong), fp, fp, fp, fp, C.POINTER(C.c_ubyte), fp,
                                                 C.POINTER(C.c_ubyte)]
+    L.hastar_grid3d_neighbors.argtypes = [vp, C.c_void_p, C.c_int, C.c_void_p, ip, ip, ip]
+    L.hastar_grid3d_check_path.argtypes = [vp, fp, C.c_int, ip]
+    L.hastar_grid3d_set_start_node.argtypes = [vp, fp, C.c_void_p, ip]
     hp = C.POINTER(C.c_void_p)
     L.hastar_update_goal_batch.argtypes = [hp, C.c_int, fp, fp]
     L.hastar_decay_batch.argtypes = [hp, C.c_int]
@@ -264,6 +267,33 @@ class HybridAStar:
         n = ln.value
         return dict(cost=cost.value, ok=bool(ok.value), path=xyh[:n].copy(), curvature=curv[:n].copy(),
                     stats=st.as_dict())
+
+    # ---- Grid3D<float> members on this planner (include/hastar_units.h) ----
+    def grid3d_neighbors(self, node):
+        """Grid3D::get_neighbors (Grid3D.cpp:47-74) of node = (x, y, h, g, vmin, ci, bin):
+        (rows n x 7 float32 with ci / bin as int bit patterns, cells n x 2, neglect)."""
+        inp = np.zeros(7, np.float32)
+        inp[:5] = node[:5]
+        inp[5:].view(np.int32)[:] = [int(node[5]), int(node[6])]
+        out = np.zeros((64, 7), np.float32)
+        cells = np.zeros((64, 2), np.int32)
+        cnt, ng = C.c_int(0), C.c_int(0)
+        _check(load_library().hastar_grid3d_neighbors(self.h, inp.ctypes.data, 64, out.ctypes.data, iptr(cells),
+                                                      C.byref(cnt), C.byref(ng)))
+        return out[:cnt.value].copy(), cells[:cnt.value].copy(), bool(ng.value)
+
+    def check_path(self, xyh):
+        free = C.c_int(0)
+        p = _f32(xyh, (-1, 3))
+        _check(load_library().hastar_grid3d_check_path(self.h, fptr(p), len(p), C.byref(free)))
+        return bool(free.value)
+
+    def set_start_node(self, start):
+        """Grid3D::set_start_node: ((x, y, h, g, vmin, ci, bin), cell)."""
+        out = np.zeros(7, np.float32)
+        cell = np.zeros(2, np.int32)
+        _check(load_library().hastar_grid3d_set_start_node(self.h, fptr(_f32(start)), out.ctypes.data, iptr(cell)))
+        return out, (int(cell[0]), int(cell[1]))
 
     def copy_path(self, n):
         """The last search's path again (hastar_copy_path), into buffers of n poses."""

@@ -95,6 +95,17 @@ int main() {
     for (const auto& n : nb)
       std::printf("%08x %08x %08x %08x %08x %d %d\n", fb(n._pose2D._x), fb(n._pose2D._y), fb(n._pose2D._heading),
                   fb(n._cost_g), fb(n._vmin_sqr), n._curvature_index, n._angle_bin);
+    // the same window through simulate_action (VehicleModel.cpp:108-136), feasible ones only
+    std::vector<Node3D<float>> sim;
+    for (int a = c[5]._curvature_index - 1; a <= c[5]._curvature_index + 1; ++a) {
+      if (a < 0 || a >= 7) continue;
+      auto r = m.simulate_action(c[5], a);
+      if (r.first) sim.push_back(r.second);
+    }
+    std::printf("SIM %zu\n", sim.size());
+    for (const auto& n : sim)
+      std::printf("%08x %08x %08x %08x %08x %d %d\n", fb(n._pose2D._x), fb(n._pose2D._y), fb(n._pose2D._heading),
+                  fb(n._cost_g), fb(n._vmin_sqr), n._curvature_index, n._angle_bin);
   }
   // ---- AStar<float>: test_astar.cpp:14-110 (60 x 60 at 0.5 m, 4 lines, 3 boxes, 5 cycles)
   {

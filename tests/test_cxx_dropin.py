@@ -16,7 +16,7 @@ LIB = ROOT / "path_planning_pkg_amd" / "lib"
 
 def _build(tmp_path):
     exe = tmp_path / "harness"
-    cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", f"-I{ROOT / 'tests' / 'cxx'}",
+    cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off",
            f"-I{ROOT / 'include' / 'path_planning_pkg'}", str(ROOT / "tests" / "cxx" / "harness_main.cpp"),
            f"-L{LIB}", "-lhastar_amd", f"-Wl,-rpath,{LIB}", "-o", str(exe)]
     subprocess.run(cmd, check=True, capture_output=True, text=True)
@@ -70,7 +70,7 @@ int main() {
 def _build_vg(tmp_path):
     src, exe = tmp_path / "vg_main.cpp", tmp_path / "vg_main"
     src.write_text(VG_MAIN)
-    cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", f"-I{ROOT / 'tests' / 'cxx'}",
+    cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off",
            f"-I{ROOT / 'include' / 'path_planning_pkg'}", str(src), f"-L{LIB}", "-lhastar_amd",
            f"-Wl,-rpath,{LIB}", "-o", str(exe)]
     subprocess.run(cmd, check=True, capture_output=True, text=True)
