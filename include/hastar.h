@@ -86,6 +86,12 @@ typedef struct hastar_stats {
 int hastar_create_f32(const hastar_params* params, int device, hastar_handle* out);
 int hastar_destroy(hastar_handle h);
 
+/* n planners with the same constructor arguments in one call (out: n handles, each behaving
+ * like one from hastar_create_f32 and destroyed one by one): their maps share one
+ * allocation and one shared copy of the motion tables (freed with the last of them), and
+ * the node maps are initialised in one launch. */
+int hastar_create_batch_f32(const hastar_params* params, int n, int device, hastar_handle* out);
+
 /* update_goal(goal, start) (HybridAStar.cpp:55-59): goal/start = {x, y, heading}. */
 int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3]);
 

@@ -22,10 +22,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hastar.h"
@@ -442,6 +444,22 @@ struct hastar_handle_s {
   bool have_last = false;
   long long last_pops = 0;      // work estimate for longest-first scheduling (last search's duration)
   int row0 = 0, row1 = 0;       // map-build row window [row0, row1) (hastar_set_row_window); [0, N) by default
+  std::shared_ptr<struct BatchSlab> batch;  // planners of one hastar_create_batch_f32 share it
+};
+
+// One allocation for the persistent state of a batch of identical planners
+// (hastar_create_batch_f32): per planner the log-odds map, node-map f plane, memo bitmap and
+// path output, plus one shared copy of the read-only motion tables.  Freed with the last
+// planner of the batch.
+struct BatchSlab {
+  void* slab = nullptr;
+  void* tables = nullptr;
+  int device = 0;
+  ~BatchSlab() {
+    hipSetDevice(device);
+    if (slab) hipFree(slab);
+    if (tables) hipFree(tables);
+  }
 };
 
 static void free_handle(hastar_handle h) {
@@ -451,7 +469,7 @@ static void free_handle(hastar_handle h) {
   if (h->slab) hipFree(h->slab);
   if (h->dc) {
     DeviceCtx& DC = *h->dc;
-    DC.side.release(h->side, h->side_bytes);
+    if (h->side) DC.side.release(h->side, h->side_bytes);
     side_free(DC, h->d_rp, (size_t)h->rp_cap * 4);
     side_free(DC, h->d_dl, (size_t)h->rp_cap);
     side_free(DC, h->d_ids, (size_t)h->ids_cap);
@@ -469,30 +487,14 @@ const char* hastar_last_error(void) { return g_err.c_str(); }
 float hastar_last_search_ms(void) { return g_last_ms; }
 int hastar_grid_size(hastar_handle h) { return h ? h->desc.N : HASTAR_EINVAL; }
 
-// HybridAStar::HybridAStar (HybridAStar.cpp:7-24) and the member constructors it runs:
-// Grid2D (Grid2D.cpp:7-62), VehicleModel (VehicleModel.cpp:7-47), Dubins (Dubins.cpp:7-16).
-int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
-  if (!p || !out) return fail(HASTAR_EINVAL, "null argument");
-  *out = nullptr;
-  if (p->grid_size < 2 || p->grid_size > 4095) return fail(HASTAR_EINVAL, "grid_size must be in [2, 4095]");
-  if (p->num_angle_bins < 1 || p->num_angle_bins > 254) return fail(HASTAR_EINVAL, "num_angle_bins must be in [1, 254]");
-  if (p->num_steering < 1 || p->num_steering > 16 || !p->steering || !p->curvature_weights)
-    return fail(HASTAR_EINVAL, "num_steering must be in [1, 16] with steering/curvature_weights arrays");
-  if (p->num_actions < 0) return fail(HASTAR_EINVAL, "num_actions must be >= 0");
-  if (p->max_pops > (int)SLOT3_IDX_MASK - 1) return fail(HASTAR_EINVAL, "max_pops must be below 2^24 - 1");
-  if (p->max_pops < 0) return fail(HASTAR_EINVAL, "max_pops must be >= 0");
-  if (!(p->grid_resolution > 0) || !(p->step_size > 0)) return fail(HASTAR_EINVAL, "resolution/step must be > 0");
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-    return fail(HASTAR_EDEVICE, "no HIP device available (this library has no CPU path)");
-  if (device < 0 || device >= ndev || device >= 64) return fail(HASTAR_EINVAL, "device ordinal out of range");
-  DeviceCtx* dc = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(g_dev[device].mu);
-    if (int rc = device_ctx(device, &dc)) return rc;
-  }
-  HIPCHK(hipSetDevice(device));
-
+// Host half of the constructor (HybridAStar.cpp:7-24 and the member constructors it runs):
+// every scalar of the planner descriptor, its arena requirements, and the motion tables
+// (VehicleModel.cpp:7-47), which the caller uploads (one copy per planner, or one shared
+// copy for a batch of identical planners).
+struct HostTables {
+  std::vector<float> off, dth, cost;
+};
+static hastar_handle new_planner(const hastar_params* p, int device, DeviceCtx* dc, HostTables& T) {
   hastar_handle h = new hastar_handle_s();
   h->device = device;
   h->dc = dc;
@@ -526,7 +528,13 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   D.a_lat2 = p->max_lat_acc * p->max_lat_acc;
   D.prec = (float)(2 * M_PI / D.bins);
   const int ns = D.nsteer, bins = D.bins;
-  std::vector<float> beta(ns), curv(ns), dth(ns), cost(ns), off((size_t)ns * (bins + 1) * 2, 0.0f);
+  std::vector<float> beta(ns), curv(ns);
+  std::vector<float>& dth = T.dth;
+  std::vector<float>& cost = T.cost;
+  std::vector<float>& off = T.off;
+  dth.assign(ns, 0.0f);
+  cost.assign(ns, 0.0f);
+  off.assign((size_t)ns * (bins + 1) * 2, 0.0f);
   for (int i = 0; i < ns; ++i) {
     beta[i] = g_atan2f(p->rear_to_cg * std::tan(p->steering[i]), p->wheelbase);
     curv[i] = g_cosf(beta[i]) * std::tan(p->steering[i]) / p->wheelbase;
@@ -592,6 +600,47 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
   // truncated).
   D.out_cap = dub_cap + std::min(h->max_pops + 2, 8 * N + 64);
 
+  return h;
+}
+
+static int check_params(const hastar_params* p) {
+  if (p->grid_size < 2 || p->grid_size > 4095) return fail(HASTAR_EINVAL, "grid_size must be in [2, 4095]");
+  if (p->num_angle_bins < 1 || p->num_angle_bins > 254) return fail(HASTAR_EINVAL, "num_angle_bins must be in [1, 254]");
+  if (p->num_steering < 1 || p->num_steering > 16 || !p->steering || !p->curvature_weights)
+    return fail(HASTAR_EINVAL, "num_steering must be in [1, 16] with steering/curvature_weights arrays");
+  if (p->num_actions < 0) return fail(HASTAR_EINVAL, "num_actions must be >= 0");
+  if (p->max_pops > (int)SLOT3_IDX_MASK - 1) return fail(HASTAR_EINVAL, "max_pops must be below 2^24 - 1");
+  if (p->max_pops < 0) return fail(HASTAR_EINVAL, "max_pops must be >= 0");
+  if (!(p->grid_resolution > 0) || !(p->step_size > 0)) return fail(HASTAR_EINVAL, "resolution/step must be > 0");
+  return 0;
+}
+
+// HybridAStar::HybridAStar (HybridAStar.cpp:7-24) and the member constructors it runs:
+// Grid2D (Grid2D.cpp:7-62), VehicleModel (VehicleModel.cpp:7-47), Dubins (Dubins.cpp:7-16).
+int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
+  if (!p || !out) return fail(HASTAR_EINVAL, "null argument");
+  *out = nullptr;
+  if (int rc = check_params(p)) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(HASTAR_EDEVICE, "no HIP device available (this library has no CPU path)");
+  if (device < 0 || device >= ndev || device >= 64) return fail(HASTAR_EINVAL, "device ordinal out of range");
+  DeviceCtx* dc = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_dev[device].mu);
+    if (int rc = device_ctx(device, &dc)) return rc;
+  }
+  HIPCHK(hipSetDevice(device));
+
+  HostTables T;
+  hastar_handle h = new_planner(p, device, dc, T);
+  PlannerDev& D = h->desc;
+  const int N = D.N;
+  const int ns = D.nsteer;
+  const size_t NN = (size_t)N * N;
+  std::vector<float>& off = T.off;
+  std::vector<float>& dth = T.dth;
+  std::vector<float>& cost = T.cost;
   // the planner's persistent state: the two N x N maps in one exact allocation (8 MiB at
   // N = 1024, a whole number of 2-MiB granules), everything else from the device's pool
   const size_t b_occ = align256(NN * sizeof(float)), b_nm = align256(NN * sizeof(float));
@@ -638,6 +687,87 @@ int hastar_create_f32(const hastar_params* p, int device, hastar_handle* out) {
     return fail(HASTAR_EDEVICE, std::string("init: ") + hipGetErrorString(he));
   }
   *out = h;
+  return HASTAR_OK;
+}
+
+// n planners with the same constructor arguments (a batch of independent queries): one
+// allocation for all their maps, one shared copy of the motion tables, one initialisation
+// launch and one synchronisation, instead of n of each.  out[i] are independent handles
+// (each behaves exactly like one from hastar_create_f32); the shared memory is released
+// with the last of them.
+int hastar_create_batch_f32(const hastar_params* p, int n, int device, hastar_handle* out) {
+  if (!p || !out || n < 0) return fail(HASTAR_EINVAL, "bad argument");
+  if (n == 0) return HASTAR_OK;
+  for (int i = 0; i < n; ++i) out[i] = nullptr;
+  if (int rc = check_params(p)) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(HASTAR_EDEVICE, "no HIP device available (this library has no CPU path)");
+  if (device < 0 || device >= ndev || device >= 64) return fail(HASTAR_EINVAL, "device ordinal out of range");
+  DeviceCtx* dc = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_dev[device].mu);
+    if (int rc = device_ctx(device, &dc)) return rc;
+  }
+  HIPCHK(hipSetDevice(device));
+  HostTables T;
+  hastar_handle h0 = new_planner(p, device, dc, T);
+  const PlannerDev D0 = h0->desc;
+  const size_t NN = (size_t)D0.N * D0.N;
+  const int ns = D0.nsteer;
+  const size_t b_map = align256(NN * sizeof(float)), b_vis = align256(bitmap_words(NN) * sizeof(uint32_t));
+  const size_t b_ox = align256((size_t)D0.out_cap * 3 * sizeof(float)), b_oc = align256((size_t)D0.out_cap * sizeof(float));
+  const size_t stride = 2 * b_map + b_vis + b_ox + b_oc;
+  const size_t b_off = align256(T.off.size() * sizeof(float)), b_s = align256((size_t)ns * sizeof(float));
+  auto bs = std::make_shared<BatchSlab>();
+  bs->device = device;
+  if (hipMalloc(&bs->slab, stride * (size_t)n) != hipSuccess || hipMalloc(&bs->tables, b_off + 3 * b_s) != hipSuccess) {
+    delete h0;
+    return fail(HASTAR_ENOMEM, "batch planner state allocation failed (" + std::to_string(stride * (size_t)n >> 20) + " MiB)");
+  }
+  char* t = static_cast<char*>(bs->tables);
+  float* d_off = reinterpret_cast<float*>(t);
+  float* d_dth = reinterpret_cast<float*>(t + b_off);
+  float* d_cost = reinterpret_cast<float*>(t + b_off + b_s);
+  float* d_ca = reinterpret_cast<float*>(t + b_off + 2 * b_s);
+  hipStream_t st = dc->stream;
+  hipError_t he = hipMemsetAsync(bs->slab, 0, stride * (size_t)n, st);
+  if (he == hipSuccess) he = hipMemcpyAsync(d_off, T.off.data(), T.off.size() * sizeof(float), hipMemcpyHostToDevice, st);
+  if (he == hipSuccess) he = hipMemcpyAsync(d_dth, T.dth.data(), ns * sizeof(float), hipMemcpyHostToDevice, st);
+  if (he == hipSuccess) he = hipMemcpyAsync(d_cost, T.cost.data(), ns * sizeof(float), hipMemcpyHostToDevice, st);
+  if (he == hipSuccess) he = hipMemcpyAsync(d_ca, h0->curv_abs.data(), ns * sizeof(float), hipMemcpyHostToDevice, st);
+  for (int i = 0; i < n && he == hipSuccess; ++i) {
+    hastar_handle h = i == 0 ? h0 : new hastar_handle_s(*h0);
+    char* q = static_cast<char*>(bs->slab) + stride * (size_t)i;
+    PlannerDev& D = h->desc;
+    D.occ = reinterpret_cast<float*>(q);
+    D.nm_f = reinterpret_cast<float*>(q + b_map);
+    D.visited = reinterpret_cast<uint32_t*>(q + 2 * b_map);
+    D.out_xyh = reinterpret_cast<float*>(q + 2 * b_map + b_vis);
+    D.out_curv = reinterpret_cast<float*>(q + 2 * b_map + b_vis + b_ox);
+    D.off = d_off;
+    D.dth = d_dth;
+    D.act_cost = d_cost;
+    D.curv_abs = d_ca;
+    D.result = nullptr;
+    D.apf = nullptr;
+    D.n_apf = 0;
+    h->slab = nullptr;
+    h->side = nullptr;
+    h->side_bytes = 0;
+    h->batch = bs;
+    out[i] = h;
+  }
+  // the node-map f planes (Grid2D ctor + compute_heuristic) of every planner in one launch
+  if (he == hipSuccess) he = launch_init_nodemap_batch(out[0]->desc, static_cast<char*>(bs->slab) + b_map, stride, n, st);
+  if (he == hipSuccess) he = hipStreamSynchronize(st);
+  if (he != hipSuccess) {
+    for (int i = 0; i < n; ++i) {
+      if (out[i]) delete out[i];
+      out[i] = nullptr;
+    }
+    return fail(HASTAR_EDEVICE, std::string("batch init: ") + hipGetErrorString(he));
+  }
   return HASTAR_OK;
 }
 
@@ -826,12 +956,27 @@ static int update_boxes_impl(const hastar_handle* hs, int n, const float* boxes,
   std::vector<BoxPrep> prep(n);
   std::vector<long long> first(n + 1, 0);
   for (int i = 0; i < n; ++i) first[i + 1] = first[i] + counts[i];
-  int max_layers = 0;
-  for (int i = 0; i < n; ++i) {
-    const long long o = first[i];
-    boxes_prep(hs[i], boxes + 4 * o, conf + o, counts[i], apf_added_radius, prep[i]);
-    if (!prep[i].big) max_layers = std::max(max_layers, prep[i].n_layers);
+  // host preparation of every planner (rotations, raster origins, layers: O(boxes^2) each),
+  // spread over host threads for large batches
+  {
+    auto work = [&](int a, int b) {
+      for (int i = a; i < b; ++i) {
+        const long long o = first[i];
+        boxes_prep(hs[i], boxes + 4 * o, conf + o, counts[i], apf_added_radius, prep[i]);
+      }
+    };
+    const int nt = n >= 256 ? (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
+    if (nt <= 1) {
+      work(0, n);
+    } else {
+      std::vector<std::thread> pool;
+      for (int t = 0; t < nt; ++t) pool.emplace_back(work, (int)((long long)n * t / nt), (int)((long long)n * (t + 1) / nt));
+      for (auto& th : pool) th.join();
+    }
   }
+  int max_layers = 0;
+  for (int i = 0; i < n; ++i)
+    if (!prep[i].big) max_layers = std::max(max_layers, prep[i].n_layers);
   // planners with an oversized box footprint take the per-planner kernel
   for (int i = 0; i < n; ++i)
     if (prep[i].big)

@@ -18,6 +18,7 @@ hipError_t launch_astar_query(const PlannerDev* d_desc, const SlotArena* d_arena
 hipError_t launch_gather_paths(const PlannerDev* d_descs, const long long* d_off, const int* d_len, int n, float* xyh,
                                float* curv, hipStream_t st);
 hipError_t launch_init_nodemap(const PlannerDev& P, hipStream_t st);
+hipError_t launch_init_nodemap_batch(const PlannerDev& P, char* base, size_t stride, int n, hipStream_t st);
 hipError_t launch_clear_bitmaps(uint32_t* const* ptrs, int n, size_t words, hipStream_t st);
 hipError_t launch_decay(float* occ, size_t NN, float lp_free, float lp_min, float lp_max, hipStream_t st);
 hipError_t launch_relocate(int N, float c, float s, float ox, float oy, const float* src, float* dst, int* winner,

@@ -1533,6 +1533,30 @@ __global__ __launch_bounds__(256) void k_init_nodemap(PlannerDev P) {
   }
 }
 
+// the same for n planners whose f planes lie `stride` bytes apart (hastar_create_batch_f32)
+__global__ __launch_bounds__(256) void k_init_nodemap_batch(PlannerDev P, char* base, size_t stride, int n) {
+  const int N = P.N;
+  for (int pl = blockIdx.y; pl < n; pl += gridDim.y) {
+    GAS float* f = gp(reinterpret_cast<float*>(base + stride * (size_t)pl));
+    for (int i = blockIdx.x; i < N; i += gridDim.x) {
+      const float dx = (float)(P.n45 - i) * P.res;
+      const float dx2 = dx * dx;
+      GAS float* row = f + (size_t)i * N;
+      for (int j = threadIdx.x; j < N; j += blockDim.x) {
+        const float dy = (float)(P.n2 - j) * P.res;
+        const float dy2 = dy * dy;
+        row[j] = sqrtf(dx2 + dy2);
+      }
+    }
+  }
+}
+hipError_t launch_init_nodemap_batch(const PlannerDev& P, char* base, size_t stride, int n, hipStream_t st) {
+  if (P.N <= 0 || n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_init_nodemap_batch, dim3(std::min(P.N, 256), std::min(n, 65535)), dim3(256), 0, st, P, base,
+                     stride, n);
+  return hipGetLastError();
+}
+
 // Grid2D::update_obstacles() (Grid2D.cpp:197-208), float4-vectorised.  `occ` may start
 // anywhere (a row window of the map, see hastar_set_row_window): the cells before the first
 // 16-B boundary and after the last one are done one by one.

@@ -76,6 +76,7 @@ def load_library():
     L.hastar_grid3d_neighbors.argtypes = [vp, C.c_void_p, C.c_int, C.c_void_p, ip, ip, ip]
     L.hastar_grid3d_check_path.argtypes = [vp, fp, C.c_int, ip]
     L.hastar_grid3d_set_start_node.argtypes = [vp, fp, C.c_void_p, ip]
+    L.hastar_create_batch_f32.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
     hp = C.POINTER(C.c_void_p)
     L.hastar_update_goal_batch.argtypes = [hp, C.c_int, fp, fp]
     L.hastar_decay_batch.argtypes = [hp, C.c_int]
@@ -187,6 +188,21 @@ class HybridAStar:
         h = C.c_void_p()
         _check(load_library().hastar_create_f32(C.byref(self._params), device, C.byref(h)))
         self.h = h
+
+    @classmethod
+    def create_batch(cls, cfg: PlannerConfig, n: int, device: int = 0):
+        """n planners with the same constructor arguments (hastar_create_batch_f32: one
+        allocation for their maps, one shared copy of the motion tables)."""
+        params = cfg.struct()
+        hs = (C.c_void_p * n)()
+        _check(load_library().hastar_create_batch_f32(C.byref(params), n, device, hs))
+        out = []
+        for i in range(n):
+            o = cls.__new__(cls)
+            o.cfg, o._params, o.N = cfg, params, cfg.grid_size
+            o.h = C.c_void_p(hs[i])
+            out.append(o)
+        return out
 
     def close(self):
         if getattr(self, "h", None) and self.h.value:

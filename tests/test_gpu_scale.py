@@ -243,3 +243,21 @@ def test_batched_map_updates_equal_single_calls(gpu, oracle_lib):
         assert_bits_equal(g.get_obstacles(), o.get_obstacles(), "drive_batch map")
         compare_results(g.find_path(proto["vel"], proto["start"]), o.find_path(proto["vel"], proto["start"]),
                         "search on a drive_batch map")
+
+
+def test_batch_created_planners_equal_single(gpu, oracle_lib):
+    """hastar_create_batch_f32: planners sharing one allocation and one copy of the motion
+    tables plan exactly like the oracle (and so like singly created ones), and destroying
+    some of them leaves the others intact."""
+    from tests.scenarios import drive_batch
+    cases = [synthetic(256, 36, 40, s) for s in (1, 2, 4, 5)]
+    gs = gpu.HybridAStar.create_batch(cases[0][0], len(cases))
+    drive_batch(gpu, gs, [p for _, p in cases])
+    gs[1].close()
+    for i in (0, 2, 3):
+        cfg, proto = cases[i]
+        o = oracle_lib.OraclePlanner(cfg)
+        drive(o, proto)
+        assert_bits_equal(gs[i].get_obstacles(), o.get_obstacles(), f"batch-created map {i}")
+        compare_results(gs[i].find_path(proto["vel"], proto["start"]), o.find_path(proto["vel"], proto["start"]),
+                        f"batch-created planner {i}")
