@@ -115,6 +115,9 @@ def parse_args(argv=None):
                          "(BASELINE.json configs[3]); cfg5: 20 Hz replan loop of start/goal pairs (configs[4])")
     ap.add_argument("--map-queries", type=int, default=16, help="cfg4: maps built both locally and row-sharded")
     ap.add_argument("--pairs", type=int, default=64, help="cfg5: start/goal pairs in total, dealt over the ranks")
+    ap.add_argument("--relaxed-delta", type=float, default=0.5, help="relaxed mode: frontier width (m)")
+    ap.add_argument("--relaxed-weight", type=float, default=1.2, help="relaxed mode: heuristic weight")
+    ap.add_argument("--no-relaxed", action="store_true", help="cfg5: skip the relaxed-mode comparison")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: exercises the launcher, sharding and reductions only (CPU rehearsal)")
@@ -220,6 +223,8 @@ def main():
         longest = {"query": qids[li], "pops": int(last.stats["pops"][li])}
         planners[li].reset()
         _, longest["gpu_ms_alone"] = gpu.find_path_batch([planners[li]], [vels[li]], [starts[li]], cap=8192)
+        relaxed = relaxed_latency_phase(gpu, planners, vels, starts, last, lat_ids + [li], qids, args,
+                                        lat + [longest["gpu_ms_alone"]])
         traffic = None
         pmc = ROOT / "profiles" / "pmc_search_summary.json"
         if pmc.exists():
@@ -270,6 +275,7 @@ def main():
         if map_build:
             out["map_build"] = map_build
         out["velocity_profile"] = vel_prof
+        out["relaxed_mode"] = relaxed
         if not args.no_cpu_baseline:
             cb = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps, lat_ids)
             out["cpu_baseline"] = cb
@@ -436,6 +442,29 @@ def map_build_phase(args, gpu, dist, torch, rank, world, device):
             "protocol": "update_goal + 5 x {decay, 200 boxes} per map (tests/scenarios.py::drive)"}
 
 
+def relaxed_latency_phase(gpu, planners, vels, starts, last, ids, qids, args, exact_ms):
+    """The RELAXED mode (hastar_find_path_relaxed_batch, SURVEY.md §8(f) rank 4: non-parity,
+    frontier-parallel with a backward-Dijkstra heuristic) on the latency queries and the longest
+    query, one query per call, beside the exact mode's result for the same inputs (the last timed
+    step).  Not part of `value`: a different algorithm, reported separately."""
+    opts = dict(delta=args.relaxed_delta, h_weight=args.relaxed_weight)
+    ms, ratios, ok, exp = [], [], 0, []
+    for i in ids:
+        r, kms = gpu.find_path_batch([planners[i]], [vels[i]], [starts[i]], cap=8192, relaxed=opts)
+        r = r[0]
+        ms.append(kms)
+        ok += int(r["ok"])
+        exp.append(int(r["stats"]["pops"]))
+        if r["ok"] and last.ok[i]:
+            ratios.append(float(r["cost"]) / float(last.cost[i]))
+    return {"queries": [qids[i] for i in ids], "gpu_ms": ms, "gpu_median_ms": float(np.median(ms)) if ms else None,
+            "exact_gpu_ms_same_queries": exact_ms, "ok": ok, "exact_ok": int(sum(int(last.ok[i]) for i in ids)),
+            "cost_ratio_vs_exact": ratios, "expansions": exp, "opts": opts,
+            "note": "non-parity mode: valid paths (tests/test_gpu_relaxed.py), cost relative to the exact "
+                    "(reference-identical) result of the same query"}
+
+
+
 def run_cfg5(args, gpu, dist, torch, rank, world, device):
     """BASELINE.json configs[4] / SURVEY.md §8d cfg5: the local planner's replan loop for
     `pairs` start/goal pairs IN TOTAL, dealt round-robin over the ranks (strong scaling, no
@@ -463,32 +492,52 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
     apf_r = pairs[0][1]["apf_r"] if pairs else 2.5
     tick = [0]
 
-    def step():
+    relaxed_opts = dict(delta=args.relaxed_delta, h_weight=args.relaxed_weight)
+    rx = {"kernel_ms": [], "wall_ms": [], "upkeep_ms": [], "ok": 0, "ratios": []}
+
+    def step(timed):
+        """One tick; returns (stats, kernel ms, successes, seconds of the exact tick).  When
+        timed, the relaxed mode also plans the tick's queries on the same maps (between the
+        exact find_path and the upkeep; its time is not part of the exact tick)."""
         t = tick[0]
+        t0 = time.perf_counter()
         starts = [replan_tick_inputs(proto, v, t)[0] for _, proto, v in pairs]
         br = gpu.find_path_batch_arrays(planners, vels, starts, buffers=bufs)
         st = br.stats.copy()
+        t_exact = time.perf_counter() - t0
+        if timed and not args.no_relaxed and planners:
+            t1 = time.perf_counter()
+            rel, rms = gpu.find_path_batch(planners, vels, starts, cap=8192, relaxed=relaxed_opts)
+            rx["wall_ms"].append((time.perf_counter() - t1) * 1e3)
+            rx["kernel_ms"].append(rms)
+            rx["ok"] += sum(int(r["ok"]) for r in rel)
+            rx["ratios"] += [float(r["cost"]) / float(br.cost[i]) for i, r in enumerate(rel) if r["ok"] and br.ok[i]]
         # the tick's map upkeep (local_planner.cpp:241,288), batched: decay + moved boxes
+        t2 = time.perf_counter()
         gpu.decay_batch(bufs)
         gpu.update_boxes_batch(bufs, [replan_tick_inputs(proto, v, t + 1)[1] for _, proto, v in pairs], conf, apf_r)
+        torch.cuda.synchronize(device)
+        up = time.perf_counter() - t2
+        if timed:
+            rx["upkeep_ms"].append(up * 1e3)
         tick[0] += 1
-        return st, br.kernel_ms, int(br.ok.sum())
+        return st, br.kernel_ms, int(br.ok.sum()), t_exact + up
 
     for _ in range(args.warmup):
-        step()
+        step(False)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
     pops, kms, oks, alg = 0, [], 0, []
+    elapsed = 0.0
     for _ in range(args.steps):
-        st, k, ok = step()
+        st, k, ok, secs = step(True)
+        elapsed += secs
         pops += int(st["pops"].sum())
         kms.append(k)
         oks += ok
         alg.append(algorithmic_bytes(st, args.obstacles))
     torch.cuda.synchronize(device)
-    elapsed = time.perf_counter() - t0
     elapsed, pops_all = reduce_over_ranks(dist, elapsed, pops, f"cuda:{device}")
     out = None
     if rank == 0:
@@ -512,6 +561,16 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
                          "kernel": "hastar_search_kernel", "kernel_ms": avg_k,
                          "alg_bytes_per_launch": float(np.mean(alg))},
         }
+        if rx["kernel_ms"]:
+            out["relaxed_mode"] = {
+                "tick_search_ms": float(np.mean(rx["kernel_ms"])), "tick_find_wall_ms": float(np.mean(rx["wall_ms"])),
+                "tick_ms": float(np.mean(rx["wall_ms"]) + np.mean(rx["upkeep_ms"])),
+                "success_rate": rx["ok"] / max(len(ids) * args.steps, 1),
+                "cost_ratio_vs_exact_mean": float(np.mean(rx["ratios"])) if rx["ratios"] else None,
+                "cost_ratio_vs_exact_max": float(np.max(rx["ratios"])) if rx["ratios"] else None,
+                "opts": relaxed_opts,
+                "note": "non-parity mode (hastar_find_path_relaxed_batch) on the same ticks' maps and starts as the "
+                        "exact loop (rank 0); tick_ms = its find_path wall + the same batched upkeep"}
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_cfg5(pairs, args.cpu_seconds, args.warmup + args.steps)
     if dist:

@@ -148,6 +148,29 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel_init
                            float* xyh, float* curv, int cap, int* len, float* cost, int* ok,
                            hastar_stats* stats);
 
+/* ---- RELAXED search mode (no reference counterpart) ----
+ * NOT bit-exact with the reference, by design: a frontier-parallel Hybrid A* (one workgroup
+ * of 8 wavefronts per planner) whose heuristic is a backward Dijkstra over the grid (the
+ * converged value of the reference's lazy holonomic A*, AStar.cpp:118-186) and whose rounds
+ * expand every open node with f <= min f + delta at once, with a best-g table per node key
+ * instead of the closed set.  Same successors, costs, APF field, Dubins shots and output
+ * format as hastar_find_path_batch, so a caller can switch per call; paths are valid
+ * (collision-free, start to goal) but may differ from, and cost more or less than, the
+ * reference's.  The exact mode's memo (node-map f, visited flags) is neither read nor written.
+ * opts may be NULL (defaults in brackets). */
+typedef struct hastar_relaxed_opts {
+  float delta;     /* frontier width in metres [0.5] */
+  float h_stop;    /* the Dijkstra stops at h_stop x the start's distance (+64 buckets) [3.0] */
+  int max_nodes;   /* node capacity per search; beyond it the search ends with HASTAR_EOVERFLOW [1 << 20] */
+  int max_rounds;  /* [1 << 20] */
+  float h_weight;  /* f = g + h_weight x max(h, Dubins length); > 1 trades cost for speed [1.2]
+                      (at the defaults the measured costs were 0.92-1.00 x the exact mode's,
+                      profiles/relaxed_sweep_r02.json) */
+} hastar_relaxed_opts;
+int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, const float* vel_init, const float* starts,
+                                   float* xyh, float* curv, int cap, int* len, float* cost, int* ok,
+                                   hastar_stats* stats, const hastar_relaxed_opts* opts);
+
 /* get_obstacles() (HybridAStar.cpp:62-65): copies the N x N log-odds map (row i = x cell). */
 int hastar_get_obstacles(hastar_handle h, float* out);
 

@@ -60,6 +60,17 @@ class HastarStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class HastarRelaxedOpts(C.Structure):
+    """hastar_relaxed_opts (include/hastar.h): 0 selects a field's default."""
+    _fields_ = [
+        ("delta", C.c_float),
+        ("h_stop", C.c_float),
+        ("max_nodes", C.c_int),
+        ("max_rounds", C.c_int),
+        ("h_weight", C.c_float),
+    ]
+
+
 class PlannerConfig:
     """Python-side planner configuration; owns the float arrays the struct points to."""
 

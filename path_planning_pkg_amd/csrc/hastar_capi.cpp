@@ -203,6 +203,12 @@ struct DeviceCtx {
   SlotArena* d_resume = nullptr;  // arena descriptors of a resume launch
   int* d_resume_order = nullptr;
   size_t resume_cap = 0;
+  // relaxed-mode arenas (hastar_find_path_relaxed_batch): one per resident planner workgroup
+  void* rslab = nullptr;
+  RelaxArena* d_rarenas = nullptr;
+  int n_rarenas = 0;
+  size_t r_cells = 0;
+  int r_nodes = 0, r_N = 0;
 };
 
 // A larger arena that continues one parked search (hastar_find_path_batch).
@@ -1442,6 +1448,119 @@ static int copy_path_out(hastar_handle h, float* xyh, float* curv, int cap, int*
   return 0;
 }
 
+// per-batch device/pinned buffers (descriptors, order, results, path offsets), grown on demand
+static int batch_acquire(DeviceCtx& DC, int n) {
+  hipStream_t st = DC.stream;
+  if (n <= DC.batch_cap) return 0;
+  {
+    HIPCHK(hipStreamSynchronize(st));
+    if (DC.d_descs) hipFree(DC.d_descs);
+    if (DC.d_order) hipFree(DC.d_order);
+    if (DC.d_results) hipFree(DC.d_results);
+    if (DC.d_off) hipFree(DC.d_off);
+    if (DC.d_len) hipFree(DC.d_len);
+    if (DC.h_results) hipHostFree(DC.h_results);
+    if (DC.h_offlen) hipHostFree(DC.h_offlen);
+    DC.d_descs = nullptr;
+    DC.d_order = nullptr;
+    DC.d_results = nullptr;
+    DC.d_off = nullptr;
+    DC.d_len = nullptr;
+    DC.h_results = nullptr;
+    DC.h_offlen = nullptr;
+    DC.batch_cap = 0;
+    HIPCHK(dalloc(&DC.d_descs, (size_t)n));
+    HIPCHK(dalloc(&DC.d_order, (size_t)n));
+    HIPCHK(dalloc(&DC.d_results, (size_t)n));
+    HIPCHK(dalloc(&DC.d_off, (size_t)n + 1));
+    HIPCHK(dalloc(&DC.d_len, (size_t)n));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_results), (size_t)n * sizeof(SearchResult)));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_offlen), ((size_t)n * 2 + 1) * sizeof(long long)));
+    DC.batch_cap = n;
+  }
+  return 0;
+}
+
+// Hand a finished batch back: per-planner outcome (stats[i].status), then the paths that fit
+// the caller's buffers packed by one gather kernel and one copy.  lpt: record each search's
+// duration as the planner's longest-first key (exact mode only).
+static int finish_batch(DeviceCtx& DC, const hastar_handle* hs, int n, float* xyh, float* curv, int cap, int* len,
+                        float* cost, int* ok, hastar_stats* stats, bool lpt) {
+  hipStream_t st = DC.stream;
+  int rc = HASTAR_OK;
+  // pack the paths that fit the caller's buffers: offsets, one gather kernel, one copy.
+  // Every planner reports its own outcome in stats[i].status: 0, HASTAR_EOVERFLOW (the
+  // search needed more device memory than it could get, or hit HASTAR_MAX_POPS_HARD),
+  // HASTAR_ENOSPC (kernel: path longer than the planner's output buffer; host: longer than
+  // `cap` — then len[i] is the length needed and hastar_copy_path fetches it).  The return
+  // code is the first ENOSPC, else the first EOVERFLOW.
+  long long* h_off = DC.h_offlen;
+  int* h_len = reinterpret_cast<int*>(DC.h_offlen + n + 1);
+  long long total = 0;
+  int rc_over = HASTAR_OK;
+  for (int i = 0; i < n; ++i) {
+    SearchResult& R = DC.h_results[i];
+    hastar_handle h = hs[i];
+    if (R.status == -75) R.ok = 0;
+    h->last = R;
+    h->have_last = true;
+    // longest-first key: the search's own duration (s_memrealtime ticks) — it weighs outer
+    // pops, inner A* pops and shots by what they actually cost, unlike a pop count
+    if (lpt) h->last_pops = R.t_end > R.t_start ? (long long)(R.t_end - R.t_start) : (long long)R.pops + R.astar_pops;
+    ok[i] = R.ok;
+    cost[i] = R.ok ? R.cost : FLT_MAX;
+    fill_stats(R, stats ? &stats[i] : nullptr);
+    len[i] = R.path_len;
+    if (R.status == -75 && rc_over == HASTAR_OK) {
+      rc_over = HASTAR_EOVERFLOW;
+      g_err = "search ended by an arena overflow (device memory) or HASTAR_MAX_POPS_HARD";
+    } else if (R.status == -28 && rc == HASTAR_OK) {
+      rc = fail(HASTAR_ENOSPC, "path longer than the planner's output buffer");
+    }
+    int take = R.path_len;
+    if (take > cap) {
+      take = 0;  // the caller fetches it with hastar_copy_path
+      if (stats) stats[i].status = HASTAR_ENOSPC;
+      if (rc == HASTAR_OK) rc = fail(HASTAR_ENOSPC, "path buffer too small");
+    }
+    h_off[i] = total;
+    h_len[i] = take;
+    total += take;
+  }
+  if (rc == HASTAR_OK && rc_over != HASTAR_OK) rc = rc_over;
+  h_off[n] = total;
+  DC.last_n = n;
+  DC.last_total = total;
+  if (total > 0) {
+    if ((size_t)total > DC.pts_cap) {
+      if (DC.d_pxyh) hipFree(DC.d_pxyh);
+      if (DC.d_pcurv) hipFree(DC.d_pcurv);
+      if (DC.h_pxyh) hipHostFree(DC.h_pxyh);
+      if (DC.h_pcurv) hipHostFree(DC.h_pcurv);
+      DC.d_pxyh = DC.d_pcurv = DC.h_pxyh = DC.h_pcurv = nullptr;
+      DC.pts_cap = 0;
+      const size_t c2 = (size_t)total + (size_t)total / 2 + 1024;
+      HIPCHK(dalloc(&DC.d_pxyh, c2 * 3));
+      HIPCHK(dalloc(&DC.d_pcurv, c2));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_pxyh), c2 * 3 * sizeof(float)));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_pcurv), c2 * sizeof(float)));
+      DC.pts_cap = c2;
+    }
+    HIPCHK(hipMemcpyAsync(DC.d_off, h_off, ((size_t)n + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(DC.d_len, h_len, (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(launch_gather_paths(DC.d_descs, DC.d_off, DC.d_len, n, DC.d_pxyh, DC.d_pcurv, st));
+    HIPCHK(hipMemcpyAsync(DC.h_pxyh, DC.d_pxyh, (size_t)total * 3 * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(DC.h_pcurv, DC.d_pcurv, (size_t)total * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (int i = 0; i < n; ++i) {
+      if (h_len[i] == 0) continue;
+      std::memcpy(xyh + (size_t)i * cap * 3, DC.h_pxyh + 3 * h_off[i], (size_t)h_len[i] * 3 * sizeof(float));
+      std::memcpy(curv + (size_t)i * cap, DC.h_pcurv + h_off[i], (size_t)h_len[i] * sizeof(float));
+    }
+  }
+  return rc;
+}
+
 extern "C" {
 
 int hastar_find_path(hastar_handle h, float vel, const float start[3], float* xyh, float* curv, int cap, int* len,
@@ -1468,32 +1587,7 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   if (const char* e = std::getenv("HASTAR_SLOTS")) W = std::max(1, std::min(W, std::atoi(e)));
   if (int rc = arenas_acquire(DC, need, W)) return rc;
   const int slots = std::min(W, DC.n_arenas);
-  if (n > DC.batch_cap) {
-    HIPCHK(hipStreamSynchronize(st));
-    if (DC.d_descs) hipFree(DC.d_descs);
-    if (DC.d_order) hipFree(DC.d_order);
-    if (DC.d_results) hipFree(DC.d_results);
-    if (DC.d_off) hipFree(DC.d_off);
-    if (DC.d_len) hipFree(DC.d_len);
-    if (DC.h_results) hipHostFree(DC.h_results);
-    if (DC.h_offlen) hipHostFree(DC.h_offlen);
-    DC.d_descs = nullptr;
-    DC.d_order = nullptr;
-    DC.d_results = nullptr;
-    DC.d_off = nullptr;
-    DC.d_len = nullptr;
-    DC.h_results = nullptr;
-    DC.h_offlen = nullptr;
-    DC.batch_cap = 0;
-    HIPCHK(dalloc(&DC.d_descs, (size_t)n));
-    HIPCHK(dalloc(&DC.d_order, (size_t)n));
-    HIPCHK(dalloc(&DC.d_results, (size_t)n));
-    HIPCHK(dalloc(&DC.d_off, (size_t)n + 1));
-    HIPCHK(dalloc(&DC.d_len, (size_t)n));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_results), (size_t)n * sizeof(SearchResult)));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_offlen), ((size_t)n * 2 + 1) * sizeof(long long)));
-    DC.batch_cap = n;
-  }
+  if (int rc = batch_acquire(DC, n)) return rc;
   std::vector<PlannerDev> descs(n);
   for (int i = 0; i < n; ++i) {
     prepare_start(hs[i], vel[i], starts + 3 * i);
@@ -1631,79 +1725,132 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     for (ResumeArena& ra : cur) hipFree(ra.slab);
   }
   g_last_ms = ms_total;
-  int rc = HASTAR_OK;
-  // pack the paths that fit the caller's buffers: offsets, one gather kernel, one copy.
-  // Every planner reports its own outcome in stats[i].status: 0, HASTAR_EOVERFLOW (the
-  // search needed more device memory than it could get, or hit HASTAR_MAX_POPS_HARD),
-  // HASTAR_ENOSPC (kernel: path longer than the planner's output buffer; host: longer than
-  // `cap` — then len[i] is the length needed and hastar_copy_path fetches it).  The return
-  // code is the first ENOSPC, else the first EOVERFLOW.
-  long long* h_off = DC.h_offlen;
-  int* h_len = reinterpret_cast<int*>(DC.h_offlen + n + 1);
-  long long total = 0;
-  int rc_over = HASTAR_OK;
-  for (int i = 0; i < n; ++i) {
-    SearchResult& R = DC.h_results[i];
-    hastar_handle h = hs[i];
-    if (R.status == -75) R.ok = 0;
-    h->last = R;
-    h->have_last = true;
-    // longest-first key: the search's own duration (s_memrealtime ticks) — it weighs outer
-    // pops, inner A* pops and shots by what they actually cost, unlike a pop count
-    h->last_pops = R.t_end > R.t_start ? (long long)(R.t_end - R.t_start) : (long long)R.pops + R.astar_pops;
-    ok[i] = R.ok;
-    cost[i] = R.ok ? R.cost : FLT_MAX;
-    fill_stats(R, stats ? &stats[i] : nullptr);
-    len[i] = R.path_len;
-    if (R.status == -75 && rc_over == HASTAR_OK) {
-      rc_over = HASTAR_EOVERFLOW;
-      g_err = "search ended by an arena overflow (device memory) or HASTAR_MAX_POPS_HARD";
-    } else if (R.status == -28 && rc == HASTAR_OK) {
-      rc = fail(HASTAR_ENOSPC, "path longer than the planner's output buffer");
-    }
-    int take = R.path_len;
-    if (take > cap) {
-      take = 0;  // the caller fetches it with hastar_copy_path
-      if (stats) stats[i].status = HASTAR_ENOSPC;
-      if (rc == HASTAR_OK) rc = fail(HASTAR_ENOSPC, "path buffer too small");
-    }
-    h_off[i] = total;
-    h_len[i] = take;
-    total += take;
-  }
-  if (rc == HASTAR_OK && rc_over != HASTAR_OK) rc = rc_over;
-  h_off[n] = total;
-  DC.last_n = n;
-  DC.last_total = total;
-  if (total > 0) {
-    if ((size_t)total > DC.pts_cap) {
-      if (DC.d_pxyh) hipFree(DC.d_pxyh);
-      if (DC.d_pcurv) hipFree(DC.d_pcurv);
-      if (DC.h_pxyh) hipHostFree(DC.h_pxyh);
-      if (DC.h_pcurv) hipHostFree(DC.h_pcurv);
-      DC.d_pxyh = DC.d_pcurv = DC.h_pxyh = DC.h_pcurv = nullptr;
-      DC.pts_cap = 0;
-      const size_t c2 = (size_t)total + (size_t)total / 2 + 1024;
-      HIPCHK(dalloc(&DC.d_pxyh, c2 * 3));
-      HIPCHK(dalloc(&DC.d_pcurv, c2));
-      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_pxyh), c2 * 3 * sizeof(float)));
-      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_pcurv), c2 * sizeof(float)));
-      DC.pts_cap = c2;
-    }
-    HIPCHK(hipMemcpyAsync(DC.d_off, h_off, ((size_t)n + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(DC.d_len, h_len, (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
-    HIPCHK(launch_gather_paths(DC.d_descs, DC.d_off, DC.d_len, n, DC.d_pxyh, DC.d_pcurv, st));
-    HIPCHK(hipMemcpyAsync(DC.h_pxyh, DC.d_pxyh, (size_t)total * 3 * sizeof(float), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(DC.h_pcurv, DC.d_pcurv, (size_t)total * sizeof(float), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    for (int i = 0; i < n; ++i) {
-      if (h_len[i] == 0) continue;
-      std::memcpy(xyh + (size_t)i * cap * 3, DC.h_pxyh + 3 * h_off[i], (size_t)h_len[i] * 3 * sizeof(float));
-      std::memcpy(curv + (size_t)i * cap, DC.h_pcurv + h_off[i], (size_t)h_len[i] * sizeof(float));
-    }
-  }
-  return rc;
+  return finish_batch(DC, hs, n, xyh, curv, cap, len, cost, ok, stats, true);
 }
+
+}  // extern "C"
+
+// ---- RELAXED mode (hastar_relaxed.hip): non-parity by design ----
+namespace {
+size_t relax_bytes(int N, int nodes, RelaxArena* A, char* q) {
+  const size_t NN = (size_t)N * N;
+  const int bcap = 32 * N;
+  uint32_t slots = 1;
+  while (slots < 2u * (uint32_t)nodes + 64) slots <<= 1;
+  const int dub_cap = 4 * N + 64;  // Dubins samples of one shot (as ArenaReq::dub)
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = q ? q + off : nullptr;
+    off += align256(bytes);
+    return p;
+  };
+  char* dist = take(NN * 4);
+  char* done = take(((NN + 31) / 32) * 4);
+  char* bucket = take((size_t)4 * bcap * 4);
+  char* table = take((size_t)slots * sizeof(Slot3));
+  char* nodes_p = take((size_t)nodes * sizeof(Node3));
+  char* lists = take((size_t)3 * nodes * 8);
+  char* dxyh = take((size_t)relaxed_waves() * dub_cap * 12);
+  char* dcurv = take((size_t)relaxed_waves() * dub_cap * 4);
+  char* chain = take((size_t)(nodes + 2) * 4);
+  if (A) {
+    std::memset(A, 0, sizeof(*A));
+    A->dist = reinterpret_cast<float*>(dist);
+    A->done = reinterpret_cast<uint32_t*>(done);
+    A->bucket = reinterpret_cast<int*>(bucket);
+    A->bcap = bcap;
+    A->table = reinterpret_cast<Slot3*>(table);
+    A->tmask = slots - 1;
+    A->nodes = reinterpret_cast<Node3*>(nodes_p);
+    A->node_cap = nodes;
+    A->lists = reinterpret_cast<int*>(lists);
+    A->list_cap = nodes;
+    A->dub_xyh = reinterpret_cast<float*>(dxyh);
+    A->dub_curv = reinterpret_cast<float*>(dcurv);
+    A->dub_cap = dub_cap;
+    A->chain = reinterpret_cast<int*>(chain);
+    A->chain_cap = nodes + 2;
+    A->cells = NN;
+  }
+  return off;
+}
+int relax_acquire(DeviceCtx& D, int N, int nodes, int want) {
+  if (D.n_rarenas >= want && D.r_N >= N && D.r_nodes >= nodes) return 0;
+  HIPCHK(hipStreamSynchronize(D.stream));
+  if (D.rslab) hipFree(D.rslab);
+  if (D.d_rarenas) hipFree(D.d_rarenas);
+  D.rslab = nullptr;
+  D.d_rarenas = nullptr;
+  D.n_rarenas = 0;
+  N = std::max(N, D.r_N);
+  nodes = std::max(nodes, D.r_nodes);
+  const size_t per = relax_bytes(N, nodes, nullptr, nullptr);
+  size_t fr = 0, tot = 0;
+  HIPCHK(hipMemGetInfo(&fr, &tot));
+  const int n = (int)std::max<size_t>(1, std::min<size_t>((size_t)want, (size_t)(0.5 * (double)fr) / per));
+  if (hipMalloc(&D.rslab, per * (size_t)n) != hipSuccess) {
+    D.rslab = nullptr;
+    return fail(HASTAR_ENOMEM, "relaxed arenas: hipMalloc failed");
+  }
+  std::vector<RelaxArena> host(n);
+  for (int i = 0; i < n; ++i) relax_bytes(N, nodes, &host[i], static_cast<char*>(D.rslab) + per * (size_t)i);
+  HIPCHK(dalloc(&D.d_rarenas, (size_t)n));
+  HIPCHK(hipMemcpyAsync(D.d_rarenas, host.data(), (size_t)n * sizeof(RelaxArena), hipMemcpyHostToDevice, D.stream));
+  HIPCHK(hipStreamSynchronize(D.stream));
+  D.n_rarenas = n;
+  D.r_N = N;
+  D.r_nodes = nodes;
+  return 0;
+}
+}  // namespace
+
+extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, const float* vel, const float* starts,
+                                              float* xyh, float* curv, int cap, int* len, float* cost, int* ok,
+                                              hastar_stats* stats, const hastar_relaxed_opts* opts) {
+  if (!hs || n <= 0 || !vel || !starts || !len || !cost || !ok || cap < 0 || (cap > 0 && (!xyh || !curv)))
+    return fail(HASTAR_EINVAL, "bad argument");
+  const int dev = hs[0] ? hs[0]->device : -1;
+  int N = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!hs[i] || hs[i]->device != dev) return fail(HASTAR_EINVAL, "null handle or handles on different devices");
+    if (!hs[i]->goal_set) return fail(HASTAR_EINVAL, "update_goal must be called before find_path");
+    N = std::max(N, hs[i]->desc.N);
+  }
+  RelaxParams rp{};
+  rp.delta = opts && opts->delta > 0.0f ? opts->delta : 0.5f;
+  rp.h_stop = opts && opts->h_stop >= 1.0f ? opts->h_stop : 3.0f;
+  rp.max_rounds = opts && opts->max_rounds > 0 ? opts->max_rounds : (1 << 20);
+  rp.h_weight = opts && opts->h_weight > 0.0f ? opts->h_weight : 1.2f;
+  const int nodes = opts && opts->max_nodes > 0 ? opts->max_nodes : (1 << 20);
+  HIPCHK(hipSetDevice(dev));
+  DeviceCtx& DC = *hs[0]->dc;
+  std::lock_guard<std::mutex> lk(DC.mu);
+  hipStream_t st = DC.stream;
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, dev));
+  int want = std::min(n, prop.multiProcessorCount);  // one 8-wave workgroup per CU (230 VGPRs)
+  if (const char* e = std::getenv("HASTAR_RELAXED_GROUPS")) want = std::max(1, std::min(want, std::atoi(e)));
+  if (int rc = relax_acquire(DC, N, nodes, want)) return rc;
+  if (int rc = batch_acquire(DC, n)) return rc;
+  std::vector<PlannerDev> descs(n);
+  for (int i = 0; i < n; ++i) {
+    prepare_start(hs[i], vel[i], starts + 3 * i);
+    descs[i] = hs[i]->desc;
+    descs[i].result = DC.d_results + i;
+  }
+  HIPCHK(hipMemcpyAsync(DC.d_descs, descs.data(), (size_t)n * sizeof(PlannerDev), hipMemcpyHostToDevice, st));
+  HIPCHK(hipEventRecord(DC.ev0, st));
+  HIPCHK(launch_relaxed(DC.d_descs, n, DC.d_rarenas, std::min(want, DC.n_rarenas), DC.d_next, rp, st));
+  HIPCHK(hipEventRecord(DC.ev1, st));
+  HIPCHK(hipMemcpyAsync(DC.h_results, DC.d_results, (size_t)n * sizeof(SearchResult), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  float ms = 0.0f;
+  hipEventElapsedTime(&ms, DC.ev0, DC.ev1);
+  g_last_ms = ms;
+  return finish_batch(DC, hs, n, xyh, curv, cap, len, cost, ok, stats, false);
+}
+
+extern "C" {
 
 int hastar_copy_path(hastar_handle h, float* xyh, float* curv, int cap, int* len) {
   if (!h || !h->have_last) return fail(HASTAR_EINVAL, "no search result");

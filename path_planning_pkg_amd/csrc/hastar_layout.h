@@ -216,4 +216,34 @@ struct SlotArena {
   int* prevl;       // prev links of the LDS-resident A* tree nodes (A_CAP)
 };
 
+// Scratch of one planner in the RELAXED (non-parity) search mode (hastar_relaxed.hip,
+// SURVEY.md §8(f) rank 4): one workgroup per planner, so one arena per resident workgroup.
+//   dist    N*N backward 8-connected distance to the goal cell (the heuristic), float bits
+//           updated with atomicMin (non-negative floats order like their bit patterns)
+//   done    N*N/32 bitmap: cells the bucket Dijkstra has settled
+//   bucket  4 x bcap cell lists (a ring of Dial buckets of width act_cost_axis)
+//   table   best g per node key (open addressing; key 0xffffffff = empty)
+//   nodes   every node ever generated (Node3 records; prev = parent node index)
+//   lists   3 x list_cap lists of {f bits, node} (8 B): the open list, the next open list
+//           and the round's expansion set (node indices only)
+//   dub_*   one Dubins-shot scratch of dub_cap samples per wave
+//   chain   path reconstruction scratch
+struct RelaxArena {
+  float* dist;      uint32_t* done;
+  int* bucket;      int bcap;       int pad0;
+  Slot3* table;     uint32_t tmask; int pad1;
+  Node3* nodes;     int node_cap;   int pad2;
+  int* lists;       int list_cap;   int pad3;
+  float* dub_xyh;   float* dub_curv; int dub_cap; int pad4;
+  int* chain;       int chain_cap;  int pad5;
+  size_t cells;     // N*N served
+};
+// options of a relaxed launch (kernel side of hastar_relaxed_opts)
+struct RelaxParams {
+  float delta;      // frontier width (m): every open node with f <= min f + delta is expanded in a round
+  float h_stop;     // the Dijkstra stops at h_stop x dist(start) + 64 buckets (cells beyond get that bound)
+  int max_rounds;
+  float h_weight;   // f = g + h_weight x max(h, Dubins length) (1: the reference's f)
+};
+
 }  // namespace hastar

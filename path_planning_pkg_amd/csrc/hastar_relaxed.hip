@@ -1,0 +1,525 @@
+// hastar_relaxed.hip — the RELAXED search mode: a frontier-parallel
+// Hybrid A* with a backward-Dijkstra heuristic, for one planner per workgroup.
+//
+// NOT bit-exact with the reference, on purpose.  The exact mode (hastar_search_kernel) keeps
+// the reference's sequential pop order (HybridAStar.cpp:107-194) and its lazy per-cell A*
+// heuristic (AStar.cpp:118-186), which leaves one wavefront per query.  This mode trades that
+// order for parallelism inside one query:
+//   1. heuristic: the 8-connected (4 when diag is off) grid distance to the goal cell over the
+//      traversable cells, i.e. the converged value of the reference's lazy A* for every cell
+//      at once (Grid2D.cpp:219-316 move costs act_cost_axis / act_cost_diag), computed by a
+//      Dial-bucket Dijkstra: buckets of width act_cost_axis (the smallest move), so every move
+//      leaves its bucket and a whole bucket is settled in parallel by the workgroup;
+//   2. search: Δ-stepping over f.  Each round expands EVERY open node with f <= min f + delta,
+//      one wavefront per node (the same fused successor / APF / Dubins-length code as the
+//      exact kernel: VehicleModel.cpp:63-105, Grid3D.cpp:47-74, 206-227, Dubins.cpp:19-69);
+//      duplicates are resolved by a best-g table per node key (atomicMin), not a closed set;
+//   3. termination as in the reference: the goal cell is reached (Node3D::operator==,
+//      Node3D.h:42) or an analytic Dubins shot is collision-free (HybridAStar.cpp:115-154,
+//      the same interval / decay schedule counted over the workgroup's expansions); the
+//      cheapest candidate of the round in which the first one appears wins;
+//   4. reconstruction and output format as the exact mode (HybridAStar.cpp:208-262).
+// Costs keep the reference's definitions (g = action costs + APF field, f = g + max(h, Dubins
+// length)), so results are comparable: tests check validity (collision-free, continuous, ends at
+// start and goal) and report the cost ratio against the exact mode, not bit parity.
+#include <hip/hip_runtime.h>
+
+#include "hastar_device.h"
+#include "hastar_kernels.h"
+
+namespace hastar {
+
+constexpr int RW = 8;                        // wavefronts per planner workgroup
+constexpr uint32_t EMPTY_KEY = 0xffffffffu;  // no node key has all bits set (x < 4096, bin < 256 with y < 4096)
+
+// L1-bypassing loads of words other waves update with atomics
+__device__ __forceinline__ uint32_t ld_sync(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_dist(const float* d, size_t c) {
+  return __uint_as_float(ld_sync(reinterpret_cast<const uint32_t*>(d) + c));
+}
+__device__ __forceinline__ void block_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ uint32_t rx_hash(uint32_t k) {
+  k ^= k >> 16;
+  k *= 0x7feb352dU;
+  k ^= k >> 15;
+  k *= 0x846ca68bU;
+  return k ^ (k >> 16);
+}
+// best-g table: lower the key's g to gbits; true when gbits is the new best.  *full is set
+// when the table has no room left.
+__device__ __forceinline__ bool table_lower(const RelaxArena& A, uint32_t key, uint32_t gbits, bool* full) {
+  uint32_t h = rx_hash(key) & A.tmask;
+  for (uint32_t probe = 0; probe <= A.tmask; ++probe) {
+    Slot3* s = &A.table[h];
+    uint32_t k = ld_sync(&s->key);
+    if (k == EMPTY_KEY) {
+      const uint32_t prev = atomicCAS(&s->key, EMPTY_KEY, key);
+      k = prev == EMPTY_KEY ? key : prev;
+    }
+    if (k == key) return atomicMin(&s->gi, gbits) > gbits;
+    h = (h + 1) & A.tmask;
+  }
+  *full = true;
+  return false;
+}
+__device__ __forceinline__ uint32_t table_best(const RelaxArena& A, uint32_t key) {
+  uint32_t h = rx_hash(key) & A.tmask;
+  for (uint32_t probe = 0; probe <= A.tmask; ++probe) {
+    const uint32_t k = ld_sync(&A.table[h].key);
+    if (k == key) return ld_sync(&A.table[h].gi);
+    if (k == EMPTY_KEY) break;
+    h = (h + 1) & A.tmask;
+  }
+  return 0xffffffffu;
+}
+
+struct RelaxShared {
+  ApfStage apf[RW];
+  int planner;
+  int cnt[4];               // Dijkstra bucket fill counts (ring)
+  int overflow, hover;
+  int stop_at;              // last bucket the Dijkstra settles (-1: start not settled yet)
+  int settled;              // cells settled (diagnostic: astar_pops)
+  int nA, nB, nE, eNext, nodes;
+  uint32_t fmin, fnext;     // float bits of the open list's min f, and of the next open list's
+  unsigned long long best;  // cheapest solution candidate: f bits << 32 | tag
+  int since_shot, interval;
+  int pops, succ, shots, rounds;
+  int shot_term[RW], shot_n[RW], shot_done[RW];
+};
+
+// Phase 1: Dial-bucket Dijkstra from the goal cell; returns the heuristic bound of cells the
+// early stop left unsettled (every such cell is at least that far).
+__device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, const RelaxParams& rp) {
+  const int tid = threadIdx.x, NT = blockDim.x;
+  const int N = P.N;
+  const float wb = P.act_cost_axis;
+  const float cd = P.act_cost_diag;
+  const int nact = P.diag ? 8 : 4;
+  uint32_t* dist = reinterpret_cast<uint32_t*>(A.dist);
+  const size_t goal = (size_t)P.goal_cx * N + P.goal_cy;
+  const size_t start = (size_t)P.start_cx * N + P.start_cy;
+  if (tid == 0) {
+    dist[goal] = 0u;
+    A.bucket[0] = (int)goal;
+    S.cnt[0] = 1;
+    S.cnt[1] = S.cnt[2] = S.cnt[3] = 0;
+    S.overflow = 0;
+    S.stop_at = -1;
+    S.settled = 0;
+  }
+  block_sync();
+  const int max_b = 4 * N + 64;
+  int cur = 0;
+  for (; cur < max_b; ++cur) {
+    const int slot = cur & 3;
+    const int m = min(S.cnt[slot], A.bcap);
+    const int live = S.cnt[0] | S.cnt[1] | S.cnt[2] | S.cnt[3];
+    const int stop_at = S.stop_at;
+    block_sync();
+    if (live == 0 || (stop_at >= 0 && cur > stop_at)) break;
+    int settled = 0;
+    for (int e = tid; e < m; e += NT) {
+      const int c = A.bucket[(size_t)slot * A.bcap + e];
+      const uint32_t bit = 1u << (c & 31);
+      if (atomicOr(&A.done[c >> 5], bit) & bit) continue;  // settled from an earlier entry
+      ++settled;
+      if ((size_t)c == start) atomicCAS(&S.stop_at, -1, cur + (int)((rp.h_stop - 1.0f) * (float)cur) + 64);
+      if ((size_t)c != goal && gp(P.occ)[c] >= P.thr) continue;  // not enterable: no move leads through it
+      const float d = __uint_as_float(ld_sync(&dist[c]));
+      const int ci = c / N, cj = c - ci * N;
+      for (int a = 0; a < nact; ++a) {
+        // the 8 moves (Grid2D.cpp:22-40), axis moves first
+        const int di = a < 4 ? ((a & 1) ? 0 : (a == 0 ? 1 : -1)) : ((a & 1) ? 1 : -1);
+        const int dj = a < 4 ? ((a & 1) ? (a == 1 ? 1 : -1) : 0) : ((a & 2) ? 1 : -1);
+        const int pi = ci + di, pj = cj + dj;
+        if (pi < 0 || pi >= N || pj < 0 || pj >= N) continue;
+        const float nd = d + (a < 4 ? wb : cd);
+        const size_t p = (size_t)pi * N + pj;
+        const uint32_t nb = __float_as_uint(nd);
+        if (atomicMin(&dist[p], nb) <= nb) continue;
+        int kb = (int)(nd / wb);
+        kb = max(kb, cur + 1);
+        kb = min(kb, cur + 3);
+        const int pos = atomicAdd(&S.cnt[kb & 3], 1);
+        if (pos < A.bcap) A.bucket[(size_t)(kb & 3) * A.bcap + pos] = (int)p;
+        else S.overflow = 1;
+      }
+    }
+    if (settled) atomicAdd(&S.settled, settled);
+    block_sync();
+    if (tid == 0) S.cnt[slot] = 0;
+    block_sync();
+  }
+  return (float)cur * wb;
+}
+
+// One expansion by one wavefront: the exact kernel's fused successor block without the
+// closed set and the lazy A* (the heuristic is the Dijkstra field).
+__device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, ApfStage& apfs,
+                               const GoalC& GC, float hlim, float hw, int idx, int wv, int lane, uint2* list_b) {
+  const Node3 cur = gload(&A.nodes[idx]);
+  const uint32_t key = ufu(cur.key);
+  const float cg = uff(cur.g), cxp = uff(cur.x), cyp = uff(cur.y), chd = uff(cur.h), cvm = uff(cur.vmin);
+  if (__float_as_uint(cg) > table_best(A, key)) return;  // a cheaper node of this key was generated since
+  const int cci = ufi((int)(cur.cc >> 8));
+  const int cx = key3_x(key), cy = key3_y(key), cbin = key3_bin(key);
+  int pop_no = 0;
+  if (lane == 0) pop_no = atomicAdd(&S.pops, 1) + 1;
+  // goal test (Node3D::operator==: the cell only, Node3D.h:42)
+  if (cx == P.goal_cx && cy == P.goal_cy) {
+    if (lane == 0) atomicMin(&S.best, ((unsigned long long)__float_as_uint(cg) << 32) | (unsigned)idx);
+    return;
+  }
+  // Dubins shot (HybridAStar.cpp:115-154): the reference's interval/decay schedule over the
+  // workgroup's expansions; a wave that found a free shot keeps its samples and shoots no more
+  const bool allowed = cvm < 1.0f;
+  int shoot = 0;
+  if (lane == 0 && allowed && !S.shot_done[wv]) {
+    const int k = atomicAdd(&S.since_shot, 1) + 1;
+    if (k >= S.interval && atomicExch(&S.since_shot, 0) >= S.interval) shoot = 1;
+  }
+  (void)pop_no;
+  if (ufi(shoot)) {
+    if (lane == 0) {
+      atomicAdd(&S.shots, 1);
+      S.interval = max(S.interval - P.shot_decay, 50);
+    }
+    int word = 0;
+    float prm[4];
+    const float r = P.r_min;
+    const float L = dubins_shortest(r, cxp, cyp, chd, P.goal_x, P.goal_y, P.goal_h, &word, prm);
+    const Centres C = dubins_centres(r, cxp, cyp, chd, P.goal_x, P.goal_y, P.goal_h);
+    GAS float* xyh = gp(A.dub_xyh) + (size_t)wv * A.dub_cap * 3;
+    GAS float* curv = gp(A.dub_curv) + (size_t)wv * A.dub_cap;
+    const int n = dubins_sample(P, C, word, prm, xyh, curv, A.dub_cap, lane);
+    wave_lds_sync();
+    const bool first_arc_long = fabsf(prm[1]) > (float)M_PI_2;
+    if (n > 0 && !first_arc_long && path_is_free(P, xyh, n, lane)) {
+      if (lane == 0) {
+        S.shot_done[wv] = 1;
+        S.shot_term[wv] = ufi(cur.prev);
+        S.shot_n[wv] = n;
+        atomicMin(&S.best, ((unsigned long long)__float_as_uint(cg + L) << 32) | 0x80000000u | (unsigned)wv);
+      }
+      return;
+    }
+  }
+  // successors (VehicleModel.cpp:63-105) in groups of gs lanes, as in the exact kernel
+  const int span = 2 * P.na + 1;
+  const int gsh = span <= 4 ? 4 : 2, gs = 1 << gsh;
+  int lo = cci - P.na;
+  lo = lo < 0 ? 0 : lo;
+  const int ca = lane >> gsh, sub = lane & (gs - 1);
+  const int ai = lo + ca;
+  bool cand = ca < span && ai < P.nsteer;
+  const int ia = cand ? ai : lo;
+  const float cabs = gp(P.curv_abs)[ia];
+  const GAS float* ofs = &gp(P.off)[2 * ((size_t)ia * (P.bins + 1) + cbin)];
+  const float ofx = ofs[0], ofy = ofs[1], odth = gp(P.dth)[ia], oact = gp(P.act_cost)[ia];
+  float vm = 0.0f;
+  if (cand && !allowed) {
+    const float lat = cvm * cabs;
+    if (lat > P.a_lat) cand = false;
+    const float al = (float)sqrt(1.0 - (double)((lat * lat) / P.a_lat2));
+    vm = cvm - 2.0f * al * P.ts;
+  }
+  float sx = 0.0f, sy = 0.0f, sh = 0.0f, sg = 0.0f;
+  int sbin = 0, scx = 0, scy = 0;
+  bool inb = false;
+  if (cand) {
+    sx = cxp + ofx;
+    sy = cyp + ofy;
+    sh = wrap_pi_f(chd + odth);
+    sg = cg + oact;
+    sbin = heading_bin(sh, P.prec);
+    scx = trunc_f(sx / P.res);
+    scy = trunc_f(sy / P.res);
+    inb = scx > -1 && scx < P.N && scy > -1 && scy < P.N;
+  }
+  const bool lead = inb && sub == 0;
+  float occv = 0.0f, h2 = 0.0f;
+  if (lead) {
+    const size_t cell = (size_t)scx * P.N + scy;
+    occv = gp(P.occ)[cell];
+    h2 = ld_dist(A.dist, cell);
+    // unsettled cells (beyond the Dijkstra's early stop, or enclosed) are at least hlim away
+    if (!(h2 < hlim)) h2 = hlim;
+  }
+  const float dub = cand_dubins(P.r_min, GC, P.goal_h, sx, sy, sh, gs, lane);
+  const float fc = apf_fused(P, apfs, cxp, cyp, sx, sy, sh, __ballot(lead), gs, lane);
+  const bool kept = lead && occv < P.thr;
+  const uint64_t km = __ballot(kept);
+  if (lane == 0) atomicAdd(&S.succ, __popcll(km));
+  if (kept) {
+    const float g = sg + fc;  // Grid3D.cpp:66-69
+    const float f = g + hw * stl_max(h2, dub);
+    const uint32_t skey = key3(scx, scy, sbin);
+    bool full = false;
+    if (table_lower(A, skey, __float_as_uint(g), &full)) {
+      const int n = atomicAdd(&S.nodes, 1);
+      const int pos = atomicAdd(&S.nB, 1);
+      if (n < A.node_cap && pos < A.list_cap) {
+        Node3 d;
+        d.key = skey;
+        d.f = f;
+        d.l = NIL;
+        d.r = NIL;
+        d.p = NIL;
+        d.cc = (uint32_t)(lo + ca) << 8;
+        d.g = g;
+        d.vmin = vm;
+        d.x = sx;
+        d.y = sy;
+        d.h = sh;
+        d.prev = idx;
+        gstore(&A.nodes[n], d);
+        list_b[pos] = make_uint2(__float_as_uint(f), (uint32_t)n);
+        atomicMin(&S.fnext, __float_as_uint(f));
+      } else {
+        S.overflow = 1;
+      }
+    }
+    if (full) S.overflow = 1;
+  }
+}
+
+__device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, const RelaxParams& rp) {
+  const int tid = threadIdx.x, NT = blockDim.x, wv = tid >> 6, lane = tid & 63;
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  const size_t NN = (size_t)P.N * P.N;
+  // ---- clear: distances to +inf, settled flags, best-g table
+  {
+    uint32_t* dist = reinterpret_cast<uint32_t*>(A.dist);
+    for (size_t i = tid; i < NN; i += NT) dist[i] = 0x7f800000u;
+    const size_t words = (NN + 31) / 32;
+    for (size_t i = tid; i < words; i += NT) A.done[i] = 0u;
+    for (size_t i = tid; i <= A.tmask; i += NT) {
+      A.table[i].key = EMPTY_KEY;
+      A.table[i].gi = 0xffffffffu;
+    }
+  }
+  block_sync();
+  const float hlim = relaxed_heuristic(P, A, S, rp);
+  // ---- the frontier-parallel search
+  apf_stage(P, S.apf[wv], lane);
+  const GoalC GC = goal_centres(P.r_min, P.goal_x, P.goal_y, P.goal_h);
+  if (tid == 0) {
+    Node3 s0;
+    s0.key = key3(P.start_cx, P.start_cy, P.start_bin);
+    float h0 = ld_dist(A.dist, (size_t)P.start_cx * P.N + P.start_cy);
+    if (!(h0 < hlim)) h0 = hlim;
+    s0.f = h0;
+    s0.l = s0.r = s0.p = NIL;
+    s0.cc = (uint32_t)P.start_ci << 8;
+    s0.g = 0.0f;
+    s0.vmin = P.start_vmin;
+    s0.x = P.start_x;
+    s0.y = P.start_y;
+    s0.h = P.start_h;
+    s0.prev = NIL;
+    gstore(&A.nodes[0], s0);
+    bool full = false;
+    table_lower(A, s0.key, 0u, &full);
+    reinterpret_cast<uint2*>(A.lists)[0] = make_uint2(__float_as_uint(s0.f), 0u);
+    S.nA = 1;
+    S.nB = 0;
+    S.nE = 0;
+    S.eNext = 0;
+    S.nodes = 1;
+    S.best = ~0ull;
+    S.since_shot = 0;
+    S.interval = P.shot_interval;
+    S.pops = S.succ = S.shots = S.rounds = 0;
+    S.fmin = __float_as_uint(s0.f);
+    S.fnext = 0x7f800000u;
+    S.hover = S.overflow;  // a bucket overflow only weakens the heuristic: reported, not fatal
+    S.overflow = 0;
+  }
+  if (lane == 0) {
+    S.shot_done[wv] = 0;
+    S.shot_n[wv] = 0;
+    S.shot_term[wv] = NIL;
+  }
+  block_sync();
+  int a = 0;  // lists[a]: open list, lists[(a + 1) % 3]: next open list, lists[(a + 2) % 3]: expansion set
+  int status = 0;
+  for (int round = 0;; ++round) {
+    // open-list entries are {f bits, node}: the split streams 8-B entries, not node records
+    uint2* LA = reinterpret_cast<uint2*>(A.lists) + (size_t)a * A.list_cap;
+    uint2* LB = reinterpret_cast<uint2*>(A.lists) + (size_t)((a + 1) % 3) * A.list_cap;
+    int* LE = reinterpret_cast<int*>(reinterpret_cast<uint2*>(A.lists) + (size_t)((a + 2) % 3) * A.list_cap);
+    const int nA = S.nA;
+    const float thr = __uint_as_float(S.fmin) + rp.delta;
+    if (nA == 0 || S.best != ~0ull) break;
+    if (round >= rp.max_rounds || S.overflow) {
+      status = -75;
+      break;
+    }
+    // split: f <= min f + delta is expanded this round, the rest waits (its min f kept)
+    uint32_t fm = 0x7f800000u;
+    for (int e = tid; e < nA; e += NT) {
+      const uint2 en = LA[e];
+      if (__uint_as_float(en.x) <= thr) {
+        LE[atomicAdd(&S.nE, 1)] = (int)en.y;
+      } else {
+        LB[atomicAdd(&S.nB, 1)] = en;
+        fm = min(fm, en.x);
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) fm = min(fm, (uint32_t)__shfl_xor((int)fm, o, 64));
+    if (lane == 0 && fm != 0x7f800000u) atomicMin(&S.fnext, fm);
+    block_sync();
+    const int nE = S.nE;
+    // one wavefront per expanded node
+    for (;;) {
+      int e = 0;
+      if (lane == 0) e = atomicAdd(&S.eNext, 1);
+      e = ufi(e);
+      if (e >= nE) break;
+      relaxed_expand(P, A, S, S.apf[wv], GC, hlim, rp.h_weight, LE[e], wv, lane, LB);
+    }
+    block_sync();
+    if (tid == 0) {
+      S.nA = min(S.nB, A.list_cap);
+      S.nB = 0;
+      S.nE = 0;
+      S.eNext = 0;
+      S.fmin = S.fnext;
+      S.fnext = 0x7f800000u;
+      S.rounds = round + 1;
+    }
+    block_sync();
+    a = (a + 1) % 3;  // the next open list becomes the open list; the old open list is free
+  }
+  block_sync();
+  // ---- result and reconstruction (HybridAStar.cpp:208-262, as the exact kernel), by wave 0
+  const unsigned long long best = S.best;
+  const bool found = best != ~0ull && status == 0;
+  if (wv == 0) {
+    int ok = found ? 1 : 0, via_shot = 0, terminal = NIL, dub_n = 0, sw = 0;
+    float cost = FLT_MAX;
+    if (found) {
+      const uint32_t tag = (uint32_t)best;
+      cost = __uint_as_float((uint32_t)(best >> 32));
+      if (tag & 0x80000000u) {
+        via_shot = 1;
+        sw = (int)(tag & 0xffu);
+        terminal = S.shot_term[sw];
+        dub_n = S.shot_n[sw];
+      } else {
+        terminal = (int)tag;
+      }
+    }
+    int path_len = 0;
+    if (ok) {
+      int L = 0;
+      for (int i = terminal; i != NIL; i = A.nodes[i].prev) {
+        if (dub_n + L >= P.out_cap || L >= A.chain_cap) {
+          status = -28;
+          break;
+        }
+        if (lane == 0) A.chain[L] = i;
+        ++L;
+      }
+      wave_lds_sync();
+      if (status == 0) {
+        const GAS float* dxyh = gp(A.dub_xyh) + (size_t)sw * A.dub_cap * 3;
+        const GAS float* dcurv = gp(A.dub_curv) + (size_t)sw * A.dub_cap;
+        const float cs = P.rot_c, sn = P.rot_s, ang = -P.grid_heading;
+        path_len = dub_n + L;
+        for (int k = lane; k < path_len; k += 64) {
+          float px, py, ph, kc = 0.0f;
+          bool has_curv = true;
+          if (k < dub_n) {
+            const int q = dub_n - 1 - k;
+            px = dxyh[3 * q];
+            py = dxyh[3 * q + 1];
+            ph = dxyh[3 * q + 2];
+            kc = dcurv[q];
+          } else {
+            const int m = k - dub_n;
+            const Node3 nd = gload(&A.nodes[A.chain[m]]);
+            px = nd.x;
+            py = nd.y;
+            ph = nd.h;
+            kc = gp(P.curv_abs)[nd.cc >> 8];
+            has_curv = (m < L - 1);
+          }
+          const float x0 = px - P.goal_x, y0 = py - P.goal_y;
+          float xr = x0 * cs + y0 * sn;
+          float yr = -x0 * sn + y0 * cs;
+          const float hr = wrap_pi_f(ph - ang);
+          xr += P.world_goal_x;
+          yr += P.world_goal_y;
+          gp(P.out_xyh)[3 * k] = xr;
+          gp(P.out_xyh)[3 * k + 1] = yr;
+          gp(P.out_xyh)[3 * k + 2] = hr;
+          if (has_curv) gp(P.out_curv)[k + 1] = kc;
+        }
+        if (lane == 0) gp(P.out_curv)[0] = 0.0f;
+      } else {
+        ok = 0;
+      }
+    }
+    if (lane == 0) {
+      SearchResult* R = P.result;
+      R->pops = S.pops;
+      R->successors = S.succ;
+      R->astar_pops = S.settled;      // cells the Dijkstra settled
+      R->astar_searches = 1;
+      R->shots = S.shots;
+      R->closed_size = min(S.nodes, A.node_cap);  // nodes generated
+      R->pop_digest = (unsigned long long)S.rounds;
+      R->closed_digest = 0;
+      R->ok = ok;
+      R->via_shot = via_shot;
+      R->status = status;
+      R->path_len = ok ? path_len : 0;
+      R->cost = ok ? cost : FLT_MAX;
+      R->terminal = terminal;
+      R->dubins_len = dub_n;
+      R->astar_migrations = S.hover;  // 1: the Dijkstra's bucket ring overflowed
+      R->astar_pops_hbm = 0;
+      R->t_start = t_start;
+      R->t_end = __builtin_amdgcn_s_memrealtime();
+      R->slot = (int)blockIdx.x;
+      R->parks = 0;
+    }
+  }
+  block_sync();
+}
+
+// Persistent: grid = resident relaxed arenas; each workgroup pulls planners from *next.
+__global__ __launch_bounds__(RW * 64) void k_relaxed_search(const PlannerDev* __restrict__ descs, int n,
+                                                           const RelaxArena* __restrict__ arenas, int* next,
+                                                           RelaxParams rp) {
+  __shared__ RelaxShared S;
+  const RelaxArena A = arenas[blockIdx.x];
+  for (;;) {
+    if (threadIdx.x == 0) S.planner = atomicAdd(next, 1);
+    block_sync();
+    const int pi = S.planner;
+    block_sync();
+    if (pi >= n) break;
+    relaxed_one(descs[pi], A, S, rp);
+  }
+}
+
+hipError_t launch_relaxed(const PlannerDev* d_descs, int n, const RelaxArena* d_arenas, int n_arenas, int* d_next,
+                          const RelaxParams& rp, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(d_next, 0, sizeof(int), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_relaxed_search, dim3(n_arenas), dim3(RW * 64), 0, st, d_descs, n, d_arenas, d_next, rp);
+  return hipGetLastError();
+}
+int relaxed_waves() { return RW; }
+
+}  // namespace hastar

@@ -13,7 +13,7 @@ from pathlib import Path
 
 import numpy as np
 
-from .capi import HastarStats, PlannerConfig, fptr, iptr
+from .capi import HastarRelaxedOpts, HastarStats, PlannerConfig, fptr, iptr
 
 import os
 
@@ -51,6 +51,8 @@ def load_library():
     L.hastar_copy_path.argtypes = [vp, fp, fp, C.c_int, ip]
     L.hastar_find_path_batch.argtypes = [C.POINTER(C.c_void_p), C.c_int, fp, fp, fp, fp, C.c_int, ip, fp, ip,
                                          C.POINTER(HastarStats)]
+    L.hastar_find_path_relaxed_batch.argtypes = [C.POINTER(C.c_void_p), C.c_int, fp, fp, fp, fp, C.c_int, ip, fp,
+                                                 ip, C.POINTER(HastarStats), C.POINTER(HastarRelaxedOpts)]
     L.hastar_get_obstacles.argtypes = [vp, fp]
     L.hastar_grid_size.argtypes = [vp]
     L.hastar_set_row_window.argtypes = [vp, C.c_int, C.c_int]
@@ -488,8 +490,10 @@ def find_path_batch_arrays(planners, vels, starts, cap=4096, buffers=None):
     return BatchResult(b.cost, b.ok, b.ln, b.xyh, b.curv, b.st, float(L.hastar_last_search_ms()), planners)
 
 
-def find_path_batch(planners, vels, starts, cap=4096):
-    """hastar_find_path_batch: one launch, one wavefront per planner."""
+def find_path_batch(planners, vels, starts, cap=4096, relaxed=None):
+    """hastar_find_path_batch: one launch, one wavefront per planner.  relaxed: None for the
+    exact mode, else a dict of hastar_relaxed_opts fields (may be empty) for the non-parity
+    frontier-parallel mode (hastar_find_path_relaxed_batch, one workgroup per planner)."""
     L = load_library()
     n = len(planners)
     hs = (C.c_void_p * n)(*[p.h.value for p in planners])
@@ -501,8 +505,13 @@ def find_path_batch(planners, vels, starts, cap=4096):
     ok = np.zeros(n, np.int32)
     cost = np.zeros(n, np.float32)
     stats = (HastarStats * n)()
-    rc = L.hastar_find_path_batch(hs, n, fptr(v), fptr(s), fptr(xyh), fptr(curv), cap, iptr(ln), fptr(cost),
-                                  iptr(ok), stats)
+    if relaxed is None:
+        rc = L.hastar_find_path_batch(hs, n, fptr(v), fptr(s), fptr(xyh), fptr(curv), cap, iptr(ln), fptr(cost),
+                                      iptr(ok), stats)
+    else:
+        opts = HastarRelaxedOpts(**relaxed)
+        rc = L.hastar_find_path_relaxed_batch(hs, n, fptr(v), fptr(s), fptr(xyh), fptr(curv), cap, iptr(ln),
+                                              fptr(cost), iptr(ok), stats, C.byref(opts))
     if rc not in (HASTAR_EOVERFLOW, HASTAR_ENOSPC):  # per-planner outcomes are in stats[i]["status"]
         _check(rc)
     ms = float(L.hastar_last_search_ms())

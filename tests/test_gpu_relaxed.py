@@ -1,0 +1,140 @@
+"""The RELAXED search mode (hastar_find_path_relaxed_batch).
+
+This mode is NOT bit-exact with the reference by design (frontier-parallel rounds and a
+backward-Dijkstra heuristic instead of the sequential pop order and the lazy A*), so the bar
+here is validity plus a cost comparison, not parity:
+  * it succeeds on every case where the exact mode (== the oracle) succeeds;
+  * the path starts at the goal end and ends at the start pose (the reference's order), every
+    pose lies on a free cell of the planner's own map, consecutive poses are at most one motion
+    primitive (or one Dubins sample step) apart, headings are wrapped to (-pi, pi];
+  * the reported cost is within a stated factor of the exact mode's (printed per case);
+  * running it leaves the exact mode's state alone: an exact search afterwards still equals the
+    oracle bit for bit (the relaxed mode neither reads nor writes the node-map memo).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from tests.scenarios import drive, replan_pairs, synthetic
+from tests.test_gpu_parity import compare_results
+
+pytestmark = pytest.mark.gpu
+
+COST_FACTOR = 1.5  # relaxed cost / exact cost bound asserted per case (the measured ratios are printed)
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    from path_planning_pkg_amd import planner
+    planner.load_library()
+    return planner
+
+
+def world_to_grid(xyh, goal, start, N, res):
+    """Inverse of the reconstruction's rotate-back (HybridAStar.cpp:208-262): grid-frame x, y."""
+    gh = math.atan2(goal[1] - start[1], goal[0] - start[0])
+    dx = xyh[:, 0].astype(np.float64) - goal[0]
+    dy = xyh[:, 1].astype(np.float64) - goal[1]
+    x0 = math.cos(gh) * dx + math.sin(gh) * dy
+    y0 = -math.sin(gh) * dx + math.cos(gh) * dy
+    # the goal cell is (round(0.8 N), N / 2) (Grid2D ctor, Grid2D.cpp:7-62)
+    return x0 + int(round(N * 0.8)) * res, y0 + (N // 2) * res
+
+
+def check_valid(r, occ, thr, proto, N, res, max_step, what):
+    path = r["path"]
+    assert r["ok"] and len(path) >= 2, f"{what}: no path"
+    s = np.asarray(proto["start"], np.float64)
+    assert np.hypot(*(path[-1, :2] - s[:2])) < 1e-2, f"{what}: path does not end at the start"
+    g = np.asarray(proto["goal"], np.float64)
+    assert np.hypot(*(path[0, :2] - g[:2])) < 2.0 * res, f"{what}: path does not begin at the goal"
+    gx, gy = world_to_grid(path, proto["goal"], proto["start"], N, res)
+    ci, cj = np.floor(gx / res + 1e-6).astype(int), np.floor(gy / res + 1e-6).astype(int)
+    ri, rj = np.rint(gx / res).astype(int), np.rint(gy / res).astype(int)
+    inside = (ci >= 0) & (ci < N) & (cj >= 0) & (cj < N)
+    assert inside.all(), f"{what}: pose outside the grid"
+    free_t = occ[ci, cj] < thr
+    rin = (ri >= 0) & (ri < N) & (rj >= 0) & (rj < N)
+    free_r = np.zeros_like(free_t)
+    free_r[rin] = occ[ri[rin], rj[rin]] < thr
+    assert (free_t | free_r).all(), f"{what}: {(~(free_t | free_r)).sum()} poses on occupied cells"
+    steps = np.hypot(np.diff(path[:, 0]), np.diff(path[:, 1]))
+    assert steps.max() <= max_step, f"{what}: a gap of {steps.max():.3f} m > {max_step:.3f}"
+    assert (np.abs(path[:, 2]) <= math.pi + 1e-5).all()
+
+
+def _run_case(gpu, oracle_lib, cases, tag, relaxed=None):
+    gs, os_ = [], []
+    for cfg, proto in cases:
+        g, o = gpu.HybridAStar(cfg), oracle_lib.OraclePlanner(cfg)
+        drive(g, proto)
+        drive(o, proto)
+        gs.append(g)
+        os_.append(o)
+    vels = [p["vel"] for _, p in cases]
+    starts = [p["start"] for _, p in cases]
+    rel, ms_rel = gpu.find_path_batch(gs, vels, starts, cap=16384, relaxed=relaxed or {})
+    # the exact mode afterwards: untouched by the relaxed run, still the oracle's
+    ex, ms_ex = gpu.find_path_batch(gs, vels, starts, cap=16384)
+    ratios = []
+    for i, ((cfg, proto), g, o) in enumerate(zip(cases, gs, os_)):
+        ro = o.find_path(proto["vel"], proto["start"])
+        compare_results(ex[i], ro, f"{tag} {i}: exact mode after a relaxed run")
+        r = rel[i]
+        assert r["stats"]["status"] == 0, f"{tag} {i}: relaxed status {r['stats']['status']}"
+        if ro["ok"]:
+            N, res = cfg.values["grid_size"], cfg.values["grid_resolution"]
+            p = cfg.values["obstacle_threshold"]
+            thr = np.float32(math.log(p / (1.0 - p)))
+            # gaps: at most one motion primitive (as in the exact path) or, where the Dubins
+            # sampling floors its segment counts (Dubins.cpp:326-563), under two sample steps —
+            # three where a floored segment has no sample at all
+            ex_gap = float(np.hypot(np.diff(ro["path"][:, 0]), np.diff(ro["path"][:, 1])).max())
+            max_step = max(1.05 * ex_gap, 3.0 * cfg.values["step_size"]) + 1e-3
+            check_valid(r, g.get_obstacles(), thr, proto, N, res, max_step, f"{tag} {i}")
+            ratios.append(r["cost"] / ro["cost"])
+            assert r["cost"] <= COST_FACTOR * ro["cost"], f"{tag} {i}: cost {r['cost']} vs exact {ro['cost']}"
+    print(f"{tag}: relaxed {ms_rel:.2f} ms vs exact {ms_ex:.2f} ms; cost ratios "
+          f"{[round(x, 3) for x in ratios]}; rounds {[r['stats']['pop_digest'] for r in rel]}; "
+          f"expansions {[r['stats']['pops'] for r in rel]} vs exact {[r['stats']['pops'] for r in ex]}")
+    return rel, ex
+
+
+@pytest.mark.parametrize("N,bins,K,seeds", [(256, 36, 40, (1, 2, 3, 4)), (512, 72, 50, (1, 2))])
+def test_relaxed_synthetic(gpu, oracle_lib, N, bins, K, seeds):
+    _run_case(gpu, oracle_lib, [synthetic(N, bins, K, s) for s in seeds], f"synthetic {N}")
+
+
+def test_relaxed_cfg3_queries(gpu, oracle_lib):
+    """cfg3 size (1024^2 x 72, K = 200): bench queries 0..3 and the longest one (10226)."""
+    _run_case(gpu, oracle_lib, [synthetic(1024, 72, 200, seed=q + 1) for q in (0, 1, 2, 3, 10226)], "cfg3")
+
+
+def test_relaxed_cfg5_pairs(gpu, oracle_lib):
+    """cfg5 pairs (1024^2, random goal frames): the tick-0 query of pairs 0..7."""
+    cases = []
+    for q in range(8):
+        cfg, proto, _ = replan_pairs(1024, 72, 200, 1, seed=1000 + q)[0]
+        cases.append((cfg, proto))
+    _run_case(gpu, oracle_lib, cases, "cfg5")
+
+
+def test_relaxed_harness_and_edges(gpu, oracle_lib):
+    """The reference harness (60 x 60 x 72) and a case whose goal is walled in: both modes fail
+    there, and the relaxed mode reports failure ({FLT_MAX, false}) without a device error."""
+    from tests.scenarios import harness
+    cfg, proto, _ = harness()
+    _run_case(gpu, oracle_lib, [(cfg, proto)], "harness")
+    cfg, proto = synthetic(128, 36, 0, 1)
+    g = gpu.HybridAStar(cfg)
+    drive(g, proto)
+    # a closed ring of boxes around the goal (grid centre == world goal (0, 0))
+    ring = [[x, y, 1.5, 1.5] for x in np.arange(-6.0, 6.5, 1.0) for y in (-6.0, 6.0)]
+    ring += [[x, y, 1.5, 1.5] for x in (-6.0, 6.0) for y in np.arange(-5.0, 5.5, 1.0)]
+    for _ in range(6):
+        g.update_boxes(np.array(ring, np.float32), [0.95] * len(ring), 0.0)
+    rel, _ = gpu.find_path_batch([g], [proto["vel"]], [proto["start"]], relaxed={})
+    # the reachable states may outgrow the node capacity first: then the status says so
+    assert not rel[0]["ok"] and rel[0]["cost"] > 1e38
+    assert rel[0]["stats"]["status"] in (0, gpu.HASTAR_EOVERFLOW)
