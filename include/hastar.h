@@ -166,6 +166,11 @@ typedef struct hastar_relaxed_opts {
   float h_weight;  /* f = g + h_weight x max(h, Dubins length); > 1 trades cost for speed [1.2]
                       (at the defaults the measured costs were 0.92-1.00 x the exact mode's,
                       profiles/relaxed_sweep_r02.json) */
+  int reuse_heuristic; /* 1: the planner keeps its heuristic field (N*N floats of device memory)
+                          and later relaxed calls reuse it until reset() or update_goal(), as the
+                          reference's A* memo persists across replans; map updates in between
+                          leave it stale (it only guides: every successor is checked against the
+                          current map) [0: recompute per call] */
 } hastar_relaxed_opts;
 int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, const float* vel_init, const float* starts,
                                    float* xyh, float* curv, int cap, int* len, float* cost, int* ok,

@@ -68,6 +68,7 @@ class HastarRelaxedOpts(C.Structure):
         ("max_nodes", C.c_int),
         ("max_rounds", C.c_int),
         ("h_weight", C.c_float),
+        ("reuse_heuristic", C.c_int),
     ]
 
 

@@ -209,6 +209,8 @@ struct DeviceCtx {
   int n_rarenas = 0;
   size_t r_cells = 0;
   int r_nodes = 0, r_N = 0;
+  RelaxField* d_rfields = nullptr;   // per-planner heuristic fields of a relaxed batch
+  size_t rfields_cap = 0;
 };
 
 // A larger arena that continues one parked search (hastar_find_path_batch).
@@ -451,6 +453,11 @@ struct hastar_handle_s {
   long long last_pops = 0;      // work estimate for longest-first scheduling (last search's duration)
   int row0 = 0, row1 = 0;       // map-build row window [row0, row1) (hastar_set_row_window); [0, N) by default
   std::shared_ptr<struct BatchSlab> batch;  // planners of one hastar_create_batch_f32 share it
+  // relaxed mode's own heuristic field (hastar_relaxed_opts.reuse_heuristic): kept until
+  // reset() / update_goal(), like the exact mode's memo
+  float* rfield = nullptr;
+  bool rvalid = false;
+  float rhlim = 0.0f;
 };
 
 // One allocation for the persistent state of a batch of identical planners
@@ -473,6 +480,7 @@ static void free_handle(hastar_handle h) {
   hipSetDevice(h->device);
   if (h->dc) hipStreamSynchronize(h->dc->stream);
   if (h->slab) hipFree(h->slab);
+  if (h->rfield) hipFree(h->rfield);
   if (h->dc) {
     DeviceCtx& DC = *h->dc;
     if (h->side) DC.side.release(h->side, h->side_bytes);
@@ -839,6 +847,7 @@ static RelocPrep goal_prep(hastar_handle h, const float goal[3], const float sta
   D.rot_c = g_cosf(-gh);
   D.rot_s = g_sinf(-gh);
   h->goal_set = true;
+  h->rvalid = false;
   return out;
 }
 
@@ -846,6 +855,7 @@ static RelocPrep goal_prep(hastar_handle h, const float goal[3], const float sta
 int hastar_reset(hastar_handle h) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
+  h->rvalid = false;
   // the memo flags are a bitmap (N*N / 8 bytes): reset clears it
   const PlannerDev& D = h->desc;
   HIPCHK(hipMemsetAsync(D.visited, 0, bitmap_words((size_t)D.N * D.N) * sizeof(uint32_t), h->dc->stream));
@@ -858,6 +868,7 @@ int hastar_reset_batch(const hastar_handle* hs, int n) {
   if (!hs || n < 0) return fail(HASTAR_EINVAL, "bad argument");
   for (int i = 0; i < n; ++i)
     if (!hs[i]) return fail(HASTAR_EINVAL, "null handle");
+  for (int i = 0; i < n; ++i) hs[i]->rvalid = false;
   std::vector<char> done(n, 0);
   for (int i = 0; i < n; ++i) {
     if (done[i]) continue;
@@ -1745,8 +1756,7 @@ size_t relax_bytes(int N, int nodes, RelaxArena* A, char* q) {
     return p;
   };
   char* dist = take(NN * 4);
-  char* done = take(((NN + 31) / 32) * 4);
-  char* bucket = take((size_t)4 * bcap * 4);
+  char* bucket = take((size_t)8 * bcap * sizeof(BucketEntry));
   char* table = take((size_t)slots * sizeof(Slot3));
   char* nodes_p = take((size_t)nodes * sizeof(Node3));
   char* lists = take((size_t)3 * nodes * 8);
@@ -1756,8 +1766,7 @@ size_t relax_bytes(int N, int nodes, RelaxArena* A, char* q) {
   if (A) {
     std::memset(A, 0, sizeof(*A));
     A->dist = reinterpret_cast<float*>(dist);
-    A->done = reinterpret_cast<uint32_t*>(done);
-    A->bucket = reinterpret_cast<int*>(bucket);
+    A->bucket = reinterpret_cast<BucketEntry*>(bucket);
     A->bcap = bcap;
     A->table = reinterpret_cast<Slot3*>(table);
     A->tmask = slots - 1;
@@ -1793,7 +1802,11 @@ int relax_acquire(DeviceCtx& D, int N, int nodes, int want) {
     return fail(HASTAR_ENOMEM, "relaxed arenas: hipMalloc failed");
   }
   std::vector<RelaxArena> host(n);
-  for (int i = 0; i < n; ++i) relax_bytes(N, nodes, &host[i], static_cast<char*>(D.rslab) + per * (size_t)i);
+  for (int i = 0; i < n; ++i) {
+    relax_bytes(N, nodes, &host[i], static_cast<char*>(D.rslab) + per * (size_t)i);
+    // the best-g tables start empty; every search leaves its table empty again
+    HIPCHK(hipMemsetAsync(host[i].table, 0xff, ((size_t)host[i].tmask + 1) * sizeof(Slot3), D.stream));
+  }
   HIPCHK(dalloc(&D.d_rarenas, (size_t)n));
   HIPCHK(hipMemcpyAsync(D.d_rarenas, host.data(), (size_t)n * sizeof(RelaxArena), hipMemcpyHostToDevice, D.stream));
   HIPCHK(hipStreamSynchronize(D.stream));
@@ -1839,11 +1852,42 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
     descs[i].result = DC.d_results + i;
   }
   HIPCHK(hipMemcpyAsync(DC.d_descs, descs.data(), (size_t)n * sizeof(PlannerDev), hipMemcpyHostToDevice, st));
+  // planners that keep their heuristic field: allocate it on first use
+  const bool reuse = opts && opts->reuse_heuristic;
+  std::vector<RelaxField> fields;
+  if (reuse) {
+    fields.resize(n);
+    for (int i = 0; i < n; ++i) {
+      hastar_handle h = hs[i];
+      const size_t NN = (size_t)h->desc.N * h->desc.N;
+      if (!h->rfield && hipMalloc(reinterpret_cast<void**>(&h->rfield), NN * sizeof(float)) != hipSuccess) {
+        h->rfield = nullptr;
+        return fail(HASTAR_ENOMEM, "relaxed heuristic field: hipMalloc failed");
+      }
+      fields[i] = RelaxField{h->rfield, h->rhlim, h->rvalid ? 1 : 0};
+    }
+    if ((size_t)n > DC.rfields_cap) {
+      HIPCHK(hipStreamSynchronize(st));
+      if (DC.d_rfields) hipFree(DC.d_rfields);
+      DC.d_rfields = nullptr;
+      DC.rfields_cap = 0;
+      HIPCHK(dalloc(&DC.d_rfields, (size_t)n));
+      DC.rfields_cap = n;
+    }
+    HIPCHK(hipMemcpyAsync(DC.d_rfields, fields.data(), (size_t)n * sizeof(RelaxField), hipMemcpyHostToDevice, st));
+  }
   HIPCHK(hipEventRecord(DC.ev0, st));
-  HIPCHK(launch_relaxed(DC.d_descs, n, DC.d_rarenas, std::min(want, DC.n_rarenas), DC.d_next, rp, st));
+  HIPCHK(launch_relaxed(DC.d_descs, n, DC.d_rarenas, std::min(want, DC.n_rarenas), DC.d_next, rp,
+                        reuse ? DC.d_rfields : nullptr, st));
   HIPCHK(hipEventRecord(DC.ev1, st));
   HIPCHK(hipMemcpyAsync(DC.h_results, DC.d_results, (size_t)n * sizeof(SearchResult), hipMemcpyDeviceToHost, st));
+  if (reuse)
+    HIPCHK(hipMemcpyAsync(fields.data(), DC.d_rfields, (size_t)n * sizeof(RelaxField), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  for (int i = 0; reuse && i < n; ++i) {
+    hs[i]->rvalid = fields[i].valid != 0;
+    hs[i]->rhlim = fields[i].hlim;
+  }
   float ms = 0.0f;
   hipEventElapsedTime(&ms, DC.ev0, DC.ev1);
   g_last_ms = ms;
@@ -1973,6 +2017,7 @@ int hastar_grid2d_update_goal_heading(hastar_handle h, const float goal[2], cons
   D.goal_cy = D.n2;
   D.grid_heading = h->grid_heading;
   h->goal_set = true;
+  h->rvalid = false;
   return HASTAR_OK;
 }
 

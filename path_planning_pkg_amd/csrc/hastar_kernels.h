@@ -10,7 +10,7 @@ hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_ar
                          long long hard_pops, hipStream_t st);
 int search_slots_per_cu();
 hipError_t launch_relaxed(const PlannerDev* d_descs, int n, const RelaxArena* d_arenas, int n_arenas, int* d_next,
-                          const RelaxParams& rp, hipStream_t st);
+                          const RelaxParams& rp, RelaxField* d_fields, hipStream_t st);
 int relaxed_waves();
 hipError_t launch_grid3d_neighbors(const PlannerDev* d_desc, const float node[5], int nci, int nbin, float* out,
                                    int* cells, int cap, int* count, int* neglect, hipStream_t st);

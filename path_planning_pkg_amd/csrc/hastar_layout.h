@@ -219,24 +219,33 @@ struct SlotArena {
 // Scratch of one planner in the RELAXED (non-parity) search mode (hastar_relaxed.hip,
 // SURVEY.md §8(f) rank 4): one workgroup per planner, so one arena per resident workgroup.
 //   dist    N*N backward 8-connected distance to the goal cell (the heuristic), float bits
-//           updated with atomicMin (non-negative floats order like their bit patterns)
-//   done    N*N/32 bitmap: cells the bucket Dijkstra has settled
-//   bucket  4 x bcap cell lists (a ring of Dial buckets of width act_cost_axis)
-//   table   best g per node key (open addressing; key 0xffffffff = empty)
-//   nodes   every node ever generated (Node3 records; prev = parent node index)
+//           updated with atomicMin (non-negative floats order like their bit patterns); used
+//           when the planner keeps no field of its own (RelaxField)
+//   bucket  8 x bcap {cell, distance bits} entries (a ring of Dial buckets of width act_cost_axis)
+//   table   best g per node key (open addressing; key 0xffffffff = empty; left empty by every search)
+//   nodes   every node ever generated (Node3 records; prev = parent node, l = its table slot)
 //   lists   3 x list_cap lists of {f bits, node} (8 B): the open list, the next open list
 //           and the round's expansion set (node indices only)
 //   dub_*   one Dubins-shot scratch of dub_cap samples per wave
 //   chain   path reconstruction scratch
+struct BucketEntry { uint32_t cell, d; };  // a Dial-bucket entry: cell and its distance bits
 struct RelaxArena {
-  float* dist;      uint32_t* done;
-  int* bucket;      int bcap;       int pad0;
+  float* dist;
+  BucketEntry* bucket;    int bcap;       int pad0;
   Slot3* table;     uint32_t tmask; int pad1;
   Node3* nodes;     int node_cap;   int pad2;
   int* lists;       int list_cap;   int pad3;
   float* dub_xyh;   float* dub_curv; int dub_cap; int pad4;
   int* chain;       int chain_cap;  int pad5;
   size_t cells;     // N*N served
+};
+// A planner's own heuristic field (hastar_relaxed_opts.reuse_heuristic): computed once, then
+// reused by later relaxed searches until reset() or update_goal() (the reference's A* memo
+// persists across find_path calls the same way, AStar.cpp:56-60, local_planner.cpp:316).
+struct RelaxField {
+  float* dist;      // N*N, or null: use the arena's scratch
+  float hlim;       // bound of the cells the Dijkstra left unsettled
+  int valid;        // 1: dist/hlim hold a finished field
 };
 // options of a relaxed launch (kernel side of hastar_relaxed_opts)
 struct RelaxParams {

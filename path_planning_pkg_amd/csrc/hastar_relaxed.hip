@@ -52,9 +52,11 @@ __device__ __forceinline__ uint32_t rx_hash(uint32_t k) {
   k *= 0x846ca68bU;
   return k ^ (k >> 16);
 }
-// best-g table: lower the key's g to gbits; true when gbits is the new best.  *full is set
+// best-g table: lower the key's g to gbits; true when gbits is the new best (*slot: the key's
+// slot, kept in the node so the search can clear exactly the slots it used).  *full is set
 // when the table has no room left.
-__device__ __forceinline__ bool table_lower(const RelaxArena& A, uint32_t key, uint32_t gbits, bool* full) {
+__device__ __forceinline__ bool table_lower(const RelaxArena& A, uint32_t key, uint32_t gbits, bool* full,
+                                            uint32_t* slot) {
   uint32_t h = rx_hash(key) & A.tmask;
   for (uint32_t probe = 0; probe <= A.tmask; ++probe) {
     Slot3* s = &A.table[h];
@@ -63,6 +65,7 @@ __device__ __forceinline__ bool table_lower(const RelaxArena& A, uint32_t key, u
       const uint32_t prev = atomicCAS(&s->key, EMPTY_KEY, key);
       k = prev == EMPTY_KEY ? key : prev;
     }
+    *slot = h;
     if (k == key) return atomicMin(&s->gi, gbits) > gbits;
     h = (h + 1) & A.tmask;
   }
@@ -83,10 +86,11 @@ __device__ __forceinline__ uint32_t table_best(const RelaxArena& A, uint32_t key
 struct RelaxShared {
   ApfStage apf[RW];
   int planner;
-  int cnt[4];               // Dijkstra bucket fill counts (ring)
+  int cnt[8];               // Dijkstra bucket fill counts (ring of 8)
   int overflow, hover;
   int stop_at;              // last bucket the Dijkstra settles (-1: start not settled yet)
   int settled;              // cells settled (diagnostic: astar_pops)
+  int buckets;              // Dijkstra buckets processed
   int nA, nB, nE, eNext, nodes;
   uint32_t fmin, fnext;     // float bits of the open list's min f, and of the next open list's
   unsigned long long best;  // cheapest solution candidate: f bits << 32 | tag
@@ -95,46 +99,58 @@ struct RelaxShared {
   int shot_term[RW], shot_n[RW], shot_done[RW];
 };
 
-// Phase 1: Dial-bucket Dijkstra from the goal cell; returns the heuristic bound of cells the
-// early stop left unsettled (every such cell is at least that far).
-__device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, const RelaxParams& rp) {
+// Phase 1: Dial-bucket Dijkstra from the goal cell into `dist`; returns the heuristic bound
+// of cells the early stop left unsettled (every such cell is at least that far).
+// Bucket entries are {cell, distance bits}: an entry is live iff the cell's distance is still
+// the one it was pushed with (a cell improves only by a strictly smaller push), so no settled
+// flags are needed.  Moves cost >= wb, so iteration `cur` pushes only into buckets cur+1 ..
+// cur+3 of a ring of 8: one barrier per bucket suffices — a bucket's count is final when its
+// iteration starts, and slot (cur-1) & 7 is recycled (reset) long before it is pushed again.
+// The run ends after 3 empty buckets in a row (nothing can be pushed past them) or at the
+// early stop; both decisions use values every thread reads identically.
+__device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, const RelaxParams& rp,
+                                   float* dist_f) {
   const int tid = threadIdx.x, NT = blockDim.x;
   const int N = P.N;
   const float wb = P.act_cost_axis;
   const float cd = P.act_cost_diag;
   const int nact = P.diag ? 8 : 4;
-  uint32_t* dist = reinterpret_cast<uint32_t*>(A.dist);
+  uint32_t* dist = reinterpret_cast<uint32_t*>(dist_f);
+  const size_t NN = (size_t)N * N;
+  for (size_t i = tid; i < NN; i += NT) dist[i] = 0x7f800000u;
   const size_t goal = (size_t)P.goal_cx * N + P.goal_cy;
   const size_t start = (size_t)P.start_cx * N + P.start_cy;
+  block_sync();
   if (tid == 0) {
     dist[goal] = 0u;
-    A.bucket[0] = (int)goal;
-    S.cnt[0] = 1;
-    S.cnt[1] = S.cnt[2] = S.cnt[3] = 0;
+    A.bucket[0] = BucketEntry{(uint32_t)goal, 0u};
+    for (int k = 0; k < 8; ++k) S.cnt[k] = k == 0 ? 1 : 0;
     S.overflow = 0;
     S.stop_at = -1;
     S.settled = 0;
   }
   block_sync();
   const int max_b = 4 * N + 64;
-  int cur = 0;
+  int cur = 0, empty_run = 0;
   for (; cur < max_b; ++cur) {
-    const int slot = cur & 3;
+    const int slot = cur & 7;
     const int m = min(S.cnt[slot], A.bcap);
-    const int live = S.cnt[0] | S.cnt[1] | S.cnt[2] | S.cnt[3];
     const int stop_at = S.stop_at;
-    block_sync();
-    if (live == 0 || (stop_at >= 0 && cur > stop_at)) break;
+    if (tid == 0) S.cnt[(cur - 1) & 7] = 0;  // recycled: pushed again no earlier than iteration cur + 4
+    empty_run = m == 0 ? empty_run + 1 : 0;
+    if (empty_run >= 3 || (stop_at >= 0 && cur > stop_at)) break;
     int settled = 0;
     for (int e = tid; e < m; e += NT) {
-      const int c = A.bucket[(size_t)slot * A.bcap + e];
-      const uint32_t bit = 1u << (c & 31);
-      if (atomicOr(&A.done[c >> 5], bit) & bit) continue;  // settled from an earlier entry
+      const BucketEntry en = A.bucket[(size_t)slot * A.bcap + e];
+      const size_t c = en.cell;
+      const uint32_t dc = ld_sync(&dist[c]);
+      const float oc = gp(P.occ)[c];
+      if (dc != en.d) continue;  // a shorter distance was pushed since: that entry settles it
       ++settled;
-      if ((size_t)c == start) atomicCAS(&S.stop_at, -1, cur + (int)((rp.h_stop - 1.0f) * (float)cur) + 64);
-      if ((size_t)c != goal && gp(P.occ)[c] >= P.thr) continue;  // not enterable: no move leads through it
-      const float d = __uint_as_float(ld_sync(&dist[c]));
-      const int ci = c / N, cj = c - ci * N;
+      if (c == start) atomicCAS(&S.stop_at, -1, cur + (int)((rp.h_stop - 1.0f) * (float)cur) + 64);
+      if (c != goal && oc >= P.thr) continue;  // not enterable: no move leads through it
+      const float d = __uint_as_float(dc);
+      const int ci = (int)(c / N), cj = (int)(c - (size_t)ci * N);
       for (int a = 0; a < nact; ++a) {
         // the 8 moves (Grid2D.cpp:22-40), axis moves first
         const int di = a < 4 ? ((a & 1) ? 0 : (a == 0 ? 1 : -1)) : ((a & 1) ? 1 : -1);
@@ -148,23 +164,24 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
         int kb = (int)(nd / wb);
         kb = max(kb, cur + 1);
         kb = min(kb, cur + 3);
-        const int pos = atomicAdd(&S.cnt[kb & 3], 1);
-        if (pos < A.bcap) A.bucket[(size_t)(kb & 3) * A.bcap + pos] = (int)p;
+        const int pos = atomicAdd(&S.cnt[kb & 7], 1);
+        if (pos < A.bcap) A.bucket[(size_t)(kb & 7) * A.bcap + pos] = BucketEntry{(uint32_t)p, nb};
         else S.overflow = 1;
       }
     }
     if (settled) atomicAdd(&S.settled, settled);
     block_sync();
-    if (tid == 0) S.cnt[slot] = 0;
-    block_sync();
   }
+  block_sync();
+  if (tid == 0) S.buckets = cur;
   return (float)cur * wb;
 }
 
 // One expansion by one wavefront: the exact kernel's fused successor block without the
 // closed set and the lazy A* (the heuristic is the Dijkstra field).
 __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, ApfStage& apfs,
-                               const GoalC& GC, float hlim, float hw, int idx, int wv, int lane, uint2* list_b) {
+                               const GoalC& GC, const float* dist, float hlim, float hw, int idx, int wv, int lane,
+                               uint2* list_b) {
   const Node3 cur = gload(&A.nodes[idx]);
   const uint32_t key = ufu(cur.key);
   const float cg = uff(cur.g), cxp = uff(cur.x), cyp = uff(cur.y), chd = uff(cur.h), cvm = uff(cur.vmin);
@@ -249,7 +266,7 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
   if (lead) {
     const size_t cell = (size_t)scx * P.N + scy;
     occv = gp(P.occ)[cell];
-    h2 = ld_dist(A.dist, cell);
+    h2 = ld_dist(dist, cell);
     // unsettled cells (beyond the Dijkstra's early stop, or enclosed) are at least hlim away
     if (!(h2 < hlim)) h2 = hlim;
   }
@@ -263,14 +280,15 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
     const float f = g + hw * stl_max(h2, dub);
     const uint32_t skey = key3(scx, scy, sbin);
     bool full = false;
-    if (table_lower(A, skey, __float_as_uint(g), &full)) {
+    uint32_t tslot = 0;
+    if (table_lower(A, skey, __float_as_uint(g), &full, &tslot)) {
       const int n = atomicAdd(&S.nodes, 1);
       const int pos = atomicAdd(&S.nB, 1);
       if (n < A.node_cap && pos < A.list_cap) {
         Node3 d;
         d.key = skey;
         d.f = f;
-        d.l = NIL;
+        d.l = (int)tslot;
         d.r = NIL;
         d.p = NIL;
         d.cc = (uint32_t)(lo + ca) << 8;
@@ -291,30 +309,36 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
   }
 }
 
-__device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, const RelaxParams& rp) {
+__device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, const RelaxParams& rp,
+                            RelaxField* F) {
   const int tid = threadIdx.x, NT = blockDim.x, wv = tid >> 6, lane = tid & 63;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  const size_t NN = (size_t)P.N * P.N;
-  // ---- clear: distances to +inf, settled flags, best-g table
-  {
-    uint32_t* dist = reinterpret_cast<uint32_t*>(A.dist);
-    for (size_t i = tid; i < NN; i += NT) dist[i] = 0x7f800000u;
-    const size_t words = (NN + 31) / 32;
-    for (size_t i = tid; i < words; i += NT) A.done[i] = 0u;
-    for (size_t i = tid; i <= A.tmask; i += NT) {
-      A.table[i].key = EMPTY_KEY;
-      A.table[i].gi = 0xffffffffu;
+  // the heuristic field: the planner's own (kept across calls until reset / update_goal, like
+  // the reference's A* memo) or the arena's scratch
+  float* dist = (F && F->dist) ? F->dist : A.dist;
+  float hlim;
+  if (F && F->dist && F->valid) {
+    hlim = F->hlim;
+    if (tid == 0) {
+      S.buckets = 0;
+      S.settled = 0;
+      S.overflow = 0;
+    }
+  } else {
+    hlim = relaxed_heuristic(P, A, S, rp, dist);
+    if (tid == 0 && F && F->dist) {
+      F->hlim = hlim;
+      F->valid = 1;
     }
   }
-  block_sync();
-  const float hlim = relaxed_heuristic(P, A, S, rp);
+  const unsigned long long t_heur = __builtin_amdgcn_s_memrealtime();
   // ---- the frontier-parallel search
   apf_stage(P, S.apf[wv], lane);
   const GoalC GC = goal_centres(P.r_min, P.goal_x, P.goal_y, P.goal_h);
   if (tid == 0) {
     Node3 s0;
     s0.key = key3(P.start_cx, P.start_cy, P.start_bin);
-    float h0 = ld_dist(A.dist, (size_t)P.start_cx * P.N + P.start_cy);
+    float h0 = ld_dist(dist, (size_t)P.start_cx * P.N + P.start_cy);
     if (!(h0 < hlim)) h0 = hlim;
     s0.f = h0;
     s0.l = s0.r = s0.p = NIL;
@@ -327,7 +351,9 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
     s0.prev = NIL;
     gstore(&A.nodes[0], s0);
     bool full = false;
-    table_lower(A, s0.key, 0u, &full);
+    uint32_t tslot = 0;
+    table_lower(A, s0.key, 0u, &full, &tslot);
+    A.nodes[0].l = (int)tslot;
     reinterpret_cast<uint2*>(A.lists)[0] = make_uint2(__float_as_uint(s0.f), 0u);
     S.nA = 1;
     S.nB = 0;
@@ -384,7 +410,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
       if (lane == 0) e = atomicAdd(&S.eNext, 1);
       e = ufi(e);
       if (e >= nE) break;
-      relaxed_expand(P, A, S, S.apf[wv], GC, hlim, rp.h_weight, LE[e], wv, lane, LB);
+      relaxed_expand(P, A, S, S.apf[wv], GC, dist, hlim, rp.h_weight, LE[e], wv, lane, LB);
     }
     block_sync();
     if (tid == 0) {
@@ -492,6 +518,28 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
       R->t_end = __builtin_amdgcn_s_memrealtime();
       R->slot = (int)blockIdx.x;
       R->parks = 0;
+      // phase split (s_memrealtime, 100 MHz; hastar_debug_cycles): clear + Dijkstra, search
+      // rounds + reconstruction, Dijkstra buckets, search rounds
+      for (int q = 0; q < NSTAMP; ++q) R->cycles[q] = 0;
+      R->cycles[0] = t_heur - t_start;
+      R->cycles[1] = R->t_end - t_heur;
+      R->cycles[2] = (unsigned long long)S.buckets;
+      R->cycles[3] = (unsigned long long)S.rounds;
+    }
+  }
+  // leave the best-g table empty for the next planner: the slots this search claimed (kept in
+  // its nodes), or the whole table when an overflow may have left claimed slots without a node
+  if (S.overflow) {
+    for (size_t i = tid; i <= A.tmask; i += NT) {
+      A.table[i].key = EMPTY_KEY;
+      A.table[i].gi = 0xffffffffu;
+    }
+  } else {
+    const int nn = min(S.nodes, A.node_cap);
+    for (int n = tid; n < nn; n += NT) {
+      const uint32_t t = (uint32_t)A.nodes[n].l;
+      A.table[t].key = EMPTY_KEY;
+      A.table[t].gi = 0xffffffffu;
     }
   }
   block_sync();
@@ -500,7 +548,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
 // Persistent: grid = resident relaxed arenas; each workgroup pulls planners from *next.
 __global__ __launch_bounds__(RW * 64) void k_relaxed_search(const PlannerDev* __restrict__ descs, int n,
                                                            const RelaxArena* __restrict__ arenas, int* next,
-                                                           RelaxParams rp) {
+                                                           RelaxParams rp, RelaxField* fields) {
   __shared__ RelaxShared S;
   const RelaxArena A = arenas[blockIdx.x];
   for (;;) {
@@ -509,15 +557,15 @@ __global__ __launch_bounds__(RW * 64) void k_relaxed_search(const PlannerDev* __
     const int pi = S.planner;
     block_sync();
     if (pi >= n) break;
-    relaxed_one(descs[pi], A, S, rp);
+    relaxed_one(descs[pi], A, S, rp, fields ? &fields[pi] : nullptr);
   }
 }
 
 hipError_t launch_relaxed(const PlannerDev* d_descs, int n, const RelaxArena* d_arenas, int n_arenas, int* d_next,
-                          const RelaxParams& rp, hipStream_t st) {
+                          const RelaxParams& rp, RelaxField* d_fields, hipStream_t st) {
   hipError_t e = hipMemsetAsync(d_next, 0, sizeof(int), st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_relaxed_search, dim3(n_arenas), dim3(RW * 64), 0, st, d_descs, n, d_arenas, d_next, rp);
+  hipLaunchKernelGGL(k_relaxed_search, dim3(n_arenas), dim3(RW * 64), 0, st, d_descs, n, d_arenas, d_next, rp, d_fields);
   return hipGetLastError();
 }
 int relaxed_waves() { return RW; }

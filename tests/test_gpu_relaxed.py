@@ -42,14 +42,14 @@ def world_to_grid(xyh, goal, start, N, res):
     return x0 + int(round(N * 0.8)) * res, y0 + (N // 2) * res
 
 
-def check_valid(r, occ, thr, proto, N, res, max_step, what):
+def check_valid(r, occ, thr, proto, N, res, max_step, what, frame_start=None):
     path = r["path"]
     assert r["ok"] and len(path) >= 2, f"{what}: no path"
     s = np.asarray(proto["start"], np.float64)
     assert np.hypot(*(path[-1, :2] - s[:2])) < 1e-2, f"{what}: path does not end at the start"
     g = np.asarray(proto["goal"], np.float64)
     assert np.hypot(*(path[0, :2] - g[:2])) < 2.0 * res, f"{what}: path does not begin at the goal"
-    gx, gy = world_to_grid(path, proto["goal"], proto["start"], N, res)
+    gx, gy = world_to_grid(path, proto["goal"], frame_start or proto["start"], N, res)
     ci, cj = np.floor(gx / res + 1e-6).astype(int), np.floor(gy / res + 1e-6).astype(int)
     ri, rj = np.rint(gx / res).astype(int), np.rint(gy / res).astype(int)
     inside = (ci >= 0) & (ci < N) & (cj >= 0) & (cj < N)
@@ -118,6 +118,42 @@ def test_relaxed_cfg5_pairs(gpu, oracle_lib):
         cfg, proto, _ = replan_pairs(1024, 72, 200, 1, seed=1000 + q)[0]
         cases.append((cfg, proto))
     _run_case(gpu, oracle_lib, cases, "cfg5")
+
+
+def test_relaxed_replan_loop_reuses_heuristic(gpu):
+    """cfg5's replan loop (no reset between ticks) with reuse_heuristic: the first tick computes
+    each planner's Dijkstra field, later ticks reuse it (no Dijkstra time, no settled cells)
+    while the boxes move, and every tick's path is valid on the CURRENT map.  reset() and
+    update_goal() invalidate the field."""
+    from tests.scenarios import replan_tick, replan_tick_inputs
+    pairs = [replan_pairs(1024, 72, 200, 1, seed=1000 + q)[0] for q in range(4)]
+    gs = []
+    for cfg, proto, _ in pairs:
+        g = gpu.HybridAStar(cfg)
+        drive(g, proto)
+        gs.append(g)
+    opts = dict(reuse_heuristic=1)
+    p = pairs[0][0].values
+    N, res, step = p["grid_size"], p["grid_resolution"], p["step_size"]
+    thr = np.float32(math.log(p["obstacle_threshold"] / (1.0 - p["obstacle_threshold"])))
+    for tick in range(3):
+        starts = [replan_tick_inputs(proto, v, tick)[0] for _, proto, v in pairs]
+        rel, _ = gpu.find_path_batch(gs, [proto["vel"] for _, proto, _ in pairs], starts, cap=16384, relaxed=opts)
+        for i, ((cfg, proto, v), g, r) in enumerate(zip(pairs, gs, rel)):
+            cyc = g.cycles()
+            if tick == 0:
+                assert cyc[2] > 0 and r["stats"]["astar_pops"] > 0, "tick 0 must run the Dijkstra"
+            else:
+                assert cyc[2] == 0 and r["stats"]["astar_pops"] == 0, f"tick {tick}: field not reused"
+            pr = dict(proto, start=starts[i])
+            check_valid(r, g.get_obstacles(), thr, pr, N, res, 3.0 * step + 1e-3, f"tick {tick} pair {i}",
+                        frame_start=proto["start"])  # the grid frame is the one update_goal set
+            replan_tick(g, proto, v, tick)
+    gs[0].reset()
+    gs[1].update_goal(pairs[1][1]["goal"], pairs[1][1]["start"])
+    starts = [replan_tick_inputs(proto, v, 3)[0] for _, proto, v in pairs]
+    gpu.find_path_batch(gs, [proto["vel"] for _, proto, _ in pairs], starts, cap=16384, relaxed=opts)
+    assert [g.cycles()[2] > 0 for g in gs] == [True, True, False, False]
 
 
 def test_relaxed_harness_and_edges(gpu, oracle_lib):
