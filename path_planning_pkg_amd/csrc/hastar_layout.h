@@ -228,7 +228,7 @@ struct SlotArena {
 //           and the round's expansion set (node indices only)
 //   dub_*   one Dubins-shot scratch of dub_cap samples per wave
 //   chain   path reconstruction scratch
-struct BucketEntry { uint32_t cell, d; };  // a Dial-bucket entry: cell and its distance bits
+struct BucketEntry { uint32_t cell, d; };  // a Dial-bucket entry: cell (i << 16 | j) and its distance bits
 struct RelaxArena {
   float* dist;
   BucketEntry* bucket;    int bcap;       int pad0;

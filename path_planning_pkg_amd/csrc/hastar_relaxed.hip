@@ -30,6 +30,22 @@
 namespace hastar {
 
 constexpr int RW = 8;                        // wavefronts per planner workgroup
+constexpr int DU = 4;                        // Dijkstra bucket entries per thread in flight
+
+// diagnostic build (-DRELAX_STAMPS): per-phase cycles of the Dijkstra's bucket loop, thread 0
+#ifdef RELAX_STAMPS
+#define RSTAMP_BEGIN() unsigned long long rt0 = (__builtin_amdgcn_s_waitcnt(0), __builtin_amdgcn_s_memtime())
+#define RSTAMP(k)                                                              \
+  do {                                                                         \
+    __builtin_amdgcn_s_waitcnt(0);                                             \
+    const unsigned long long rt1 = __builtin_amdgcn_s_memtime();               \
+    rst[k] += rt1 - rt0;                                                       \
+    rt0 = rt1;                                                                 \
+  } while (0)
+#else
+#define RSTAMP_BEGIN() (void)0
+#define RSTAMP(k) (void)0
+#endif
 constexpr uint32_t EMPTY_KEY = 0xffffffffu;  // no node key has all bits set (x < 4096, bin < 256 with y < 4096)
 
 // L1-bypassing loads of words other waves update with atomics
@@ -97,6 +113,7 @@ struct RelaxShared {
   int since_shot, interval;
   int pops, succ, shots, rounds;
   int shot_term[RW], shot_n[RW], shot_done[RW];
+  unsigned long long stamp[6];
 };
 
 // Phase 1: Dial-bucket Dijkstra from the goal cell into `dist`; returns the heuristic bound
@@ -118,12 +135,14 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
   uint32_t* dist = reinterpret_cast<uint32_t*>(dist_f);
   const size_t NN = (size_t)N * N;
   for (size_t i = tid; i < NN; i += NT) dist[i] = 0x7f800000u;
-  const size_t goal = (size_t)P.goal_cx * N + P.goal_cy;
-  const size_t start = (size_t)P.start_cx * N + P.start_cy;
+  // entries name cells as (i << 16 | j): no integer division per entry
+  const uint32_t goal_ij = ((uint32_t)P.goal_cx << 16) | (uint32_t)P.goal_cy;
+  const uint32_t start_ij = ((uint32_t)P.start_cx << 16) | (uint32_t)P.start_cy;
+  const float inv_wb = 1.0f / wb;  // bucket index only: rounding is absorbed by the clamp below
   block_sync();
   if (tid == 0) {
-    dist[goal] = 0u;
-    A.bucket[0] = BucketEntry{(uint32_t)goal, 0u};
+    dist[(size_t)P.goal_cx * N + P.goal_cy] = 0u;
+    A.bucket[0] = BucketEntry{goal_ij, 0u};
     for (int k = 0; k < 8; ++k) S.cnt[k] = k == 0 ? 1 : 0;
     S.overflow = 0;
     S.stop_at = -1;
@@ -132,6 +151,9 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
   block_sync();
   const int max_b = 4 * N + 64;
   int cur = 0, empty_run = 0;
+#ifdef RELAX_STAMPS
+  unsigned long long rst[6] = {0, 0, 0, 0, 0, 0};
+#endif
   for (; cur < max_b; ++cur) {
     const int slot = cur & 7;
     const int m = min(S.cnt[slot], A.bcap);
@@ -139,41 +161,107 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
     if (tid == 0) S.cnt[(cur - 1) & 7] = 0;  // recycled: pushed again no earlier than iteration cur + 4
     empty_run = m == 0 ? empty_run + 1 : 0;
     if (empty_run >= 3 || (stop_at >= 0 && cur > stop_at)) break;
+    // DU entries per thread at a time, phase by phase (entries, then distances and occupancy,
+    // then every relaxation's atomicMin, then the pushes), so the dependent global round trips
+    // of DU entries overlap instead of queueing one entry after the other
     int settled = 0;
-    for (int e = tid; e < m; e += NT) {
-      const BucketEntry en = A.bucket[(size_t)slot * A.bcap + e];
-      const size_t c = en.cell;
-      const uint32_t dc = ld_sync(&dist[c]);
-      const float oc = gp(P.occ)[c];
-      if (dc != en.d) continue;  // a shorter distance was pushed since: that entry settles it
-      ++settled;
-      if (c == start) atomicCAS(&S.stop_at, -1, cur + (int)((rp.h_stop - 1.0f) * (float)cur) + 64);
-      if (c != goal && oc >= P.thr) continue;  // not enterable: no move leads through it
-      const float d = __uint_as_float(dc);
-      const int ci = (int)(c / N), cj = (int)(c - (size_t)ci * N);
-      for (int a = 0; a < nact; ++a) {
-        // the 8 moves (Grid2D.cpp:22-40), axis moves first
-        const int di = a < 4 ? ((a & 1) ? 0 : (a == 0 ? 1 : -1)) : ((a & 1) ? 1 : -1);
-        const int dj = a < 4 ? ((a & 1) ? (a == 1 ? 1 : -1) : 0) : ((a & 2) ? 1 : -1);
-        const int pi = ci + di, pj = cj + dj;
-        if (pi < 0 || pi >= N || pj < 0 || pj >= N) continue;
-        const float nd = d + (a < 4 ? wb : cd);
-        const size_t p = (size_t)pi * N + pj;
-        const uint32_t nb = __float_as_uint(nd);
-        if (atomicMin(&dist[p], nb) <= nb) continue;
-        int kb = (int)(nd / wb);
-        kb = max(kb, cur + 1);
-        kb = min(kb, cur + 3);
-        const int pos = atomicAdd(&S.cnt[kb & 7], 1);
-        if (pos < A.bcap) A.bucket[(size_t)(kb & 7) * A.bcap + pos] = BucketEntry{(uint32_t)p, nb};
-        else S.overflow = 1;
+    RSTAMP_BEGIN();
+    for (int e0 = tid; e0 < m; e0 += NT * DU) {
+      BucketEntry en[DU];
+      uint32_t dc[DU];
+      float oc[DU];
+#pragma unroll
+      for (int u = 0; u < DU; ++u) {
+        const int e = e0 + u * NT;
+        en[u] = e < m ? A.bucket[(size_t)slot * A.bcap + e] : BucketEntry{0xffffffffu, 0u};
+      }
+      RSTAMP(0);
+#pragma unroll
+      for (int u = 0; u < DU; ++u) {
+        dc[u] = 0u;
+        oc[u] = 0.0f;
+        if (en[u].cell != 0xffffffffu) {
+          const uint32_t c = (en[u].cell >> 16) * (uint32_t)N + (en[u].cell & 0xffffu);
+          dc[u] = ld_sync(&dist[c]);
+          oc[u] = gp(P.occ)[c];
+        }
+      }
+      RSTAMP(1);
+      uint32_t old[DU][8];
+      uint32_t nbv[DU][8];
+#pragma unroll
+      for (int u = 0; u < DU; ++u) {
+        const uint32_t cij = en[u].cell;
+        // live: still the cell's distance (else a shorter push settles it); expanding: enterable
+        const bool live = cij != 0xffffffffu && dc[u] == en[u].d;
+        if (live) {
+          ++settled;
+          if (cij == start_ij) atomicCAS(&S.stop_at, -1, cur + (int)((rp.h_stop - 1.0f) * (float)cur) + 64);
+        }
+        const bool expand = live && (cij == goal_ij || oc[u] < P.thr);
+        const float d = __uint_as_float(dc[u]);
+        const int ci = (int)(cij >> 16), cj = (int)(cij & 0xffffu);
+        // the neighbours' current distances first (all in flight together):
+        // most are already at or below the offer, and only the others take an atomic — the
+        // atomics of one wavefront front hit few cache lines and serialise in L2
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+          // the 8 moves (Grid2D.cpp:22-40), axis moves first
+          const int di = a < 4 ? ((a & 1) ? 0 : (a == 0 ? 1 : -1)) : ((a & 1) ? 1 : -1);
+          const int dj = a < 4 ? ((a & 1) ? (a == 1 ? 1 : -1) : 0) : ((a & 2) ? 1 : -1);
+          const int pi = ci + di, pj = cj + dj;
+          const bool ok = expand && a < nact && pi >= 0 && pi < N && pj >= 0 && pj < N;
+          const uint32_t nb = __float_as_uint(d + (a < 4 ? wb : cd));
+          nbv[u][a] = nb;
+          // a plain (possibly L1-stale) load: distances only fall, so a stale value only
+          // costs an extra atomic, never a missed relaxation
+          old[u][a] = ok ? gp(dist)[(uint32_t)pi * (uint32_t)N + (uint32_t)pj] : nb;
+        }
+      }
+      RSTAMP(2);
+#pragma unroll
+      for (int u = 0; u < DU; ++u) {
+        const uint32_t cij = en[u].cell;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+          if (old[u][a] <= nbv[u][a]) continue;
+          const int di = a < 4 ? ((a & 1) ? 0 : (a == 0 ? 1 : -1)) : ((a & 1) ? 1 : -1);
+          const int dj = a < 4 ? ((a & 1) ? (a == 1 ? 1 : -1) : 0) : ((a & 2) ? 1 : -1);
+          const uint32_t pidx = (uint32_t)((int)(cij >> 16) + di) * (uint32_t)N + (uint32_t)((int)(cij & 0xffffu) + dj);
+          old[u][a] = atomicMin(&dist[pidx], nbv[u][a]);
+        }
+      }
+      RSTAMP(3);
+#pragma unroll
+      for (int u = 0; u < DU; ++u) {
+        const uint32_t cij = en[u].cell;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+          const uint32_t nb = nbv[u][a];
+          if (old[u][a] <= nb) continue;  // no improvement (or not relaxed at all)
+          const int di = a < 4 ? ((a & 1) ? 0 : (a == 0 ? 1 : -1)) : ((a & 1) ? 1 : -1);
+          const int dj = a < 4 ? ((a & 1) ? (a == 1 ? 1 : -1) : 0) : ((a & 2) ? 1 : -1);
+          const uint32_t pij = (uint32_t)((int)(cij >> 16) + di) << 16 | (uint32_t)((int)(cij & 0xffffu) + dj);
+          int kb = (int)(__uint_as_float(nb) * inv_wb);
+          kb = max(kb, cur + 1);
+          kb = min(kb, cur + 3);
+          const int pos = atomicAdd(&S.cnt[kb & 7], 1);
+          if (pos < A.bcap) A.bucket[(size_t)(kb & 7) * A.bcap + pos] = BucketEntry{pij, nb};
+          else S.overflow = 1;
+        }
       }
     }
+    RSTAMP(4);
     if (settled) atomicAdd(&S.settled, settled);
     block_sync();
+    RSTAMP(5);
   }
   block_sync();
   if (tid == 0) S.buckets = cur;
+#ifdef RELAX_STAMPS
+  if (tid == 0)
+    for (int k = 0; k < 6; ++k) S.stamp[k] = rst[k];
+#endif
   return (float)cur * wb;
 }
 
@@ -525,6 +613,9 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
       R->cycles[1] = R->t_end - t_heur;
       R->cycles[2] = (unsigned long long)S.buckets;
       R->cycles[3] = (unsigned long long)S.rounds;
+#ifdef RELAX_STAMPS
+      for (int k = 0; k < 6; ++k) R->cycles[8 + k] = S.stamp[k];
+#endif
     }
   }
   // leave the best-g table empty for the next planner: the slots this search claimed (kept in
