@@ -115,7 +115,7 @@ def parse_args(argv=None):
                          "(BASELINE.json configs[3]); cfg5: 20 Hz replan loop of start/goal pairs (configs[4])")
     ap.add_argument("--map-queries", type=int, default=16, help="cfg4: maps built both locally and row-sharded")
     ap.add_argument("--pairs", type=int, default=64, help="cfg5: start/goal pairs in total, dealt over the ranks")
-    ap.add_argument("--relaxed-delta", type=float, default=0.5, help="relaxed mode: frontier width (m)")
+    ap.add_argument("--relaxed-delta", type=float, default=0.25, help="relaxed mode: frontier width (m)")
     ap.add_argument("--relaxed-weight", type=float, default=1.2, help="relaxed mode: heuristic weight")
     ap.add_argument("--no-relaxed", action="store_true", help="cfg5: skip the relaxed-mode comparison")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")

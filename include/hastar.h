@@ -159,8 +159,9 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel_init
  * reference's.  The exact mode's memo (node-map f, visited flags) is neither read nor written.
  * opts may be NULL (defaults in brackets). */
 typedef struct hastar_relaxed_opts {
-  float delta;     /* frontier width in metres [0.5] */
-  float h_stop;    /* the Dijkstra stops at h_stop x the start's distance (+64 buckets) [3.0] */
+  float delta;     /* frontier width in metres [0.25] */
+  float h_stop;    /* the Dijkstra covers the ellipse d(c) + |c - start| <= h_stop x |goal - start| + 64 moves;
+                      cells outside get bound - |c - start| [1.5] */
   int max_nodes;   /* node capacity per search; beyond it the search ends with HASTAR_EOVERFLOW [1 << 20] */
   int max_rounds;  /* [1 << 20] */
   float h_weight;  /* f = g + h_weight x max(h, Dubins length); > 1 trades cost for speed [1.2]

@@ -47,7 +47,10 @@ namespace orc {
 // reaches it stops with stats.status = HASTAR_EOVERFLOW and is reported as failed.
 long long g_max_pops = 0;
 #ifdef ORC_SHAPE_STATS
-long long g_shape[8];
+long long g_shape[16];
+bool g_search_unsafe;       // the current inner search met a shape-dependent find/insert
+long long g_search_pops;    // pops of the current inner search
+long long g_pops_to_unsafe; // pops before its first shape-dependent event
 #endif
 
 template <class T> struct P2 { T x, y; };
@@ -521,12 +524,14 @@ template <class T> struct Planner {
   // matter for find/insert (a node of the same cell on the "wrong" side of the probe f).
   template <class S> void shape_probe(const S& op, int i, int j, T fprobe, T fn) {
     bool same = false, unsafe_find = false, unsafe_ins = false;
+    int nsame = 0;
     T prev = -std::numeric_limits<T>::infinity();
     for (const auto& n : op) {
       if (!(n.f > prev)) g_shape[7]++;  // strict f order violated
       prev = n.f;
       if (n.x == i && n.y == j) {
         same = true;
+        ++nsame;
         if (n.f < fprobe) unsafe_find = true;
         if (n.f > fn) unsafe_ins = true;
       }
@@ -535,6 +540,24 @@ template <class T> struct Planner {
     g_shape[1] += same;
     g_shape[2] += unsafe_find;
     g_shape[3] += unsafe_ins;
+    // the kernel's rank-only path is exact unless one of these holds (csrc: astar_loop_lds)
+    if ((unsafe_find || unsafe_ins || nsame > 1) && !g_search_unsafe) {
+      g_search_unsafe = true;
+      g_pops_to_unsafe = g_search_pops;
+    }
+  }
+  // per inner search: [8] searches, [9] searches with a shape-dependent event, [10] pops of all
+  // searches, [11] pops of those searches, [12] their pops before the first event
+  void shape_search_end() {
+    g_shape[8]++;
+    g_shape[10] += g_search_pops;
+    if (g_search_unsafe) {
+      g_shape[9]++;
+      g_shape[11] += g_search_pops;
+      g_shape[12] += g_pops_to_unsafe;
+    }
+    g_search_unsafe = false;
+    g_search_pops = 0;
   }
   void shape_size(size_t n) {
     if ((long long)n > g_shape[4]) g_shape[4] = (long long)n;
@@ -560,9 +583,16 @@ template <class T> struct Planner {
     cl2.clear();
     op2.clear();
     op2.insert(N2<T>{si, sj, 0, nm_f[(size_t)si * N + sj], nullptr});
+#ifdef ORC_SHAPE_STATS
+    struct End {
+      Planner* p;
+      ~End() { p->shape_search_end(); }
+    } end_{this};
+#endif
     while (!op2.empty()) {
 #ifdef ORC_SHAPE_STATS
       shape_size(op2.size());
+      g_search_pops++;
 #endif
       auto it = op2.begin();
       const N2<T>* cur = &*cl2.insert(*it).first;
@@ -1181,6 +1211,6 @@ extern "C" void orc_run_batch_threads(void* const* hs, int n, const float* vel, 
 
 #ifdef ORC_SHAPE_STATS
 extern "C" void orc_shape_stats(long long* out) {
-  for (int q = 0; q < 8; ++q) out[q] = orc::g_shape[q], orc::g_shape[q] = 0;
+  for (int q = 0; q < 16; ++q) out[q] = orc::g_shape[q], orc::g_shape[q] = 0;
 }
 #endif

@@ -458,6 +458,7 @@ struct hastar_handle_s {
   float* rfield = nullptr;
   bool rvalid = false;
   float rhlim = 0.0f;
+  int rstart = 0;
 };
 
 // One allocation for the persistent state of a batch of identical planners
@@ -1830,8 +1831,8 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
     N = std::max(N, hs[i]->desc.N);
   }
   RelaxParams rp{};
-  rp.delta = opts && opts->delta > 0.0f ? opts->delta : 0.5f;
-  rp.h_stop = opts && opts->h_stop >= 1.0f ? opts->h_stop : 3.0f;
+  rp.delta = opts && opts->delta > 0.0f ? opts->delta : 0.25f;
+  rp.h_stop = opts && opts->h_stop >= 1.0f ? opts->h_stop : 1.5f;
   rp.max_rounds = opts && opts->max_rounds > 0 ? opts->max_rounds : (1 << 20);
   rp.h_weight = opts && opts->h_weight > 0.0f ? opts->h_weight : 1.2f;
   const int nodes = opts && opts->max_nodes > 0 ? opts->max_nodes : (1 << 20);
@@ -1864,7 +1865,7 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
         h->rfield = nullptr;
         return fail(HASTAR_ENOMEM, "relaxed heuristic field: hipMalloc failed");
       }
-      fields[i] = RelaxField{h->rfield, h->rhlim, h->rvalid ? 1 : 0};
+      fields[i] = RelaxField{h->rfield, h->rhlim, h->rvalid ? 1 : 0, h->rstart};
     }
     if ((size_t)n > DC.rfields_cap) {
       HIPCHK(hipStreamSynchronize(st));
@@ -1887,6 +1888,7 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
   for (int i = 0; reuse && i < n; ++i) {
     hs[i]->rvalid = fields[i].valid != 0;
     hs[i]->rhlim = fields[i].hlim;
+    hs[i]->rstart = fields[i].start_ij;
   }
   float ms = 0.0f;
   hipEventElapsedTime(&ms, DC.ev0, DC.ev1);

@@ -244,13 +244,14 @@ struct RelaxArena {
 // persists across find_path calls the same way, AStar.cpp:56-60, local_planner.cpp:316).
 struct RelaxField {
   float* dist;      // N*N, or null: use the arena's scratch
-  float hlim;       // bound of the cells the Dijkstra left unsettled
+  float hlim;       // the ellipse bound the field was built with (relaxed_h)
   int valid;        // 1: dist/hlim hold a finished field
+  int start_ij;     // the start cell (i << 16 | j) the ellipse was built around
 };
 // options of a relaxed launch (kernel side of hastar_relaxed_opts)
 struct RelaxParams {
   float delta;      // frontier width (m): every open node with f <= min f + delta is expanded in a round
-  float h_stop;     // the Dijkstra stops at h_stop x dist(start) + 64 buckets (cells beyond get that bound)
+  float h_stop;     // the Dijkstra covers the ellipse d(c) + |c - start| <= h_stop x |goal - start| + 64 moves
   int max_rounds;
   float h_weight;   // f = g + h_weight x max(h, Dubins length) (1: the reference's f)
 };

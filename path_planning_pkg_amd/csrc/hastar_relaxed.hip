@@ -31,6 +31,22 @@ namespace hastar {
 
 constexpr int RW = 8;                        // wavefronts per planner workgroup
 constexpr int DU = 4;                        // Dijkstra bucket entries per thread in flight
+constexpr int BL = 1536;                     // Dijkstra bucket entries per ring slot held in LDS
+// The bucket ring lives in dynamic LDS (8 x BL entries, 96 KiB: one 8-wave workgroup per CU
+// leaves the LDS to it); entries past BL of a slot spill to the arena's HBM lists.
+constexpr size_t RELAX_DYN_LDS = (size_t)8 * BL * sizeof(BucketEntry);
+__device__ __forceinline__ BucketEntry bucket_get(const RelaxArena& A, const BucketEntry* lds, int slot, int e) {
+  return e < BL ? lds[slot * BL + e] : A.bucket[(size_t)slot * A.bcap + (e - BL)];
+}
+__device__ __forceinline__ bool bucket_put(const RelaxArena& A, BucketEntry* lds, int slot, int e, BucketEntry v) {
+  if (e < BL) {
+    lds[slot * BL + e] = v;
+    return true;
+  }
+  if (e - BL >= A.bcap) return false;
+  A.bucket[(size_t)slot * A.bcap + (e - BL)] = v;
+  return true;
+}
 
 // diagnostic build (-DRELAX_STAMPS): per-phase cycles of the Dijkstra's bucket loop, thread 0
 #ifdef RELAX_STAMPS
@@ -104,7 +120,6 @@ struct RelaxShared {
   int planner;
   int cnt[8];               // Dijkstra bucket fill counts (ring of 8)
   int overflow, hover;
-  int stop_at;              // last bucket the Dijkstra settles (-1: start not settled yet)
   int settled;              // cells settled (diagnostic: astar_pops)
   int buckets;              // Dijkstra buckets processed
   int nA, nB, nE, eNext, nodes;
@@ -116,8 +131,9 @@ struct RelaxShared {
   unsigned long long stamp[6];
 };
 
-// Phase 1: Dial-bucket Dijkstra from the goal cell into `dist`; returns the heuristic bound
-// of cells the early stop left unsettled (every such cell is at least that far).
+// Phase 1: Dial-bucket Dijkstra from the goal cell into `dist`, restricted to the ellipse
+// d(c) + |c - start| <= bound (bound = h_stop x |goal - start| + 64 moves); returns the
+// bound.  A cell left unsettled gets the lower bound bound - |c - start| (relaxed_h).
 // Bucket entries are {cell, distance bits}: an entry is live iff the cell's distance is still
 // the one it was pushed with (a cell improves only by a strictly smaller push), so no settled
 // flags are needed.  Moves cost >= wb, so iteration `cur` pushes only into buckets cur+1 ..
@@ -126,7 +142,7 @@ struct RelaxShared {
 // The run ends after 3 empty buckets in a row (nothing can be pushed past them) or at the
 // early stop; both decisions use values every thread reads identically.
 __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, const RelaxParams& rp,
-                                   float* dist_f) {
+                                   float* dist_f, BucketEntry* bl) {
   const int tid = threadIdx.x, NT = blockDim.x;
   const int N = P.N;
   const float wb = P.act_cost_axis;
@@ -137,30 +153,31 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
   for (size_t i = tid; i < NN; i += NT) dist[i] = 0x7f800000u;
   // entries name cells as (i << 16 | j): no integer division per entry
   const uint32_t goal_ij = ((uint32_t)P.goal_cx << 16) | (uint32_t)P.goal_cy;
-  const uint32_t start_ij = ((uint32_t)P.start_cx << 16) | (uint32_t)P.start_cy;
   const float inv_wb = 1.0f / wb;  // bucket index only: rounding is absorbed by the clamp below
+  // relax only inside the ellipse d(c) + |c - start| <= bound around the goal-start segment
+  const float gsx = (float)(P.goal_cx - P.start_cx), gsy = (float)(P.goal_cy - P.start_cy);
+  const float bound = rp.h_stop * P.res * sqrtf(gsx * gsx + gsy * gsy) + 64.0f * wb;
   block_sync();
   if (tid == 0) {
     dist[(size_t)P.goal_cx * N + P.goal_cy] = 0u;
-    A.bucket[0] = BucketEntry{goal_ij, 0u};
+    bl[0] = BucketEntry{goal_ij, 0u};
     for (int k = 0; k < 8; ++k) S.cnt[k] = k == 0 ? 1 : 0;
     S.overflow = 0;
-    S.stop_at = -1;
     S.settled = 0;
   }
   block_sync();
   const int max_b = 4 * N + 64;
   int cur = 0, empty_run = 0;
+  const int cap = BL + A.bcap;
 #ifdef RELAX_STAMPS
   unsigned long long rst[6] = {0, 0, 0, 0, 0, 0};
 #endif
   for (; cur < max_b; ++cur) {
     const int slot = cur & 7;
-    const int m = min(S.cnt[slot], A.bcap);
-    const int stop_at = S.stop_at;
+    const int m = min(S.cnt[slot], cap);
     if (tid == 0) S.cnt[(cur - 1) & 7] = 0;  // recycled: pushed again no earlier than iteration cur + 4
     empty_run = m == 0 ? empty_run + 1 : 0;
-    if (empty_run >= 3 || (stop_at >= 0 && cur > stop_at)) break;
+    if (empty_run >= 3) break;
     // DU entries per thread at a time, phase by phase (entries, then distances and occupancy,
     // then every relaxation's atomicMin, then the pushes), so the dependent global round trips
     // of DU entries overlap instead of queueing one entry after the other
@@ -173,7 +190,7 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
 #pragma unroll
       for (int u = 0; u < DU; ++u) {
         const int e = e0 + u * NT;
-        en[u] = e < m ? A.bucket[(size_t)slot * A.bcap + e] : BucketEntry{0xffffffffu, 0u};
+        en[u] = e < m ? bucket_get(A, bl, slot, e) : BucketEntry{0xffffffffu, 0u};
       }
       RSTAMP(0);
 #pragma unroll
@@ -194,10 +211,7 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
         const uint32_t cij = en[u].cell;
         // live: still the cell's distance (else a shorter push settles it); expanding: enterable
         const bool live = cij != 0xffffffffu && dc[u] == en[u].d;
-        if (live) {
-          ++settled;
-          if (cij == start_ij) atomicCAS(&S.stop_at, -1, cur + (int)((rp.h_stop - 1.0f) * (float)cur) + 64);
-        }
+        if (live) ++settled;
         const bool expand = live && (cij == goal_ij || oc[u] < P.thr);
         const float d = __uint_as_float(dc[u]);
         const int ci = (int)(cij >> 16), cj = (int)(cij & 0xffffu);
@@ -241,13 +255,17 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
           if (old[u][a] <= nb) continue;  // no improvement (or not relaxed at all)
           const int di = a < 4 ? ((a & 1) ? 0 : (a == 0 ? 1 : -1)) : ((a & 1) ? 1 : -1);
           const int dj = a < 4 ? ((a & 1) ? (a == 1 ? 1 : -1) : 0) : ((a & 2) ? 1 : -1);
-          const uint32_t pij = (uint32_t)((int)(cij >> 16) + di) << 16 | (uint32_t)((int)(cij & 0xffffu) + dj);
+          const int pi = (int)(cij >> 16) + di, pj = (int)(cij & 0xffffu) + dj;
+          // the ellipse: a cell whose distance plus its straight-line distance to the start
+          // exceeds the bound cannot lie on a path the search needs; it stays unsettled
+          const float es = P.res * sqrtf((float)((pi - P.start_cx) * (pi - P.start_cx) + (pj - P.start_cy) * (pj - P.start_cy)));
+          if (__uint_as_float(nb) + es > bound) continue;
+          const uint32_t pij = (uint32_t)pi << 16 | (uint32_t)pj;
           int kb = (int)(__uint_as_float(nb) * inv_wb);
           kb = max(kb, cur + 1);
           kb = min(kb, cur + 3);
           const int pos = atomicAdd(&S.cnt[kb & 7], 1);
-          if (pos < A.bcap) A.bucket[(size_t)(kb & 7) * A.bcap + pos] = BucketEntry{pij, nb};
-          else S.overflow = 1;
+          if (!bucket_put(A, bl, kb & 7, pos, BucketEntry{pij, nb})) S.overflow = 1;
         }
       }
     }
@@ -265,11 +283,21 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
   return (float)cur * wb;
 }
 
+// The heuristic of cell (i, j): its Dijkstra distance, or for a cell the ellipse left
+// unsettled the bound minus its straight-line distance to the field's start cell.
+__device__ __forceinline__ float relaxed_h(const PlannerDev& P, const float* dist, size_t cell, int i, int j,
+                                          float bound, int sx, int sy) {
+  const float d = ld_dist(dist, cell);
+  if (d < FLT_MAX) return d;
+  const float es = P.res * sqrtf((float)((i - sx) * (i - sx) + (j - sy) * (j - sy)));
+  return fmaxf(bound - es, 0.0f);
+}
+
 // One expansion by one wavefront: the exact kernel's fused successor block without the
 // closed set and the lazy A* (the heuristic is the Dijkstra field).
 __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, ApfStage& apfs,
-                               const GoalC& GC, const float* dist, float hlim, float hw, int idx, int wv, int lane,
-                               uint2* list_b) {
+                               const GoalC& GC, const float* dist, float hlim, int hs_x, int hs_y, float hw, int idx,
+                               int wv, int lane, uint2* list_b) {
   const Node3 cur = gload(&A.nodes[idx]);
   const uint32_t key = ufu(cur.key);
   const float cg = uff(cur.g), cxp = uff(cur.x), cyp = uff(cur.y), chd = uff(cur.h), cvm = uff(cur.vmin);
@@ -354,9 +382,7 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
   if (lead) {
     const size_t cell = (size_t)scx * P.N + scy;
     occv = gp(P.occ)[cell];
-    h2 = ld_dist(dist, cell);
-    // unsettled cells (beyond the Dijkstra's early stop, or enclosed) are at least hlim away
-    if (!(h2 < hlim)) h2 = hlim;
+    h2 = relaxed_h(P, dist, cell, scx, scy, hlim, hs_x, hs_y);
   }
   const float dub = cand_dubins(P.r_min, GC, P.goal_h, sx, sy, sh, gs, lane);
   const float fc = apf_fused(P, apfs, cxp, cyp, sx, sy, sh, __ballot(lead), gs, lane);
@@ -398,24 +424,28 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
 }
 
 __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, const RelaxParams& rp,
-                            RelaxField* F) {
+                            RelaxField* F, BucketEntry* bl) {
   const int tid = threadIdx.x, NT = blockDim.x, wv = tid >> 6, lane = tid & 63;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   // the heuristic field: the planner's own (kept across calls until reset / update_goal, like
   // the reference's A* memo) or the arena's scratch
   float* dist = (F && F->dist) ? F->dist : A.dist;
   float hlim;
+  int hs_x = P.start_cx, hs_y = P.start_cy;  // the start cell the field's ellipse was built around
   if (F && F->dist && F->valid) {
     hlim = F->hlim;
+    hs_x = F->start_ij >> 16;
+    hs_y = F->start_ij & 0xffff;
     if (tid == 0) {
       S.buckets = 0;
       S.settled = 0;
       S.overflow = 0;
     }
   } else {
-    hlim = relaxed_heuristic(P, A, S, rp, dist);
+    hlim = relaxed_heuristic(P, A, S, rp, dist, bl);
     if (tid == 0 && F && F->dist) {
       F->hlim = hlim;
+      F->start_ij = (P.start_cx << 16) | P.start_cy;
       F->valid = 1;
     }
   }
@@ -426,8 +456,8 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
   if (tid == 0) {
     Node3 s0;
     s0.key = key3(P.start_cx, P.start_cy, P.start_bin);
-    float h0 = ld_dist(dist, (size_t)P.start_cx * P.N + P.start_cy);
-    if (!(h0 < hlim)) h0 = hlim;
+    const float h0 = relaxed_h(P, dist, (size_t)P.start_cx * P.N + P.start_cy, P.start_cx, P.start_cy, hlim, hs_x,
+                               hs_y);
     s0.f = h0;
     s0.l = s0.r = s0.p = NIL;
     s0.cc = (uint32_t)P.start_ci << 8;
@@ -498,7 +528,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
       if (lane == 0) e = atomicAdd(&S.eNext, 1);
       e = ufi(e);
       if (e >= nE) break;
-      relaxed_expand(P, A, S, S.apf[wv], GC, dist, hlim, rp.h_weight, LE[e], wv, lane, LB);
+      relaxed_expand(P, A, S, S.apf[wv], GC, dist, hlim, hs_x, hs_y, rp.h_weight, LE[e], wv, lane, LB);
     }
     block_sync();
     if (tid == 0) {
@@ -641,6 +671,7 @@ __global__ __launch_bounds__(RW * 64) void k_relaxed_search(const PlannerDev* __
                                                            const RelaxArena* __restrict__ arenas, int* next,
                                                            RelaxParams rp, RelaxField* fields) {
   __shared__ RelaxShared S;
+  extern __shared__ BucketEntry relax_dyn_lds[];
   const RelaxArena A = arenas[blockIdx.x];
   for (;;) {
     if (threadIdx.x == 0) S.planner = atomicAdd(next, 1);
@@ -648,7 +679,7 @@ __global__ __launch_bounds__(RW * 64) void k_relaxed_search(const PlannerDev* __
     const int pi = S.planner;
     block_sync();
     if (pi >= n) break;
-    relaxed_one(descs[pi], A, S, rp, fields ? &fields[pi] : nullptr);
+    relaxed_one(descs[pi], A, S, rp, fields ? &fields[pi] : nullptr, relax_dyn_lds);
   }
 }
 
@@ -656,7 +687,15 @@ hipError_t launch_relaxed(const PlannerDev* d_descs, int n, const RelaxArena* d_
                           const RelaxParams& rp, RelaxField* d_fields, hipStream_t st) {
   hipError_t e = hipMemsetAsync(d_next, 0, sizeof(int), st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_relaxed_search, dim3(n_arenas), dim3(RW * 64), 0, st, d_descs, n, d_arenas, d_next, rp, d_fields);
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void*>(k_relaxed_search),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)RELAX_DYN_LDS);
+    if (a != hipSuccess) return a;
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_relaxed_search, dim3(n_arenas), dim3(RW * 64), RELAX_DYN_LDS, st, d_descs, n, d_arenas, d_next,
+                     rp, d_fields);
   return hipGetLastError();
 }
 int relaxed_waves() { return RW; }

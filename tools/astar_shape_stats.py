@@ -1,6 +1,8 @@
 """Analysis: how often does the inner A*'s open-tree SHAPE decide a find/insert?
 
 Builds the oracle with -DORC_SHAPE_STATS into /tmp and replays synthetic cfg3 seeds.
+Per inner search: how many meet at least one shape-dependent event (a tree-free run would
+have to restart them with the tree) and the pops they take before the first event.
 Counts per find(): probes, probes with a node of the same cell in the open tree,
 "unsafe" finds (a same-cell node with f < probe f: the lower_bound predicate is then
 non-monotone and the result depends on the tree shape), unsafe inserts (same-cell node
@@ -28,11 +30,12 @@ for s in seeds:
     cfg, proto = synthetic(1024, 72, 200, s)
     o = po.OraclePlanner(cfg)
     drive(o, proto)
-    st = (C.c_longlong * 8)()
+    st = (C.c_longlong * 16)()
     L.orc_shape_stats(st)
     r = o.find_path(proto["vel"], proto["start"])
     L.orc_shape_stats(st)
     names = ["probes", "same_cell_present", "unsafe_find", "unsafe_insert", "max_open", "pops_open_gt256",
-             "pops_open_gt1024", "order_violations"]
+             "pops_open_gt1024", "order_violations", "searches", "searches_shape_dependent", "pops_all",
+             "pops_in_shape_dependent_searches", "pops_before_first_event"]
     print(json.dumps(dict(seed=s, apops=r["stats"]["astar_pops"], **{n: st[q] for q, n in enumerate(names)})))
     o.close()

@@ -7,5 +7,5 @@ timeout -k 10 300 python -u tools/relaxed_sweep.py --groups syn512,cfg3,cfg5 --o
 python - <<'PY'
 import json
 for r in json.load(open("gpurun_out/rlx/sweep.json")):
-    print(r["group"], r["delta"], r["h_weight"], r["ms"], r["ok"], r["cost_ratio_mean"], [round(x[0], 2) for x in r["split_ms"]], [round(x[1], 2) for x in r["split_ms"]])
+    print(r["group"], r["delta"], r["h_weight"], r["h_stop"], r["ms"], r["ok"], r["cost_ratio_mean"], [round(x[0], 2) for x in r["split_ms"]], [round(x[1], 2) for x in r["split_ms"]])
 PY
