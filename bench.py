@@ -118,6 +118,8 @@ def parse_args(argv=None):
     ap.add_argument("--relaxed-delta", type=float, default=0.25, help="relaxed mode: frontier width (m)")
     ap.add_argument("--relaxed-weight", type=float, default=1.2, help="relaxed mode: heuristic weight")
     ap.add_argument("--no-relaxed", action="store_true", help="cfg5: skip the relaxed-mode comparison")
+    ap.add_argument("--relaxed-batch", type=int, default=4096,
+                    help="cfg3/cfg4: queries of the batch also planned in one relaxed call (query rate)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: exercises the launcher, sharding and reductions only (CPU rehearsal)")
@@ -224,7 +226,7 @@ def main():
         planners[li].reset()
         _, longest["gpu_ms_alone"] = gpu.find_path_batch([planners[li]], [vels[li]], [starts[li]], cap=8192)
         relaxed = relaxed_latency_phase(gpu, planners, vels, starts, last, lat_ids + [li], qids, args,
-                                        lat + [longest["gpu_ms_alone"]])
+                                        lat + [longest["gpu_ms_alone"]], B / (ms_per_step * 1e-3))
         traffic = None
         pmc = ROOT / "profiles" / "pmc_search_summary.json"
         if pmc.exists():
@@ -442,7 +444,7 @@ def map_build_phase(args, gpu, dist, torch, rank, world, device):
             "protocol": "update_goal + 5 x {decay, 200 boxes} per map (tests/scenarios.py::drive)"}
 
 
-def relaxed_latency_phase(gpu, planners, vels, starts, last, ids, qids, args, exact_ms):
+def relaxed_latency_phase(gpu, planners, vels, starts, last, ids, qids, args, exact_ms, exact_qps):
     """The RELAXED mode (hastar_find_path_relaxed_batch, SURVEY.md §8(f) rank 4: non-parity,
     frontier-parallel with a backward-Dijkstra heuristic) on the latency queries and the longest
     query, one query per call, beside the exact mode's result for the same inputs (the last timed
@@ -457,7 +459,22 @@ def relaxed_latency_phase(gpu, planners, vels, starts, last, ids, qids, args, ex
         exp.append(int(r["stats"]["pops"]))
         if r["ok"] and last.ok[i]:
             ratios.append(float(r["cost"]) / float(last.cost[i]))
-    return {"queries": [qids[i] for i in ids], "gpu_ms": ms, "gpu_median_ms": float(np.median(ms)) if ms else None,
+    # the batch's first queries in one relaxed call (one workgroup per planner, every CU busy),
+    # against the exact mode's query rate of the timed steps
+    nb = min(args.relaxed_batch, len(planners))
+    batch = None
+    if nb > 0:
+        t0 = time.perf_counter()
+        rb, bms = gpu.find_path_batch(planners[:nb], vels[:nb], starts[:nb], cap=8192, relaxed=opts)
+        wall = time.perf_counter() - t0
+        br = [float(r["cost"]) / float(last.cost[i]) for i, r in enumerate(rb) if r["ok"] and last.ok[i]]
+        batch = {"queries": nb, "kernel_ms": bms, "wall_ms": wall * 1e3, "queries_per_s": nb / (bms * 1e-3),
+                 "exact_queries_per_s": exact_qps, "ok": sum(int(r["ok"]) for r in rb),
+                 "exact_ok": int(sum(int(last.ok[i]) for i in range(nb))),
+                 "status": sorted({int(r["stats"]["status"]) for r in rb}),
+                 "cost_ratio_vs_exact_mean": float(np.mean(br)) if br else None,
+                 "cost_ratio_vs_exact_max": float(np.max(br)) if br else None}
+    return {"batch": batch, "queries": [qids[i] for i in ids], "gpu_ms": ms, "gpu_median_ms": float(np.median(ms)) if ms else None,
             "exact_gpu_ms_same_queries": exact_ms, "ok": ok, "exact_ok": int(sum(int(last.ok[i]) for i in ids)),
             "cost_ratio_vs_exact": ratios, "expansions": exp, "opts": opts,
             "note": "non-parity mode: valid paths (tests/test_gpu_relaxed.py), cost relative to the exact "

@@ -162,7 +162,7 @@ typedef struct hastar_relaxed_opts {
   float delta;     /* frontier width in metres [0.25] */
   float h_stop;    /* the Dijkstra covers the ellipse d(c) + |c - start| <= h_stop x |goal - start| + 64 moves;
                       cells outside get bound - |c - start| [1.5] */
-  int max_nodes;   /* node capacity per search; beyond it the search ends with HASTAR_EOVERFLOW [1 << 20] */
+  int max_nodes;   /* node capacity per search; beyond it the search ends with HASTAR_EOVERFLOW [1 << 18] */
   int max_rounds;  /* [1 << 20] */
   float h_weight;  /* f = g + h_weight x max(h, Dubins length); > 1 trades cost for speed [1.2]
                       (at the defaults the measured costs were 0.92-1.00 x the exact mode's,

@@ -1835,7 +1835,7 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
   rp.h_stop = opts && opts->h_stop >= 1.0f ? opts->h_stop : 1.5f;
   rp.max_rounds = opts && opts->max_rounds > 0 ? opts->max_rounds : (1 << 20);
   rp.h_weight = opts && opts->h_weight > 0.0f ? opts->h_weight : 1.2f;
-  const int nodes = opts && opts->max_nodes > 0 ? opts->max_nodes : (1 << 20);
+  const int nodes = opts && opts->max_nodes > 0 ? opts->max_nodes : (1 << 18);
   HIPCHK(hipSetDevice(dev));
   DeviceCtx& DC = *hs[0]->dc;
   std::lock_guard<std::mutex> lk(DC.mu);
