@@ -80,6 +80,67 @@ def synthetic(N, bins, K, seed, res=0.5, clear=8.0):
     return cfg, proto
 
 
+class MT19937:
+    """std::mt19937 with its default (init_genrand) seeding, as libstdc++ defines it."""
+
+    def __init__(self, seed):
+        mt = [seed & 0xffffffff]
+        for i in range(1, 624):
+            mt.append((1812433253 * (mt[i - 1] ^ (mt[i - 1] >> 30)) + i) & 0xffffffff)
+        self.mt, self.i = mt, 624
+
+    def __call__(self):
+        mt = self.mt
+        if self.i >= 624:
+            for k in range(624):
+                y = (mt[k] & 0x80000000) | (mt[(k + 1) % 624] & 0x7fffffff)
+                mt[k] = mt[(k + 397) % 624] ^ (y >> 1) ^ (0x9908b0df if y & 1 else 0)
+            self.i = 0
+        y = mt[self.i]
+        self.i += 1
+        y ^= y >> 11
+        y ^= (y << 7) & 0x9d2c5680
+        y ^= (y << 15) & 0xefc60000
+        return (y ^ (y >> 18)) & 0xffffffff
+
+
+def _uniform_f32(rng, a, b):
+    """std::uniform_real_distribution<float>(a, b)(rng) of libstdc++: generate_canonical<float,
+    24> takes one 32-bit draw, u / 2^32 in float (clamped below 1), then canonical * (b - a) + a."""
+    c = np.float32(rng()) / np.float32(4294967296.0)
+    if c >= np.float32(1):
+        c = np.nextafter(np.float32(1), np.float32(0))
+    return np.float32(c * np.float32(b - a)) + a
+
+
+def synthetic_ref(N, bins, K, seed, res=0.5, clear=8.0):
+    """SURVEY.md §8d's synthetic case drawn the way the survey's reference runs drew it:
+    std::mt19937(seed) and std::uniform_real_distribution<float>; per candidate box the centre
+    (x in [-0.8W, 0.2W], y in [-0.5W, 0.5W]) then the sides U(1, 6) m; a box whose centre lies
+    within 8 m of the start or the goal is redrawn.  With these draws the oracle reproduces the
+    pop counts the survey measured on the compiled reference (cfg3 seed 1: 3,297 pops; seed 3:
+    7,107 pops, 21,170 successors, 20,234 inner A* pops), which
+    pins it at full size (tools/mt19937_synth.cpp is the same generator in C++)."""
+    f = np.float32
+    W = f(N) * f(res)
+    ax, bx = f(-0.8 * float(W)), f(0.2 * float(W))
+    ay, by = f(-0.5 * float(W)), f(0.5 * float(W))
+    stx = f(-0.6 * float(W))
+    rng = MT19937(seed)
+    boxes = []
+    while len(boxes) < K:
+        cx, cy = _uniform_f32(rng, ax, bx), _uniform_f32(rng, ay, by)
+        sx, sy = _uniform_f32(rng, f(1), f(6)), _uniform_f32(rng, f(1), f(6))
+        if f(np.hypot(f(cx - stx), cy)) < f(clear) or f(np.hypot(cx, cy)) < f(clear):
+            continue
+        boxes.append([cx, cy, sx, sy])
+    cfg = PlannerConfig(grid_size=N, num_angle_bins=bins, steering=steering_from_degrees([-30, -15, 0, 15, 30]))
+    proto = dict(goal=[0.0, 0.0, 0.0], start=[float(stx), 0.0, 0.0], vel=2.0, cycles=5,
+                 lines=np.zeros((0, 4), np.float32), line_conf=0.6, line_width=1.25,
+                 boxes=np.array(boxes, np.float32).reshape(-1, 4), box_conf=0.75, apf_r=2.5)
+    return cfg, proto
+
+
 def drive(planner, proto):
     """The fixture protocol: update_goal, 5 x {decay, lines, boxes}, reset."""
     planner.update_goal(proto["goal"], proto["start"])

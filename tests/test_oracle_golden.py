@@ -2,7 +2,9 @@
 
 These pin the oracle: utils/hybrid_astar/plot.py:47-51, utils/dubins_paths.py:6 and
 utils/vehicle_mode.py:12 were printed by the reference with ostream's default %g; we
-compare at that precision, element by element.
+compare at that precision, element by element.  At full cfg3 size the oracle is pinned by the
+pop / successor / inner-A* counts the survey measured on the compiled reference for its
+std::mt19937 inputs (tests/golden/survey_reference_counts.json).
 """
 import json
 import math
@@ -58,3 +60,21 @@ def test_equal_f_insert_is_dropped(oracle_lib):
     keys = o.closed_keys()
     assert len(keys) == st["closed_size"]
     assert len({tuple(k) for k in keys.tolist()}) == len(keys)
+
+
+def test_oracle_matches_survey_reference_counts(oracle_lib):
+    """The oracle at full cfg3 size against counts the survey measured on the compiled
+    reference (tests/golden/survey_reference_counts.json): the same std::mt19937 inputs
+    (tests/scenarios.py:synthetic_ref) give the same pops, successors and inner A* pops."""
+    from tests.scenarios import synthetic_ref
+    g = json.loads((GOLDEN / "survey_reference_counts.json").read_text())
+    for case in g["cases"]:
+        cfg, proto = synthetic_ref(g["grid"], g["angle_bins"], g["obstacles"], case["seed"])
+        o = oracle_lib.OraclePlanner(cfg)
+        drive(o, proto)
+        r = o.find_path(proto["vel"], proto["start"])
+        o.close()
+        assert r["ok"]
+        for k in ("pops", "successors", "astar_pops"):
+            if k in case:
+                assert r["stats"][k] == case[k], f"seed {case['seed']}: {k} {r['stats'][k]} vs reference {case[k]}"
