@@ -16,7 +16,12 @@
 //   * find_path appends to `path`/`curvature` like the reference does for the empty
 //     vectors its caller passes (HybridAStar.cpp:208-262 mixes push_back and resize, so
 //     non-empty inputs are not a supported contract there either);
-//   * the device is HIP ordinal $HASTAR_DEVICE (default 0).
+//   * the device is HIP ordinal $HASTAR_DEVICE (default 0);
+//   * extension: set_relaxed(true) — or $HASTAR_RELAXED=1 at construction, so the unchanged
+//     caller can opt in — routes find_path to the RELAXED search mode
+//     (hastar_find_path_relaxed_batch).  That mode is NOT the reference's
+//     algorithm: its paths are valid and comparable in cost but not identical.  It keeps its
+//     heuristic field until reset() / update_goal(), as the reference keeps its A* memo.
 #ifndef HYBRID_ASTAR
 #define HYBRID_ASTAR
 
@@ -72,7 +77,12 @@ class HybridAStar<float> {
     p.curvature_weights = curvature_weights.data();
     const char* dev = std::getenv("HASTAR_DEVICE");
     check(hastar_create_f32(&p, dev ? std::atoi(dev) : 0, &_h));
+    const char* rel = std::getenv("HASTAR_RELAXED");
+    _relaxed = rel && std::atoi(rel) != 0;
   }
+  // extension (not in the reference): select the relaxed search mode for find_path
+  void set_relaxed(bool on) { _relaxed = on; }
+  bool relaxed() const { return _relaxed; }
   ~HybridAStar() {
     if (_h) hastar_destroy(_h);
   }
@@ -130,7 +140,16 @@ class HybridAStar<float> {
     float cost = std::numeric_limits<float>::max();
     if (_xyh.size() < 3 * _cap) _xyh.resize(3 * _cap);
     if (_curv.size() < _cap) _curv.resize(_cap);
-    int rc = hastar_find_path(_h, vel_init, s, _xyh.data(), _curv.data(), (int)_cap, &len, &cost, &ok, nullptr);
+    int rc;
+    if (_relaxed) {
+      hastar_relaxed_opts o{};
+      o.reuse_heuristic = 1;
+      hastar_stats st{};
+      rc = hastar_find_path_relaxed_batch(&_h, 1, &vel_init, s, _xyh.data(), _curv.data(), (int)_cap, &len, &cost,
+                                          &ok, &st, &o);
+    } else {
+      rc = hastar_find_path(_h, vel_init, s, _xyh.data(), _curv.data(), (int)_cap, &len, &cost, &ok, nullptr);
+    }
     if (rc == HASTAR_ENOSPC && len > (int)_cap) {  // grow and fetch the stored path
       _cap = (size_t)len;
       _xyh.resize(3 * _cap);
@@ -157,6 +176,7 @@ class HybridAStar<float> {
   hastar_handle _h = nullptr;
   int _n;
   size_t _cap = 4096;
+  bool _relaxed = false;
   std::vector<float> _xyh, _curv;
   mutable std::vector<std::vector<float>> _grid_cache;
 };

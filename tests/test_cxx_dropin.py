@@ -51,6 +51,22 @@ def test_dropin_harness_matches_oracle_and_golden(tmp_path, oracle_lib):
     assert mine == g["path_start_to_goal"]
 
 
+@pytest.mark.gpu
+def test_dropin_harness_relaxed_mode(tmp_path):
+    """The unchanged harness with $HASTAR_RELAXED=1: the class routes find_path to the relaxed
+    (non-parity) mode; the result is a path from the goal end back to the harness start."""
+    import os
+    env = dict(os.environ, HASTAR_RELAXED="1")
+    out = subprocess.run([str(_build(tmp_path))], check=True, capture_output=True, text=True, timeout=120,
+                         env=env).stdout
+    lines = out.strip().splitlines()
+    ok, cost_bits, n, rows = lines[0].split()
+    assert int(ok) == 1 and int(n) >= 2
+    pts = np.array([[int(v, 16) for v in ln.split()] for ln in lines[1:]], np.uint32)[:, :3].view(np.float32)
+    assert np.allclose(pts[-1, :2], [18.0, 18.0], atol=1e-3)  # the harness start (test_hybrid_astar.cpp)
+    assert np.hypot(pts[0, 0] - 26.0, pts[0, 1] - 36.0) < 1.0  # ... and the goal end first
+
+
 VG_MAIN = r"""
 #include <cstdio>
 #include "VelocityGenerator.h"
