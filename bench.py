@@ -1,7 +1,8 @@
 """bench.py — Hybrid A* node expansions/sec on the 1024x1024x72 grid (BASELINE.json configs[2]).
 
 Workload (one "step"): a batch of B independent planners per GPU (SURVEY.md §8d synthetic
-generator: N = 1024, 72 angle bins, K = 200 box obstacles, seed = query id + 1; the
+generator with its std::mt19937 draws, tests/scenarios.py:synthetic_ref: N = 1024, 72 angle bins,
+K = 200 box obstacles, seed = query id + 1; the
 reference's only motion mode: forward Dubins), each already set up in HBM (update_goal,
 5 x {decay, boxes} through the batched map-update ABI); the step resets the holonomic memo
 of every planner (HybridAStar::reset) and runs ONE batched find_path — one wavefront per
@@ -115,6 +116,9 @@ def parse_args(argv=None):
                          "(BASELINE.json configs[3]); cfg5: 20 Hz replan loop of start/goal pairs (configs[4])")
     ap.add_argument("--map-queries", type=int, default=16, help="cfg4: maps built both locally and row-sharded")
     ap.add_argument("--pairs", type=int, default=64, help="cfg5: start/goal pairs in total, dealt over the ranks")
+    ap.add_argument("--generator", choices=("mt19937", "pcg64"), default="mt19937",
+                    help="cfg3/cfg4 inputs: SURVEY.md §8d's std::mt19937 draws (the survey's reference runs) or "
+                         "round 1's numpy PCG64 draws")
     ap.add_argument("--relaxed-delta", type=float, default=0.25, help="relaxed mode: frontier width (m)")
     ap.add_argument("--relaxed-weight", type=float, default=1.2, help="relaxed mode: heuristic weight")
     ap.add_argument("--no-relaxed", action="store_true", help="cfg5: skip the relaxed-mode comparison")
@@ -248,7 +252,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (SURVEY.md §8d generator; seeds = query ids + 1)",
+            "data": ("synthetic (SURVEY.md §8d generator, std::mt19937 draws as in the survey's reference runs; "
+                     "seeds = query ids + 1)") if args.generator == "mt19937" else
+                    "synthetic (SURVEY.md §8d geometry, numpy PCG64 draws; seeds = query ids + 1)",
             "config": {"workload": f"{args.workload}: {args.grid}x{args.grid}x{args.bins} grid, {args.obstacles} box "
                                    f"obstacles, batch of {B} independent queries per GPU, forward Dubins"
                                    + (", map build row-sharded over the ranks + RCCL all-gather (map_build)"
@@ -290,8 +296,9 @@ def main():
 
 
 def query_case(args, q):
-    from tests.scenarios import synthetic
-    cfg, proto = synthetic(args.grid, args.bins, args.obstacles, seed=q + 1)
+    from tests.scenarios import synthetic, synthetic_ref
+    gen = synthetic_ref if args.generator == "mt19937" else synthetic
+    cfg, proto = gen(args.grid, args.bins, args.obstacles, seed=q + 1)
     cfg.values["max_pops"] = args.max_pops
     cfg.values["max_astar_nodes"] = args.max_astar_nodes
     return cfg, proto

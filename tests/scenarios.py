@@ -113,14 +113,35 @@ def _uniform_f32(rng, a, b):
     return np.float32(c * np.float32(b - a)) + a
 
 
-def synthetic_ref(N, bins, K, seed, res=0.5, clear=8.0):
-    """SURVEY.md §8d's synthetic case drawn the way the survey's reference runs drew it:
-    std::mt19937(seed) and std::uniform_real_distribution<float>; per candidate box the centre
-    (x in [-0.8W, 0.2W], y in [-0.5W, 0.5W]) then the sides U(1, 6) m; a box whose centre lies
-    within 8 m of the start or the goal is redrawn.  With these draws the oracle reproduces the
-    pop counts the survey measured on the compiled reference (cfg3 seed 1: 3,297 pops; seed 3:
-    7,107 pops, 21,170 successors, 20,234 inner A* pops; SURVEY.md §8d, BASELINE.md), which
-    pins it at full size (tools/mt19937_synth.cpp is the same generator in C++)."""
+def _uniform_f32_vec(u, a, b):
+    """_uniform_f32 over an array of raw 32-bit draws (float32 arithmetic, op by op)."""
+    c = u.astype(np.float32) / np.float32(4294967296.0)
+    c = np.where(c >= np.float32(1), np.nextafter(np.float32(1), np.float32(0)), c).astype(np.float32)
+    return (c * np.float32(b - a)).astype(np.float32) + np.float32(a)
+
+
+def synthetic_ref_boxes(N, K, seed, res=0.5, clear=8.0):
+    """The box list of synthetic_ref, vectorised: numpy's RandomState(seed) is std::mt19937
+    with init_genrand seeding, and randint(0, 2^32) returns its raw 32-bit draws in order
+    (tests/test_oracle_golden.py checks it against the scalar MT19937 above)."""
+    f = np.float32
+    W = f(N) * f(res)
+    ax, bx = f(-0.8 * float(W)), f(0.2 * float(W))
+    ay, by = f(-0.5 * float(W)), f(0.5 * float(W))
+    stx = f(-0.6 * float(W))
+    rs = np.random.RandomState(seed & 0xffffffff)
+    out = np.zeros((0, 4), np.float32)
+    while len(out) < K:
+        u = rs.randint(0, 2 ** 32, size=(2 * K + 16, 4), dtype=np.uint64)
+        cx, cy = _uniform_f32_vec(u[:, 0], ax, bx), _uniform_f32_vec(u[:, 1], ay, by)
+        sx, sy = _uniform_f32_vec(u[:, 2], f(1), f(6)), _uniform_f32_vec(u[:, 3], f(1), f(6))
+        keep = ~((np.hypot((cx - stx).astype(np.float32), cy) < f(clear)) | (np.hypot(cx, cy) < f(clear)))
+        out = np.concatenate([out, np.stack([cx, cy, sx, sy], 1)[keep]])
+    return out[:K].astype(np.float32), float(stx)
+
+
+def synthetic_ref_boxes_scalar(N, K, seed, res=0.5, clear=8.0):
+    """The same boxes one draw at a time with the MT19937 class (the definition)."""
     f = np.float32
     W = f(N) * f(res)
     ax, bx = f(-0.8 * float(W)), f(0.2 * float(W))
@@ -134,10 +155,23 @@ def synthetic_ref(N, bins, K, seed, res=0.5, clear=8.0):
         if f(np.hypot(f(cx - stx), cy)) < f(clear) or f(np.hypot(cx, cy)) < f(clear):
             continue
         boxes.append([cx, cy, sx, sy])
+    return np.array(boxes, np.float32).reshape(-1, 4), float(stx)
+
+
+def synthetic_ref(N, bins, K, seed, res=0.5, clear=8.0):
+    """SURVEY.md §8d's synthetic case drawn the way the survey's reference runs drew it:
+    std::mt19937(seed) and std::uniform_real_distribution<float>; per candidate box the centre
+    (x in [-0.8W, 0.2W], y in [-0.5W, 0.5W]) then the sides U(1, 6) m; a box whose centre lies
+    within 8 m of the start or the goal is redrawn.  With these draws the oracle reproduces the
+    pop counts the survey measured on the compiled reference (cfg3 seed 1: 3,297 pops; seed 3:
+    7,107 pops, 21,170 successors, 20,234 inner A* pops; SURVEY.md §8d, BASELINE.md), which
+    pins it at full size (tools/mt19937_synth.cpp is the same generator in C++).  bench.py's
+    workloads use this generator (seed = query id + 1)."""
+    boxes, stx = synthetic_ref_boxes(N, K, seed, res, clear)
     cfg = PlannerConfig(grid_size=N, num_angle_bins=bins, steering=steering_from_degrees([-30, -15, 0, 15, 30]))
-    proto = dict(goal=[0.0, 0.0, 0.0], start=[float(stx), 0.0, 0.0], vel=2.0, cycles=5,
+    proto = dict(goal=[0.0, 0.0, 0.0], start=[stx, 0.0, 0.0], vel=2.0, cycles=5,
                  lines=np.zeros((0, 4), np.float32), line_conf=0.6, line_width=1.25,
-                 boxes=np.array(boxes, np.float32).reshape(-1, 4), box_conf=0.75, apf_r=2.5)
+                 boxes=boxes, box_conf=0.75, apf_r=2.5)
     return cfg, proto
 
 

@@ -2,10 +2,12 @@
 
 BASELINE.json configs[2..4]: cfg3 1024x1024x72 with K = 200 boxes, cfg4
 2048x2048x72 (plus its row-sharded map build), cfg5 the 1024^2 replan loop without reset.
-The query ids are bench.py's (seed = id + 1); the long ones come from the oracle's pop
-census (profiles/census_cfg*_r02.csv, tools/pop_census.py): cfg3 query 10226 (177,407 pops)
-and cfg4 query 3298 (590,557 pops), which outgrows the default 262,144-pop arena and must
-finish through a park + resume, as the reference (no limit, HybridAStar.cpp:107) does.
+The cfg3 query ids are bench.py's (seed = id + 1, the std::mt19937 generator
+tests/scenarios.py:synthetic_ref); the long ones come from the oracle's pop census
+(profiles/census_cfg3_mt19937_r02.csv, tools/pop_census.py): cfg3 query 2395 (172,207 pops).
+cfg4 query 1830 (650,107 pops, profiles/census_cfg4_mt19937_r02.csv) outgrows the default
+262,144-pop arena and must finish through a park + resume, as the reference (no limit,
+HybridAStar.cpp:107) does.
 
 The bar is the one of test_gpu_parity.py: bit-identical pops, successors, A* pops, shots,
 ordered pop digest, closed-set digest, path, curvature and cost.
@@ -95,9 +97,12 @@ def test_statuses_reported_per_planner(gpu, oracle_lib, monkeypatch):
 # ------------------------------------------------------------------ cfg3 (1024^2) ------
 def test_cfg3_parity_batch(gpu, oracle_lib):
     """BASELINE configs[2]: 1024x1024x72, K = 200, bench query ids 0, 1, 2 and the longest
-    query of the bench batch (10226, 177,407 pops), searched in one batched launch."""
-    qs = [0, 1, 2, 10226]
-    cases = [synthetic(1024, 72, 200, seed=q + 1) for q in qs]
+    query of the bench batch (2395, 172,207 pops), searched in one batched launch, plus round 1's
+    longest PCG64 query (10226, 177,407 pops)."""
+    from tests.scenarios import synthetic_ref
+    qs = [0, 1, 2, 2395, "pcg64:10226"]
+    cases = [synthetic_ref(1024, 72, 200, seed=q + 1) if isinstance(q, int) else
+             synthetic(1024, 72, 200, seed=int(q.split(":")[1]) + 1) for q in qs]
     gs, os_ = [], []
     for cfg, proto in cases:
         g, o = _pair(gpu, oracle_lib, cfg, proto)
@@ -136,12 +141,14 @@ def test_cfg3_survey_reference_cases(gpu, oracle_lib):
 
 
 # ------------------------------------------------------------------ cfg4 (2048^2) ------
-@pytest.mark.parametrize("q", [0, 3, 3298])
+@pytest.mark.parametrize("q", [0, 3, 1830])
 def test_cfg4_parity(gpu, oracle_lib, q):
-    """BASELINE configs[3] at its own size: 2048x2048x72, K = 200.  Query 3298 needs 590,557
-    pops (census): it parks at the default arena's 262,144 and resumes, and must end with
-    the oracle's success, cost and path (round 1 reported it as an overflow failure)."""
-    cfg, proto = synthetic(2048, 72, 200, seed=q + 1)
+    """BASELINE configs[3] at its own size: 2048x2048x72, K = 200, bench query ids (std::mt19937
+    inputs).  Query 1830 is the longest of the bench batch (650,107 pops,
+    profiles/census_cfg4_mt19937_r02.csv): it parks at the default arena's 262,144 and resumes,
+    and must end with the oracle's success, cost and path (round 1 cut such queries off)."""
+    from tests.scenarios import synthetic_ref
+    cfg, proto = synthetic_ref(2048, 72, 200, seed=q + 1)
     g, o = _pair(gpu, oracle_lib, cfg, proto)
     assert_bits_equal(g.get_obstacles(), o.get_obstacles(), f"cfg4 query {q} map")
     rg = g.find_path(proto["vel"], proto["start"], cap=16384)

@@ -78,3 +78,21 @@ def test_oracle_matches_survey_reference_counts(oracle_lib):
         for k in ("pops", "successors", "astar_pops"):
             if k in case:
                 assert r["stats"][k] == case[k], f"seed {case['seed']}: {k} {r['stats'][k]} vs reference {case[k]}"
+
+
+def test_reference_generator_definitions_agree(tmp_path):
+    """synthetic_ref's vectorised draw == the scalar std::mt19937 restatement == the C++
+    generator compiled with libstdc++ (tools/mt19937_synth.cpp, variant 3), bit for bit."""
+    import subprocess
+    from pathlib import Path
+    from tests.scenarios import synthetic_ref_boxes, synthetic_ref_boxes_scalar
+    root = Path(__file__).resolve().parents[1]
+    exe = tmp_path / "mt19937_synth"
+    subprocess.run(["g++", "-O2", "-std=c++17", str(root / "tools" / "mt19937_synth.cpp"), "-o", str(exe)], check=True)
+    for seed in (1, 3, 10227):
+        a, _ = synthetic_ref_boxes(1024, 200, seed)
+        b, _ = synthetic_ref_boxes_scalar(1024, 200, seed)
+        c = np.array(json.loads(subprocess.run([str(exe), "1024", "200", str(seed), "3"], capture_output=True,
+                                               text=True, check=True).stdout), np.float32).reshape(-1, 4)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        assert np.array_equal(a.view(np.uint32), c.view(np.uint32))

@@ -23,9 +23,10 @@ ARGS = None
 
 def one(q):
     from oracle import pyoracle
-    from tests.scenarios import drive, synthetic
+    from tests.scenarios import drive, synthetic, synthetic_ref
     pyoracle.set_max_pops(ARGS.max_pops)
-    cfg, proto = synthetic(ARGS.grid, ARGS.bins, ARGS.obstacles, seed=q + 1)
+    gen = synthetic_ref if ARGS.generator == "mt19937" else synthetic
+    cfg, proto = gen(ARGS.grid, ARGS.bins, ARGS.obstacles, seed=q + 1)
     o = pyoracle.OraclePlanner(cfg)
     drive(o, proto)
     t0 = time.perf_counter()
@@ -51,6 +52,7 @@ def main():
     ap.add_argument("--count", type=int, default=64)
     ap.add_argument("--max-pops", type=int, default=0)
     ap.add_argument("--procs", type=int, default=max(1, (os.cpu_count() or 2) - 2))
+    ap.add_argument("--generator", choices=("mt19937", "pcg64"), default="mt19937")
     a = ap.parse_args()
     with Pool(a.procs, initializer=init, initargs=(a,)) as pool:
         for rec in pool.imap_unordered(one, range(a.start, a.start + a.count), chunksize=4):
