@@ -120,13 +120,13 @@ def test_cfg3_parity_batch(gpu, oracle_lib):
 
 
 def test_cfg3_survey_reference_cases(gpu, oracle_lib):
-    """The survey's own cfg3 cases (std::mt19937 seeds 1 and 3, tests/scenarios.py:synthetic_ref):
-    GPU == oracle bit for bit, and both equal the counts the survey measured on the compiled
-    reference (tests/golden/survey_reference_counts.json)."""
+    """The survey's own cases, 256² to 2048² including cfg3 seeds 1 and 3 (std::mt19937 inputs,
+    tests/scenarios.py:synthetic_ref): GPU == oracle bit for bit, and both equal the counts the
+    survey measured on the compiled reference (tests/golden/survey_reference_counts.json)."""
     import json
     from tests.scenarios import GOLDEN, synthetic_ref
     g = json.loads((GOLDEN / "survey_reference_counts.json").read_text())
-    cases = [synthetic_ref(g["grid"], g["angle_bins"], g["obstacles"], c["seed"]) for c in g["cases"]]
+    cases = [synthetic_ref(c["grid"], c["angle_bins"], c["obstacles"], c["seed"]) for c in g["cases"]]
     gs, os_ = [], []
     for cfg, proto in cases:
         gp, op = _pair(gpu, oracle_lib, cfg, proto)
@@ -134,10 +134,10 @@ def test_cfg3_survey_reference_cases(gpu, oracle_lib):
         os_.append(op)
     res, _ = gpu.find_path_batch(gs, [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases], cap=8192)
     for ref, r, o, (cfg, proto) in zip(g["cases"], res, os_, cases):
-        compare_results(r, o.find_path(proto["vel"], proto["start"]), f"survey seed {ref['seed']}")
+        compare_results(r, o.find_path(proto["vel"], proto["start"]), f"survey case {ref}")
         for k in ("pops", "successors", "astar_pops"):
             if k in ref:
-                assert r["stats"][k] == ref[k], f"seed {ref['seed']}: {k} {r['stats'][k]} vs reference {ref[k]}"
+                assert r["stats"][k] == ref[k], f"{ref}: {k} {r['stats'][k]} vs reference {ref[k]}"
 
 
 # ------------------------------------------------------------------ cfg4 (2048^2) ------

@@ -63,13 +63,13 @@ def test_equal_f_insert_is_dropped(oracle_lib):
 
 
 def test_oracle_matches_survey_reference_counts(oracle_lib):
-    """The oracle at full cfg3 size against counts the survey measured on the compiled
-    reference (tests/golden/survey_reference_counts.json): the same std::mt19937 inputs
-    (tests/scenarios.py:synthetic_ref) give the same pops, successors and inner A* pops."""
+    """The oracle against counts the survey measured on the compiled reference at 256² to 2048²,
+    including full cfg3 size (tests/golden/survey_reference_counts.json): the same std::mt19937
+    inputs (tests/scenarios.py:synthetic_ref) give the same pops, successors and inner A* pops."""
     from tests.scenarios import synthetic_ref
     g = json.loads((GOLDEN / "survey_reference_counts.json").read_text())
     for case in g["cases"]:
-        cfg, proto = synthetic_ref(g["grid"], g["angle_bins"], g["obstacles"], case["seed"])
+        cfg, proto = synthetic_ref(case["grid"], case["angle_bins"], case["obstacles"], case["seed"])
         o = oracle_lib.OraclePlanner(cfg)
         drive(o, proto)
         r = o.find_path(proto["vel"], proto["start"])
@@ -77,7 +77,7 @@ def test_oracle_matches_survey_reference_counts(oracle_lib):
         assert r["ok"]
         for k in ("pops", "successors", "astar_pops"):
             if k in case:
-                assert r["stats"][k] == case[k], f"seed {case['seed']}: {k} {r['stats'][k]} vs reference {case[k]}"
+                assert r["stats"][k] == case[k], f"{case}: {k} {r['stats'][k]} vs reference {case[k]}"
 
 
 def test_reference_generator_definitions_agree(tmp_path):
