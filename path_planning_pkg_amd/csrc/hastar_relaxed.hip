@@ -687,12 +687,16 @@ hipError_t launch_relaxed(const PlannerDev* d_descs, int n, const RelaxArena* d_
                           const RelaxParams& rp, RelaxField* d_fields, hipStream_t st) {
   hipError_t e = hipMemsetAsync(d_next, 0, sizeof(int), st);
   if (e != hipSuccess) return e;
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void*>(k_relaxed_search),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)RELAX_DYN_LDS);
+  // the dynamic-LDS opt-in, once per device (callers hold the device context's lock)
+  static bool attr[64] = {};
+  int dev = 0;
+  hipError_t a = hipGetDevice(&dev);
+  if (a != hipSuccess) return a;
+  if (!attr[dev & 63]) {
+    a = hipFuncSetAttribute(reinterpret_cast<const void*>(k_relaxed_search), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)RELAX_DYN_LDS);
     if (a != hipSuccess) return a;
-    attr = true;
+    attr[dev & 63] = true;
   }
   hipLaunchKernelGGL(k_relaxed_search, dim3(n_arenas), dim3(RW * 64), RELAX_DYN_LDS, st, d_descs, n, d_arenas, d_next,
                      rp, d_fields);
