@@ -49,6 +49,7 @@ long long g_max_pops = 0;
 #ifdef ORC_SHAPE_STATS
 long long g_shape[16];
 bool g_search_unsafe;       // the current inner search met a shape-dependent find/insert
+int g_migrated;             // bit k: the current inner search's open set has exceeded kCaps[k]
 long long g_search_pops;    // pops of the current inner search
 long long g_pops_to_unsafe; // pops before its first shape-dependent event
 #endif
@@ -558,11 +559,20 @@ template <class T> struct Planner {
     }
     g_search_unsafe = false;
     g_search_pops = 0;
+    g_migrated = 0;
   }
   void shape_size(size_t n) {
     if ((long long)n > g_shape[4]) g_shape[4] = (long long)n;
     g_shape[5] += n > 256;
     g_shape[6] += n > 1024;
+    // [13..15]: pops of inner searches after their open set first exceeded 703 / 767 / 1023
+    // nodes (the LDS pool sizes of the kernel, minus the header): the pops an LDS pool of that
+    // size would run in HBM mode (migration is one-way)
+    static const size_t kCaps[3] = {703, 767, 1023};
+    for (int k = 0; k < 3; ++k) {
+      if (n > kCaps[k]) g_migrated |= 1 << k;
+      if (g_migrated & (1 << k)) g_shape[13 + k]++;
+    }
   }
 #endif
   // ----------------------------------------------------- holonomic heuristic (AStar)

@@ -25,9 +25,10 @@ po.LIB = Path(so)
 from tests.scenarios import drive, synthetic  # noqa: E402
 
 seeds = [int(a) for a in sys.argv[1:]] or list(range(1, 9))
+from tests.scenarios import synthetic_ref  # noqa: E402
 L = C.CDLL(so)
 for s in seeds:
-    cfg, proto = synthetic(1024, 72, 200, s)
+    cfg, proto = synthetic_ref(1024, 72, 200, s)
     o = po.OraclePlanner(cfg)
     drive(o, proto)
     st = (C.c_longlong * 16)()
@@ -36,6 +37,7 @@ for s in seeds:
     L.orc_shape_stats(st)
     names = ["probes", "same_cell_present", "unsafe_find", "unsafe_insert", "max_open", "pops_open_gt256",
              "pops_open_gt1024", "order_violations", "searches", "searches_shape_dependent", "pops_all",
-             "pops_in_shape_dependent_searches", "pops_before_first_event"]
+             "pops_in_shape_dependent_searches", "pops_before_first_event", "hbm_pops_cap703",
+             "hbm_pops_cap767", "hbm_pops_cap1023"]
     print(json.dumps(dict(seed=s, apops=r["stats"]["astar_pops"], **{n: st[q] for q, n in enumerate(names)})))
     o.close()
