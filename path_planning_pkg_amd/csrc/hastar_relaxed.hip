@@ -304,8 +304,7 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
   if (__float_as_uint(cg) > table_best(A, key)) return;  // a cheaper node of this key was generated since
   const int cci = ufi((int)(cur.cc >> 8));
   const int cx = key3_x(key), cy = key3_y(key), cbin = key3_bin(key);
-  int pop_no = 0;
-  if (lane == 0) pop_no = atomicAdd(&S.pops, 1) + 1;
+  if (lane == 0) atomicAdd(&S.pops, 1);
   // goal test (Node3D::operator==: the cell only, Node3D.h:42)
   if (cx == P.goal_cx && cy == P.goal_cy) {
     if (lane == 0) atomicMin(&S.best, ((unsigned long long)__float_as_uint(cg) << 32) | (unsigned)idx);
@@ -319,7 +318,6 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
     const int k = atomicAdd(&S.since_shot, 1) + 1;
     if (k >= S.interval && atomicExch(&S.since_shot, 0) >= S.interval) shoot = 1;
   }
-  (void)pop_no;
   if (ufi(shoot)) {
     if (lane == 0) {
       atomicAdd(&S.shots, 1);
