@@ -1,5 +1,5 @@
 """CPU-side checks of the drop-in boundary: the C-ABI library loads, exports every
-symbol include/hastar.h and include/hastar_test.h declare, and refuses to run without a
+symbol include/hastar.h, include/hastar_units.h and include/hastar_test.h declare, and refuses to run without a
 GPU (no CPU fallback).  Also the libstdc++ red-black-tree replica used by the search
 kernel vs std::set (tools/rbtree_check.cpp)."""
 import ctypes as C
@@ -14,7 +14,7 @@ ROOT = Path(__file__).resolve().parents[1]
 
 def declared_symbols():
     names = []
-    for hdr in ("hastar.h", "hastar_test.h"):
+    for hdr in ("hastar.h", "hastar_test.h", "hastar_units.h"):
         text = (ROOT / "include" / hdr).read_text()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         names += re.findall(r"\b(hastar_[a-z0-9_]+)\s*\(", text)
