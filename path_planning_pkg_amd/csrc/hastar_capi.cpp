@@ -1758,7 +1758,7 @@ size_t relax_bytes(int N, int nodes, RelaxArena* A, char* q) {
   };
   char* dist = take(NN * 4);
   char* bucket = take((size_t)8 * bcap * sizeof(BucketEntry));
-  char* table = take((size_t)slots * sizeof(Slot3));
+  char* table = take((size_t)slots * sizeof(RelaxSlot));
   char* nodes_p = take((size_t)nodes * sizeof(Node3));
   char* lists = take((size_t)3 * nodes * 8);
   char* dxyh = take((size_t)relaxed_waves() * dub_cap * 12);
@@ -1769,7 +1769,7 @@ size_t relax_bytes(int N, int nodes, RelaxArena* A, char* q) {
     A->dist = reinterpret_cast<float*>(dist);
     A->bucket = reinterpret_cast<BucketEntry*>(bucket);
     A->bcap = bcap;
-    A->table = reinterpret_cast<Slot3*>(table);
+    A->table = reinterpret_cast<RelaxSlot*>(table);
     A->tmask = slots - 1;
     A->nodes = reinterpret_cast<Node3*>(nodes_p);
     A->node_cap = nodes;
@@ -1783,6 +1783,20 @@ size_t relax_bytes(int N, int nodes, RelaxArena* A, char* q) {
     A->cells = NN;
   }
   return off;
+}
+// debug: per-wave progress words of the relaxed kernel in pinned host memory, readable while
+// a launch runs (HASTAR_RELAXED_PROGRESS set; hastar_debug_relaxed_progress)
+unsigned* relaxed_progress() {
+  static unsigned* words = nullptr;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    if (std::getenv("HASTAR_RELAXED_PROGRESS") &&
+        hipHostMalloc(reinterpret_cast<void**>(&words), 4096 * 64 * sizeof(unsigned), hipHostMallocCoherent) != hipSuccess)
+      words = nullptr;
+    if (words) std::memset(words, 0, 4096 * 64 * sizeof(unsigned));
+  }
+  return words;
 }
 int relax_acquire(DeviceCtx& D, int N, int nodes, int want) {
   if (D.n_rarenas >= want && D.r_N >= N && D.r_nodes >= nodes) return 0;
@@ -1806,7 +1820,7 @@ int relax_acquire(DeviceCtx& D, int N, int nodes, int want) {
   for (int i = 0; i < n; ++i) {
     relax_bytes(N, nodes, &host[i], static_cast<char*>(D.rslab) + per * (size_t)i);
     // the best-g tables start empty; every search leaves its table empty again
-    HIPCHK(hipMemsetAsync(host[i].table, 0xff, ((size_t)host[i].tmask + 1) * sizeof(Slot3), D.stream));
+    HIPCHK(hipMemsetAsync(host[i].table, 0xff, ((size_t)host[i].tmask + 1) * sizeof(RelaxSlot), D.stream));
   }
   HIPCHK(dalloc(&D.d_rarenas, (size_t)n));
   HIPCHK(hipMemcpyAsync(D.d_rarenas, host.data(), (size_t)n * sizeof(RelaxArena), hipMemcpyHostToDevice, D.stream));
@@ -1877,6 +1891,7 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
     }
     HIPCHK(hipMemcpyAsync(DC.d_rfields, fields.data(), (size_t)n * sizeof(RelaxField), hipMemcpyHostToDevice, st));
   }
+  rp.progress = relaxed_progress();
   HIPCHK(hipEventRecord(DC.ev0, st));
   HIPCHK(launch_relaxed(DC.d_descs, n, DC.d_rarenas, std::min(want, DC.n_rarenas), DC.d_next, rp,
                         reuse ? DC.d_rfields : nullptr, st));
@@ -1897,6 +1912,8 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
 }
 
 extern "C" {
+
+const unsigned* hastar_debug_relaxed_progress(void) { return relaxed_progress(); }
 
 int hastar_copy_path(hastar_handle h, float* xyh, float* curv, int cap, int* len) {
   if (!h || !h->have_last) return fail(HASTAR_EINVAL, "no search result");

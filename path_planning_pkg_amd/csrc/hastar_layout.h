@@ -222,17 +222,27 @@ struct SlotArena {
 //           updated with atomicMin (non-negative floats order like their bit patterns); used
 //           when the planner keeps no field of its own (RelaxField)
 //   bucket  8 x bcap {cell, distance bits} entries (a ring of Dial buckets of width act_cost_axis)
-//   table   best g per node key (open addressing; key 0xffffffff = empty; left empty by every search)
-//   nodes   every node ever generated (Node3 records; prev = parent node, l = its table slot)
+//   table   best {g, tie} per node key (open addressing; key 0xffffffff = empty; left empty by
+//           every search)
+//   nodes   every node ever generated (Node3 records; prev = parent node, l = its table slot,
+//           r = its tie)
 //   lists   3 x list_cap lists of {f bits, node} (8 B): the open list, the next open list
-//           and the round's expansion set (node indices only)
-//   dub_*   one Dubins-shot scratch of dub_cap samples per wave
+//           (the round's raw successors first) and the round's expansion set (node indices)
+//   dub_*   one Dubins-shot scratch of dub_cap samples per shot of a round
 //   chain   path reconstruction scratch
 struct BucketEntry { uint32_t cell, d; };  // a Dial-bucket entry: cell (i << 16 | j) and its distance bits
+// best-g table slot of the relaxed search: best = g bits << 32 | tie, where tie hashes the
+// (parent key, action) that generated the node, so equal-g offers resolve by value, not by
+// which wavefront got there first
+struct alignas(16) RelaxSlot {
+  uint32_t key;
+  uint32_t pad;
+  unsigned long long best;
+};
 struct RelaxArena {
   float* dist;
   BucketEntry* bucket;    int bcap;       int pad0;
-  Slot3* table;     uint32_t tmask; int pad1;
+  RelaxSlot* table; uint32_t tmask; int pad1;
   Node3* nodes;     int node_cap;   int pad2;
   int* lists;       int list_cap;   int pad3;
   float* dub_xyh;   float* dub_curv; int dub_cap; int pad4;
@@ -254,6 +264,8 @@ struct RelaxParams {
   float h_stop;     // the Dijkstra covers the ellipse d(c) + |c - start| <= h_stop x |goal - start| + 64 moves
   int max_rounds;
   float h_weight;   // f = g + h_weight x max(h, Dubins length) (1: the reference's f)
+  int pad;
+  unsigned* progress;  // debug (HASTAR_RELAXED_PROGRESS): per-wave phase words in host memory, or null
 };
 
 }  // namespace hastar

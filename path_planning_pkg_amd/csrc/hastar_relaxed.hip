@@ -62,7 +62,16 @@ __device__ __forceinline__ bool bucket_put(const RelaxArena& A, BucketEntry* lds
 #define RSTAMP_BEGIN() (void)0
 #define RSTAMP(k) (void)0
 #endif
+constexpr unsigned long long RELAX_WATCHDOG = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
 constexpr uint32_t EMPTY_KEY = 0xffffffffu;  // no node key has all bits set (x < 4096, bin < 256 with y < 4096)
+
+// debug progress words (RelaxParams::progress): workgroup b, wave w -> words [(b * RW + w) * 4, +4)
+#define RPROG(k, v)                                                                                   \
+  do {                                                                                                \
+    if (rp.progress && lane == 0)                                                                     \
+      __hip_atomic_store(rp.progress + ((size_t)blockIdx.x * RW + wv) * 4 + (k), (unsigned)(v),         \
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);                                  \
+  } while (0)
 
 // L1-bypassing loads of words other waves update with atomics
 __device__ __forceinline__ uint32_t ld_sync(const uint32_t* p) {
@@ -84,35 +93,46 @@ __device__ __forceinline__ uint32_t rx_hash(uint32_t k) {
   k *= 0x846ca68bU;
   return k ^ (k >> 16);
 }
-// best-g table: lower the key's g to gbits; true when gbits is the new best (*slot: the key's
-// slot, kept in the node so the search can clear exactly the slots it used).  *full is set
-// when the table has no room left.
-__device__ __forceinline__ bool table_lower(const RelaxArena& A, uint32_t key, uint32_t gbits, bool* full,
+// best-g table: lower the key's best to v = g bits << 32 | tie; true when v is the new best
+// (*slot: the key's slot, kept in the node so the search can clear exactly the slots it used).
+// *full is set when the table has no room left.
+__device__ __forceinline__ bool table_lower(const RelaxArena& A, uint32_t key, unsigned long long v, bool* full,
                                             uint32_t* slot) {
   uint32_t h = rx_hash(key) & A.tmask;
   for (uint32_t probe = 0; probe <= A.tmask; ++probe) {
-    Slot3* s = &A.table[h];
+    RelaxSlot* s = &A.table[h];
     uint32_t k = ld_sync(&s->key);
     if (k == EMPTY_KEY) {
       const uint32_t prev = atomicCAS(&s->key, EMPTY_KEY, key);
       k = prev == EMPTY_KEY ? key : prev;
     }
     *slot = h;
-    if (k == key) return atomicMin(&s->gi, gbits) > gbits;
+    if (k == key) return atomicMin(&s->best, v) > v;
     h = (h + 1) & A.tmask;
   }
   *full = true;
   return false;
 }
-__device__ __forceinline__ uint32_t table_best(const RelaxArena& A, uint32_t key) {
-  uint32_t h = rx_hash(key) & A.tmask;
-  for (uint32_t probe = 0; probe <= A.tmask; ++probe) {
-    const uint32_t k = ld_sync(&A.table[h].key);
-    if (k == key) return ld_sync(&A.table[h].gi);
-    if (k == EMPTY_KEY) break;
-    h = (h + 1) & A.tmask;
+// A node is current iff it still holds its key's best {g, tie}.  Only asked between rounds,
+// when the table is final for the round, so the answer does not depend on wavefront timing.
+__device__ __forceinline__ bool node_current(const RelaxArena& A, int idx, float* vmin) {
+  const int4 q0 = *reinterpret_cast<const int4*>(&A.nodes[idx]);      // key, f, l, r
+  const float4 q1 = *(reinterpret_cast<const float4*>(&A.nodes[idx]) + 1);  // p, cc, g, vmin
+  if (vmin) *vmin = q1.w;
+  const unsigned long long mine = ((unsigned long long)__float_as_uint(q1.z) << 32) | (uint32_t)q0.w;
+  return __hip_atomic_load(&A.table[(uint32_t)q0.z].best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == mine;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long w = ((unsigned long long)(uint32_t)__shfl_xor((int)(v >> 32), o, 64) << 32) |
+                                 (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
+    v = w < v ? w : v;
   }
-  return 0xffffffffu;
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
 }
 
 struct RelaxShared {
@@ -122,12 +142,14 @@ struct RelaxShared {
   int overflow, hover;
   int settled;              // cells settled (diagnostic: astar_pops)
   int buckets;              // Dijkstra buckets processed
-  int nA, nB, nE, eNext, nodes;
+  int nA, nB, nE, nN, eNext, nodes, nE_last, n_allowed;
   uint32_t fmin, fnext;     // float bits of the open list's min f, and of the next open list's
-  unsigned long long best;  // cheapest solution candidate: f bits << 32 | tag
+  unsigned long long best;  // cheapest solution candidate: cost bits << 32 | tag
   int since_shot, interval;
   int pops, succ, shots, rounds;
-  int shot_term[RW], shot_n[RW], shot_done[RW];
+  int n_sel;                     // shots of this round
+  unsigned long long sel[RW];    // their shooters: f bits << 32 | tie, lowest first
+  int shot_term[RW], shot_n[RW];
   unsigned long long stamp[6];
 };
 
@@ -294,55 +316,63 @@ __device__ __forceinline__ float relaxed_h(const PlannerDev& P, const float* dis
 }
 
 // One expansion by one wavefront: the exact kernel's fused successor block without the
-// closed set and the lazy A* (the heuristic is the Dijkstra field).
+// closed set and the lazy A* (the heuristic is the Dijkstra field).  Every decision is keyed by
+// values (g, f and the node's tie), never by the order in which the round's wavefronts run, so
+// a query gives the same path on every run.
 __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, ApfStage& apfs,
                                const GoalC& GC, const float* dist, float hlim, int hs_x, int hs_y, float hw, int idx,
-                               int wv, int lane, uint2* list_b) {
+                               int lane, uint2* list_n) {
   const Node3 cur = gload(&A.nodes[idx]);
-  const uint32_t key = ufu(cur.key);
-  const float cg = uff(cur.g), cxp = uff(cur.x), cyp = uff(cur.y), chd = uff(cur.h), cvm = uff(cur.vmin);
-  if (__float_as_uint(cg) > table_best(A, key)) return;  // a cheaper node of this key was generated since
+  const uint32_t key = ufu(cur.key), tie = ufu((uint32_t)cur.r);
+  const float cg = uff(cur.g), cf = uff(cur.f), cxp = uff(cur.x), cyp = uff(cur.y), chd = uff(cur.h),
+              cvm = uff(cur.vmin);
   const int cci = ufi((int)(cur.cc >> 8));
   const int cx = key3_x(key), cy = key3_y(key), cbin = key3_bin(key);
   if (lane == 0) atomicAdd(&S.pops, 1);
-  // goal test (Node3D::operator==: the cell only, Node3D.h:42)
+  // goal test (Node3D::operator==: the cell only, Node3D.h:42).  The stages below run under
+  // wave-uniform flags (no early return out of divergent code).
+  int done = 0;
   if (cx == P.goal_cx && cy == P.goal_cy) {
-    if (lane == 0) atomicMin(&S.best, ((unsigned long long)__float_as_uint(cg) << 32) | (unsigned)idx);
-    return;
+    if (lane == 0) atomicMin(&S.best, ((unsigned long long)__float_as_uint(cg) << 32) | (tie & 0x7fffffffu));
+    done = 1;
   }
-  // Dubins shot (HybridAStar.cpp:115-154): the reference's interval/decay schedule over the
-  // workgroup's expansions; a wave that found a free shot keeps its samples and shoots no more
+  // Dubins shot (HybridAStar.cpp:115-154): the round's shooters were chosen between rounds
+  // (the reference's interval / decay schedule over the expansions, lowest f first)
   const bool allowed = cvm < 1.0f;
-  int shoot = 0;
-  if (lane == 0 && allowed && !S.shot_done[wv]) {
-    const int k = atomicAdd(&S.since_shot, 1) + 1;
-    if (k >= S.interval && atomicExch(&S.since_shot, 0) >= S.interval) shoot = 1;
+  int shot = -1;
+  if (!done && allowed) {
+    const unsigned long long v = ((unsigned long long)__float_as_uint(cf) << 32) | tie;
+    for (int q = 0; q < S.n_sel; ++q)
+      if (S.sel[q] == v) shot = q;
   }
-  if (ufi(shoot)) {
-    if (lane == 0) {
-      atomicAdd(&S.shots, 1);
-      S.interval = max(S.interval - P.shot_decay, 50);
-    }
+  shot = ufi(shot);
+  if (shot >= 0) {
+    if (lane == 0) atomicAdd(&S.shots, 1);
     int word = 0;
     float prm[4];
     const float r = P.r_min;
     const float L = dubins_shortest(r, cxp, cyp, chd, P.goal_x, P.goal_y, P.goal_h, &word, prm);
     const Centres C = dubins_centres(r, cxp, cyp, chd, P.goal_x, P.goal_y, P.goal_h);
-    GAS float* xyh = gp(A.dub_xyh) + (size_t)wv * A.dub_cap * 3;
-    GAS float* curv = gp(A.dub_curv) + (size_t)wv * A.dub_cap;
-    const int n = dubins_sample(P, C, word, prm, xyh, curv, A.dub_cap, lane);
+    GAS float* xyh = gp(A.dub_xyh) + (size_t)shot * A.dub_cap * 3;
+    GAS float* curv = gp(A.dub_curv) + (size_t)shot * A.dub_cap;
+    const int n = ufi(dubins_sample(P, C, word, prm, xyh, curv, A.dub_cap, lane));
     wave_lds_sync();
-    const bool first_arc_long = fabsf(prm[1]) > (float)M_PI_2;
-    if (n > 0 && !first_arc_long && path_is_free(P, xyh, n, lane)) {
+    const int first_arc_long = ufi(fabsf(prm[1]) > (float)M_PI_2 ? 1 : 0);
+    int free_shot = 0;
+    if (n > 0 && !first_arc_long) free_shot = path_is_free(P, xyh, n, lane) ? 1 : 0;
+    free_shot = ufi(free_shot);
+    if (free_shot) {
+      const int term = ufi(cur.prev);
       if (lane == 0) {
-        S.shot_done[wv] = 1;
-        S.shot_term[wv] = ufi(cur.prev);
-        S.shot_n[wv] = n;
-        atomicMin(&S.best, ((unsigned long long)__float_as_uint(cg + L) << 32) | 0x80000000u | (unsigned)wv);
+        S.shot_term[shot] = term;
+        S.shot_n[shot] = n;
+        atomicMin(&S.best, ((unsigned long long)__float_as_uint(cg + L) << 32) | 0x80000000u | (unsigned)shot);
       }
-      return;
+      done = 1;
     }
   }
+  done = ufi(done);
+  if (done) return;
   // successors (VehicleModel.cpp:63-105) in groups of gs lanes, as in the exact kernel
   const int span = 2 * P.na + 1;
   const int gsh = span <= 4 ? 4 : 2, gs = 1 << gsh;
@@ -391,17 +421,19 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
     const float g = sg + fc;  // Grid3D.cpp:66-69
     const float f = g + hw * stl_max(h2, dub);
     const uint32_t skey = key3(scx, scy, sbin);
+    // equal-g offers for one key resolve by this tie, a hash of (parent key, action)
+    const uint32_t stie = rx_hash(key * 0x9e3779b1u + (uint32_t)ai);
     bool full = false;
     uint32_t tslot = 0;
-    if (table_lower(A, skey, __float_as_uint(g), &full, &tslot)) {
+    if (table_lower(A, skey, ((unsigned long long)__float_as_uint(g) << 32) | stie, &full, &tslot)) {
       const int n = atomicAdd(&S.nodes, 1);
-      const int pos = atomicAdd(&S.nB, 1);
+      const int pos = atomicAdd(&S.nN, 1);
       if (n < A.node_cap && pos < A.list_cap) {
         Node3 d;
         d.key = skey;
         d.f = f;
         d.l = (int)tslot;
-        d.r = NIL;
+        d.r = (int)stie;
         d.p = NIL;
         d.cc = (uint32_t)(lo + ca) << 8;
         d.g = g;
@@ -411,8 +443,7 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
         d.h = sh;
         d.prev = idx;
         gstore(&A.nodes[n], d);
-        list_b[pos] = make_uint2(__float_as_uint(f), (uint32_t)n);
-        atomicMin(&S.fnext, __float_as_uint(f));
+        list_n[pos] = make_uint2(__float_as_uint(f), (uint32_t)n);
       } else {
         S.overflow = 1;
       }
@@ -425,6 +456,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
                             RelaxField* F, BucketEntry* bl) {
   const int tid = threadIdx.x, NT = blockDim.x, wv = tid >> 6, lane = tid & 63;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  RPROG(0, 1);
   // the heuristic field: the planner's own (kept across calls until reset / update_goal, like
   // the reference's A* memo) or the arena's scratch
   float* dist = (F && F->dist) ? F->dist : A.dist;
@@ -448,6 +480,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
     }
   }
   const unsigned long long t_heur = __builtin_amdgcn_s_memrealtime();
+  RPROG(0, 2);
   // ---- the frontier-parallel search
   apf_stage(P, S.apf[wv], lane);
   const GoalC GC = goal_centres(P.r_min, P.goal_x, P.goal_y, P.goal_h);
@@ -457,7 +490,8 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
     const float h0 = relaxed_h(P, dist, (size_t)P.start_cx * P.N + P.start_cy, P.start_cx, P.start_cy, hlim, hs_x,
                                hs_y);
     s0.f = h0;
-    s0.l = s0.r = s0.p = NIL;
+    s0.l = s0.p = NIL;
+    s0.r = 0;
     s0.cc = (uint32_t)P.start_ci << 8;
     s0.g = 0.0f;
     s0.vmin = P.start_vmin;
@@ -468,12 +502,16 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
     gstore(&A.nodes[0], s0);
     bool full = false;
     uint32_t tslot = 0;
-    table_lower(A, s0.key, 0u, &full, &tslot);
-    A.nodes[0].l = (int)tslot;
+    table_lower(A, s0.key, 0ull, &full, &tslot);
+    A.nodes[0].l = (int)tslot;  // tie 0: s0.r
     reinterpret_cast<uint2*>(A.lists)[0] = make_uint2(__float_as_uint(s0.f), 0u);
     S.nA = 1;
     S.nB = 0;
     S.nE = 0;
+    S.nN = 0;
+    S.nE_last = 0;
+    S.n_allowed = 0;
+    S.n_sel = 0;
     S.eNext = 0;
     S.nodes = 1;
     S.best = ~0ull;
@@ -486,18 +524,22 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
     S.overflow = 0;
   }
   if (lane == 0) {
-    S.shot_done[wv] = 0;
     S.shot_n[wv] = 0;
     S.shot_term[wv] = NIL;
   }
   block_sync();
-  int a = 0;  // lists[a]: open list, lists[(a + 1) % 3]: next open list, lists[(a + 2) % 3]: expansion set
+  // lists L[a]: the open list; L[a ^ 1]: the next open list; LE: the round's expansion set.
+  // A round: split the open list (f <= min f + delta and still current -> LE, f above -> next),
+  // choose the round's shooters, expand LE (raw successors -> the free L[a]), then keep the
+  // successors still current at the round's end.  Every choice is made between rounds from
+  // values, so the rounds — and the path — do not depend on wavefront timing.
+  uint2* const L0 = reinterpret_cast<uint2*>(A.lists);
+  int* const LE = reinterpret_cast<int*>(L0 + (size_t)2 * A.list_cap);
+  int a = 0;
   int status = 0;
   for (int round = 0;; ++round) {
-    // open-list entries are {f bits, node}: the split streams 8-B entries, not node records
-    uint2* LA = reinterpret_cast<uint2*>(A.lists) + (size_t)a * A.list_cap;
-    uint2* LB = reinterpret_cast<uint2*>(A.lists) + (size_t)((a + 1) % 3) * A.list_cap;
-    int* LE = reinterpret_cast<int*>(reinterpret_cast<uint2*>(A.lists) + (size_t)((a + 2) % 3) * A.list_cap);
+    uint2* LA = L0 + (size_t)a * A.list_cap;
+    uint2* LB = L0 + (size_t)(a ^ 1) * A.list_cap;
     const int nA = S.nA;
     const float thr = __uint_as_float(S.fmin) + rp.delta;
     if (nA == 0 || S.best != ~0ull) break;
@@ -505,42 +547,110 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
       status = -75;
       break;
     }
-    // split: f <= min f + delta is expanded this round, the rest waits (its min f kept)
+    RPROG(0, 3);
+    RPROG(1, round);
+    // split; a candidate no longer current (a cheaper node of its key exists) is dropped
     uint32_t fm = 0x7f800000u;
+    int allowed = 0;
     for (int e = tid; e < nA; e += NT) {
       const uint2 en = LA[e];
       if (__uint_as_float(en.x) <= thr) {
-        LE[atomicAdd(&S.nE, 1)] = (int)en.y;
+        float vm;
+        if (node_current(A, (int)en.y, &vm)) {
+          LE[atomicAdd(&S.nE, 1)] = (int)en.y;
+          allowed += vm < 1.0f;
+        }
       } else {
         LB[atomicAdd(&S.nB, 1)] = en;
         fm = min(fm, en.x);
       }
     }
-    for (int o = 32; o > 0; o >>= 1) fm = min(fm, (uint32_t)__shfl_xor((int)fm, o, 64));
+    fm = wave_min_u32(fm);
     if (lane == 0 && fm != 0x7f800000u) atomicMin(&S.fnext, fm);
+    if (allowed) atomicAdd(&S.n_allowed, allowed);
     block_sync();
-    const int nE = S.nE;
+    // the shot schedule (HybridAStar.cpp:115-154): the counter advances by the round's
+    // shot-allowed expansions; each time it reaches the interval one shot is due and the
+    // interval decays.  The due shots go to the round's allowed nodes of lowest {f, tie}.
+    if (tid == 0) {
+      int c = S.since_shot + S.n_allowed, k = 0;
+      while (c >= S.interval && k < RW) {
+        c -= S.interval;
+        S.interval = max(S.interval - P.shot_decay, 50);
+        ++k;
+      }
+      S.since_shot = k == RW ? 0 : c;
+      S.n_sel = k;
+      for (int q = 0; q < RW; ++q) S.sel[q] = ~0ull;
+    }
+    block_sync();
+    const int nE = S.nE, n_sel = S.n_sel;
+    RPROG(0, 4);
+    RPROG(2, nE);
+    unsigned long long prev_sel = 0;
+    for (int q = 0; q < n_sel; ++q) {
+      unsigned long long m = ~0ull;
+      for (int e = tid; e < nE; e += NT) {
+        const Node3* nd = &A.nodes[LE[e]];
+        const int4 q0 = *reinterpret_cast<const int4*>(nd);
+        if (nd->vmin >= 1.0f) continue;
+        const unsigned long long v = ((unsigned long long)(uint32_t)q0.y << 32) | (uint32_t)q0.w;
+        if ((q == 0 || v > prev_sel) && v < m) m = v;
+      }
+      m = wave_min_u64(m);
+      if (lane == 0 && m != ~0ull) atomicMin(&S.sel[q], m);
+      block_sync();
+      prev_sel = S.sel[q];
+    }
     // one wavefront per expanded node
     for (;;) {
       int e = 0;
       if (lane == 0) e = atomicAdd(&S.eNext, 1);
       e = ufi(e);
       if (e >= nE) break;
-      relaxed_expand(P, A, S, S.apf[wv], GC, dist, hlim, hs_x, hs_y, rp.h_weight, LE[e], wv, lane, LB);
+      RPROG(0, 5);
+      RPROG(3, e);
+      relaxed_expand(P, A, S, S.apf[wv], GC, dist, hlim, hs_x, hs_y, rp.h_weight, LE[e], lane, LA);
     }
+    RPROG(0, 6);
+    block_sync();
+    // the round's successors that are still their key's best join the next open list
+    const int nN = min(S.nN, A.list_cap);
+    fm = 0x7f800000u;
+    for (int e = tid; e < nN; e += NT) {
+      const uint2 en = LA[e];
+      if (!node_current(A, (int)en.y, nullptr)) continue;
+      const int pos = atomicAdd(&S.nB, 1);
+      if (pos < A.list_cap) {
+        LB[pos] = en;
+        fm = min(fm, en.x);
+      } else {
+        S.overflow = 1;
+      }
+    }
+    fm = wave_min_u32(fm);
+    if (lane == 0 && fm != 0x7f800000u) atomicMin(&S.fnext, fm);
+    RPROG(0, 7);
     block_sync();
     if (tid == 0) {
       S.nA = min(S.nB, A.list_cap);
       S.nB = 0;
+      S.nE_last = nE;
       S.nE = 0;
+      S.nN = 0;
+      S.n_allowed = 0;
+      S.n_sel = 0;
       S.eNext = 0;
       S.fmin = S.fnext;
       S.fnext = 0x7f800000u;
       S.rounds = round + 1;
+      // watchdog: a search still running after RELAX_WATCHDOG ticks ends as an overflow
+      if (__builtin_amdgcn_s_memrealtime() - t_start > RELAX_WATCHDOG) S.overflow = 2;
     }
     block_sync();
-    a = (a + 1) % 3;  // the next open list becomes the open list; the old open list is free
+    a ^= 1;  // the next open list becomes the open list
   }
+  RPROG(0, 8);
   block_sync();
   // ---- result and reconstruction (HybridAStar.cpp:208-262, as the exact kernel), by wave 0
   const unsigned long long best = S.best;
@@ -557,7 +667,20 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
         terminal = S.shot_term[sw];
         dub_n = S.shot_n[sw];
       } else {
-        terminal = (int)tag;
+        // the goal node of the last round whose {g, tie} won (its LE is still intact)
+        int t = 0x7fffffff;
+        for (int e = lane; e < S.nE_last; e += 64) {
+          const int idx = LE[e];
+          const Node3 nd = A.nodes[idx];
+          if (key3_x(nd.key) == P.goal_cx && key3_y(nd.key) == P.goal_cy &&
+              (((unsigned long long)__float_as_uint(nd.g) << 32) | ((uint32_t)nd.r & 0x7fffffffu)) == best)
+            t = min(t, idx);
+        }
+        terminal = (int)wave_min_u32((uint32_t)t);
+        if (terminal == 0x7fffffff) {
+          ok = 0;
+          status = -75;
+        }
       }
     }
     int path_len = 0;
@@ -641,27 +764,33 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
       R->cycles[1] = R->t_end - t_heur;
       R->cycles[2] = (unsigned long long)S.buckets;
       R->cycles[3] = (unsigned long long)S.rounds;
+      R->cycles[4] = (unsigned long long)S.overflow;
+      R->cycles[5] = (unsigned long long)S.nA;
+      R->cycles[6] = (unsigned long long)S.nE_last;
+      R->cycles[7] = (unsigned long long)S.fmin;
 #ifdef RELAX_STAMPS
       for (int k = 0; k < 6; ++k) R->cycles[8 + k] = S.stamp[k];
 #endif
     }
   }
+  RPROG(0, 9);
   // leave the best-g table empty for the next planner: the slots this search claimed (kept in
   // its nodes), or the whole table when an overflow may have left claimed slots without a node
   if (S.overflow) {
     for (size_t i = tid; i <= A.tmask; i += NT) {
       A.table[i].key = EMPTY_KEY;
-      A.table[i].gi = 0xffffffffu;
+      A.table[i].best = ~0ull;
     }
   } else {
     const int nn = min(S.nodes, A.node_cap);
     for (int n = tid; n < nn; n += NT) {
       const uint32_t t = (uint32_t)A.nodes[n].l;
       A.table[t].key = EMPTY_KEY;
-      A.table[t].gi = 0xffffffffu;
+      A.table[t].best = ~0ull;
     }
   }
   block_sync();
+  RPROG(0, 10);
 }
 
 // Persistent: grid = resident relaxed arenas; each workgroup pulls planners from *next.
