@@ -1,0 +1,44 @@
+"""Slot utilisation of one batched find_path (the bench's cfg3 batch): how much of the kernel's
+time the resident slots are busy, from each search's s_memrealtime start/end (10 ns ticks).
+
+    python tools/tail_analysis.py [--batch 23552] [--steps 2]
+Prints the kernel time, sum of search durations / slots (the ideal time with no tail), the
+busy fraction, and the number of busy slots over time (deciles of the kernel)."""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import bench  # noqa: E402
+from path_planning_pkg_amd import planner as gpu  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=23552)
+ap.add_argument("--steps", type=int, default=2)
+a = ap.parse_args()
+args = bench.parse_args(["--batch", str(a.batch)])
+if args.grid is None:
+    args.grid = 1024
+cfgs = [bench.query_case(args, q) for q in range(a.batch)]
+planners, _ = bench.build_planners(gpu, cfgs, 0)
+vels = [c[1]["vel"] for c in cfgs]
+starts = [c[1]["start"] for c in cfgs]
+bufs = gpu.BatchBuffers(planners, cap=8192)
+for step in range(a.steps):
+    gpu.reset_batch(bufs)
+    r = gpu.find_path_batch_arrays(planners, vels, starts, buffers=bufs)
+    t = np.array([p.timing() for p in planners], dtype=np.float64)
+    t0, t1 = t[:, 0].min(), t[:, 1].max()
+    dur = (t[:, 1] - t[:, 0]) * 1e-5  # ms
+    slots = len(set(int(s) for s in t[:, 2]))
+    span = (t1 - t0) * 1e-5
+    grid = np.linspace(t0, t1, 11)
+    busy = [int(((t[:, 0] <= g) & (t[:, 1] > g)).sum()) for g in grid[:-1]]
+    print(json.dumps({"step": step, "kernel_ms": r.kernel_ms, "span_ms": span, "slots_used": slots,
+                      "sum_dur_ms": float(dur.sum()), "ideal_ms": float(dur.sum() / slots),
+                      "busy_frac": float(dur.sum() / (slots * span)), "longest_ms": float(dur.max()),
+                      "busy_slots_by_decile": busy}), flush=True)
