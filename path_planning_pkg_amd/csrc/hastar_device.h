@@ -462,6 +462,16 @@ __device__ __forceinline__ float apf_fused(const PlannerDev& P, ApfStage& S, flo
 // Angles and distances accumulate sequentially exactly like the reference loops; each
 // lane keeps the value of its own sample index.  Returns the sample count or -1 when
 // the scratch is too small.
+// MODE 0: sample only.  MODE 1: also check every sample as Grid3D::check_path does
+// (path_is_free's cell rule) chunk by chunk and return -2 at the first blocked chunk, so a failed
+// shot stops early; a non-negative result then means the whole path is free.  MODE 2: count
+// only (the scratch-size check of MODE 0, no samples written).
+__device__ __forceinline__ bool sample_blocked(const PlannerDev& P, float x, float y) {
+  const int ci = trunc_f(roundf(x / P.res));
+  const int cj = trunc_f(roundf(y / P.res));
+  return ci < 0 || ci >= P.N || cj < 0 || cj >= P.N || gp(P.occ)[(size_t)ci * P.N + cj] >= P.thr;
+}
+template <int MODE = 0>
 __device__ inline int dubins_sample(const PlannerDev& P, const Centres& C, int word, const float prm[4], GAS float* xyh,
                                     GAS float* curv, int cap, int lane) {
   const float r = P.r_min, as = P.ang_step, st = P.step;
@@ -479,6 +489,7 @@ __device__ inline int dubins_sample(const PlannerDev& P, const Centres& C, int w
   const int n2 = n1 + trunc_f(floorf(lst / st));
   const int n3 = n2 + trunc_f(floorf((g_right ? -prm[3] : prm[3]) / as));
   if (n1 < 0 || n2 < n1 || n3 < n2 || n3 + 1 > cap) return -1;
+  if (MODE == 2) return n3 + 1;
   const float k = 1.0f / r;
   // first arc
   float th = prm[0];
@@ -489,12 +500,16 @@ __device__ inline int dubins_sample(const PlannerDev& P, const Centres& C, int w
       th = s_right ? th - as : th + as;
     }
     const int i = base + lane;
+    bool bad = false;
     if (i < n1) {
-      xyh[3 * i] = csx + r * g_cosf(mine);
-      xyh[3 * i + 1] = csy + r * g_sinf(mine);
+      const float x = csx + r * g_cosf(mine), y = csy + r * g_sinf(mine);
+      xyh[3 * i] = x;
+      xyh[3 * i + 1] = y;
       xyh[3 * i + 2] = (float)(s_right ? wrap_pi_d((double)mine - M_PI_2) : wrap_pi_d((double)mine + M_PI_2));
       curv[i] = k;
+      if (MODE == 1) bad = sample_blocked(P, x, y);
     }
+    if (MODE == 1 && __ballot(bad)) return -2;
   }
   // straight segment
   const float ts = g_atan2f(ey, ex);
@@ -507,12 +522,16 @@ __device__ inline int dubins_sample(const PlannerDev& P, const Centres& C, int w
       dd += st;
     }
     const int i = base + lane;
+    bool bad = false;
     if (i < n2) {
-      xyh[3 * i] = ax + mine * ct;
-      xyh[3 * i + 1] = ay + mine * sn;
+      const float x = ax + mine * ct, y = ay + mine * sn;
+      xyh[3 * i] = x;
+      xyh[3 * i + 1] = y;
       xyh[3 * i + 2] = ts;
       curv[i] = 0.0f;
+      if (MODE == 1) bad = sample_blocked(P, x, y);
     }
+    if (MODE == 1 && __ballot(bad)) return -2;
   }
   // second arc
   th = prm[2];
@@ -523,20 +542,28 @@ __device__ inline int dubins_sample(const PlannerDev& P, const Centres& C, int w
       th = g_right ? th - as : th + as;
     }
     const int i = base + lane;
+    bool bad = false;
     if (i < n3) {
-      xyh[3 * i] = cgx + r * g_cosf(mine);
-      xyh[3 * i + 1] = cgy + r * g_sinf(mine);
+      const float x = cgx + r * g_cosf(mine), y = cgy + r * g_sinf(mine);
+      xyh[3 * i] = x;
+      xyh[3 * i + 1] = y;
       xyh[3 * i + 2] = (float)(g_right ? wrap_pi_d((double)mine - M_PI_2) : wrap_pi_d((double)mine + M_PI_2));
       curv[i] = k;
+      if (MODE == 1) bad = sample_blocked(P, x, y);
     }
+    if (MODE == 1 && __ballot(bad)) return -2;
   }
+  bool bad = false;
   if (lane == 0) {
     const float e = prm[2] + prm[3];
-    xyh[3 * n3] = cgx + r * g_cosf(e);
-    xyh[3 * n3 + 1] = cgy + r * g_sinf(e);
+    const float x = cgx + r * g_cosf(e), y = cgy + r * g_sinf(e);
+    xyh[3 * n3] = x;
+    xyh[3 * n3 + 1] = y;
     xyh[3 * n3 + 2] = (float)(g_right ? wrap_pi_d((double)e - M_PI_2) : wrap_pi_d((double)e + M_PI_2));
     curv[n3] = 0.0f;
+    if (MODE == 1) bad = sample_blocked(P, x, y);
   }
+  if (MODE == 1 && __ballot(bad)) return -2;
   return n3 + 1;
 }
 
@@ -544,11 +571,8 @@ __device__ inline int dubins_sample(const PlannerDev& P, const Centres& C, int w
 // lanes: caller must order (block barrier) before calling.
 __device__ __forceinline__ bool path_is_free(const PlannerDev& P, const GAS float* xyh, int n, int lane) {
   bool bad = false;
-  for (int i = lane; i < n; i += 64) {
-    const int ci = trunc_f(roundf(xyh[3 * i] / P.res));
-    const int cj = trunc_f(roundf(xyh[3 * i + 1] / P.res));
-    if (ci < 0 || ci >= P.N || cj < 0 || cj >= P.N || gp(P.occ)[(size_t)ci * P.N + cj] >= P.thr) bad = true;
-  }
+  for (int i = lane; i < n; i += 64)
+    if (sample_blocked(P, xyh[3 * i], xyh[3 * i + 1])) bad = true;
   return __ballot(bad) == 0;
 }
 

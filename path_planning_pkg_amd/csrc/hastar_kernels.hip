@@ -997,11 +997,16 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
         // Dubins::get_shortest_path (Dubins.cpp:125-153)
         const float L = dubins_shortest(r, cur.x, cur.y, cur.h, P.goal_x, P.goal_y, P.goal_h, &word, prm);
         const Centres C = dubins_centres(r, cur.x, cur.y, cur.h, P.goal_x, P.goal_y, P.goal_h);
-        const int n = dubins_sample(P, C, word, prm, gp(A.dub_xyh), gp(A.dub_curv), A.dub_cap, lane);
-        if (n < 0) { c.status = -75; break; }
-        wave_lds_sync();
+        // the shot counts only when its first arc turns <= 90 degrees (Dubins.cpp:125-153); the
+        // samples are checked as they are made (Grid3D::check_path), so a blocked shot stops at
+        // its first blocked chunk
         const bool first_arc_long = fabsf(prm[1]) > (float)M_PI_2;
-        if (!first_arc_long && path_is_free(P, gp(A.dub_xyh), n, lane)) {
+        const int n = first_arc_long
+                          ? dubins_sample<2>(P, C, word, prm, gp(A.dub_xyh), gp(A.dub_curv), A.dub_cap, lane)
+                          : dubins_sample<1>(P, C, word, prm, gp(A.dub_xyh), gp(A.dub_curv), A.dub_cap, lane);
+        if (n == -1) { c.status = -75; break; }
+        wave_lds_sync();
+        if (!first_arc_long && n > 0) {
           terminal = cur.prev;
           cost = cur.g + L;
           ok = 1;

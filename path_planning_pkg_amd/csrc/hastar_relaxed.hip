@@ -62,6 +62,7 @@ __device__ __forceinline__ bool bucket_put(const RelaxArena& A, BucketEntry* lds
 #define RSTAMP_BEGIN() (void)0
 #define RSTAMP(k) (void)0
 #endif
+constexpr float SHOT_ADVANCE = 0.8f;  // an extra shot once the frontier's best f - g falls to 0.8x the last shooter's
 constexpr unsigned long long RELAX_WATCHDOG = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
 constexpr uint32_t EMPTY_KEY = 0xffffffffu;  // no node key has all bits set (x < 4096, bin < 256 with y < 4096)
 
@@ -122,6 +123,12 @@ __device__ __forceinline__ bool node_current(const RelaxArena& A, int idx, float
   const unsigned long long mine = ((unsigned long long)__float_as_uint(q1.z) << 32) | (uint32_t)q0.w;
   return __hip_atomic_load(&A.table[(uint32_t)q0.z].best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == mine;
 }
+// a shooter's rank among the round's allowed nodes: the nearest to the goal by the heuristic
+// part of f (f - g), then the tie.  The round's nodes share f to within delta, so this picks
+// the frontier's most advanced nodes, whose shots are the likeliest to be free.
+__device__ __forceinline__ unsigned long long shot_key(float f, float g, uint32_t tie) {
+  return ((unsigned long long)__float_as_uint(fmaxf(f - g, 0.0f)) << 32) | tie;
+}
 __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
   for (int o = 32; o > 0; o >>= 1) {
     const unsigned long long w = ((unsigned long long)(uint32_t)__shfl_xor((int)(v >> 32), o, 64) << 32) |
@@ -148,7 +155,8 @@ struct RelaxShared {
   int since_shot, interval;
   int pops, succ, shots, rounds;
   int n_sel;                     // shots of this round
-  unsigned long long sel[RW];    // their shooters: f bits << 32 | tie, lowest first
+  float last_shot_h;             // f - g of the last shooter
+  unsigned long long sel[RW];    // their shooters' shot_key, lowest first
   int shot_term[RW], shot_n[RW];
   unsigned long long stamp[6];
 };
@@ -330,18 +338,17 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
   const int cx = key3_x(key), cy = key3_y(key), cbin = key3_bin(key);
   if (lane == 0) atomicAdd(&S.pops, 1);
   // goal test (Node3D::operator==: the cell only, Node3D.h:42).  The stages below run under
-  // wave-uniform flags (no early return out of divergent code).
+  // wave-uniform flags, with no early return out of divergent code.
   int done = 0;
   if (cx == P.goal_cx && cy == P.goal_cy) {
     if (lane == 0) atomicMin(&S.best, ((unsigned long long)__float_as_uint(cg) << 32) | (tie & 0x7fffffffu));
     done = 1;
   }
   // Dubins shot (HybridAStar.cpp:115-154): the round's shooters were chosen between rounds
-  // (the reference's interval / decay schedule over the expansions, lowest f first)
   const bool allowed = cvm < 1.0f;
   int shot = -1;
   if (!done && allowed) {
-    const unsigned long long v = ((unsigned long long)__float_as_uint(cf) << 32) | tie;
+    const unsigned long long v = shot_key(cf, cg, tie);
     for (int q = 0; q < S.n_sel; ++q)
       if (S.sel[q] == v) shot = q;
   }
@@ -355,13 +362,11 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
     const Centres C = dubins_centres(r, cxp, cyp, chd, P.goal_x, P.goal_y, P.goal_h);
     GAS float* xyh = gp(A.dub_xyh) + (size_t)shot * A.dub_cap * 3;
     GAS float* curv = gp(A.dub_curv) + (size_t)shot * A.dub_cap;
-    const int n = ufi(dubins_sample(P, C, word, prm, xyh, curv, A.dub_cap, lane));
-    wave_lds_sync();
+    // sampled and checked chunk by chunk: a blocked shot stops at its first blocked chunk
     const int first_arc_long = ufi(fabsf(prm[1]) > (float)M_PI_2 ? 1 : 0);
-    int free_shot = 0;
-    if (n > 0 && !first_arc_long) free_shot = path_is_free(P, xyh, n, lane) ? 1 : 0;
-    free_shot = ufi(free_shot);
-    if (free_shot) {
+    const int n = first_arc_long ? -1 : ufi(dubins_sample<1>(P, C, word, prm, xyh, curv, A.dub_cap, lane));
+    wave_lds_sync();
+    if (n > 0) {
       const int term = ufi(cur.prev);
       if (lane == 0) {
         S.shot_term[shot] = term;
@@ -512,6 +517,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
     S.nE_last = 0;
     S.n_allowed = 0;
     S.n_sel = 0;
+    S.last_shot_h = FLT_MAX;
     S.eNext = 0;
     S.nodes = 1;
     S.best = ~0ull;
@@ -571,7 +577,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
     block_sync();
     // the shot schedule (HybridAStar.cpp:115-154): the counter advances by the round's
     // shot-allowed expansions; each time it reaches the interval one shot is due and the
-    // interval decays.  The due shots go to the round's allowed nodes of lowest {f, tie}.
+    // interval decays.  The due shots go to the round's allowed nodes of lowest shot_key.
     if (tid == 0) {
       int c = S.since_shot + S.n_allowed, k = 0;
       while (c >= S.interval && k < RW) {
@@ -584,7 +590,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
       for (int q = 0; q < RW; ++q) S.sel[q] = ~0ull;
     }
     block_sync();
-    const int nE = S.nE, n_sel = S.n_sel;
+    const int nE = S.nE, n_due = S.n_sel, n_sel = max(n_due, S.n_allowed > 0 ? 1 : 0);
     RPROG(0, 4);
     RPROG(2, nE);
     unsigned long long prev_sel = 0;
@@ -593,15 +599,29 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
       for (int e = tid; e < nE; e += NT) {
         const Node3* nd = &A.nodes[LE[e]];
         const int4 q0 = *reinterpret_cast<const int4*>(nd);
-        if (nd->vmin >= 1.0f) continue;
-        const unsigned long long v = ((unsigned long long)(uint32_t)q0.y << 32) | (uint32_t)q0.w;
+        const float4 q1 = *(reinterpret_cast<const float4*>(nd) + 1);  // p, cc, g, vmin
+        if (q1.w >= 1.0f) continue;
+        const unsigned long long v = shot_key(__int_as_float(q0.y), q1.z, (uint32_t)q0.w);
         if ((q == 0 || v > prev_sel) && v < m) m = v;
       }
       m = wave_min_u64(m);
       if (lane == 0 && m != ~0ull) atomicMin(&S.sel[q], m);
       block_sync();
       prev_sel = S.sel[q];
+      if (q == 0) {
+        // besides the schedule's due shots: one from the frontier's most advanced node whenever
+        // its heuristic has fallen to SHOT_ADVANCE of the last shooter's (a shot costs one
+        // wavefront for a few microseconds; a round without one can cost the search many rounds)
+        const float h0 = __uint_as_float((uint32_t)(prev_sel >> 32));
+        if (tid == 0) {
+          const bool advance = prev_sel != ~0ull && h0 <= SHOT_ADVANCE * S.last_shot_h;
+          if (advance || n_due > 0) S.last_shot_h = h0;
+          S.n_sel = n_due > 0 ? n_due : (advance ? 1 : 0);
+        }
+        if (n_due == 0) break;
+      }
     }
+    block_sync();
     // one wavefront per expanded node
     for (;;) {
       int e = 0;
