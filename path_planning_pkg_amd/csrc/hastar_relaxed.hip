@@ -116,10 +116,13 @@ __device__ __forceinline__ bool table_lower(const RelaxArena& A, uint32_t key, u
 }
 // A node is current iff it still holds its key's best {g, tie}.  Only asked between rounds,
 // when the table is final for the round, so the answer does not depend on wavefront timing.
-__device__ __forceinline__ bool node_current(const RelaxArena& A, int idx, float* vmin) {
+__device__ __forceinline__ bool node_current(const RelaxArena& A, int idx, float* vmin = nullptr,
+                                             float* g = nullptr, uint32_t* tie = nullptr) {
   const int4 q0 = *reinterpret_cast<const int4*>(&A.nodes[idx]);      // key, f, l, r
   const float4 q1 = *(reinterpret_cast<const float4*>(&A.nodes[idx]) + 1);  // p, cc, g, vmin
   if (vmin) *vmin = q1.w;
+  if (g) *g = q1.z;
+  if (tie) *tie = (uint32_t)q0.w;
   const unsigned long long mine = ((unsigned long long)__float_as_uint(q1.z) << 32) | (uint32_t)q0.w;
   return __hip_atomic_load(&A.table[(uint32_t)q0.z].best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == mine;
 }
@@ -517,6 +520,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
     S.nE_last = 0;
     S.n_allowed = 0;
     S.n_sel = 0;
+    for (int q = 0; q < RW; ++q) S.sel[q] = ~0ull;
     S.last_shot_h = FLT_MAX;
     S.eNext = 0;
     S.nodes = 1;
@@ -555,16 +559,23 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
     }
     RPROG(0, 3);
     RPROG(1, round);
-    // split; a candidate no longer current (a cheaper node of its key exists) is dropped
+    // split; a candidate no longer current (a cheaper node of its key exists) is dropped.  The
+    // split also ranks the round's shot-allowed candidates (shot_key) for the first shooter.
     uint32_t fm = 0x7f800000u;
     int allowed = 0;
+    unsigned long long mk = ~0ull;
     for (int e = tid; e < nA; e += NT) {
       const uint2 en = LA[e];
       if (__uint_as_float(en.x) <= thr) {
-        float vm;
-        if (node_current(A, (int)en.y, &vm)) {
+        float vm, g;
+        uint32_t tie;
+        if (node_current(A, (int)en.y, &vm, &g, &tie)) {
           LE[atomicAdd(&S.nE, 1)] = (int)en.y;
-          allowed += vm < 1.0f;
+          if (vm < 1.0f) {
+            ++allowed;
+            const unsigned long long v = shot_key(__uint_as_float(en.x), g, tie);
+            mk = v < mk ? v : mk;
+          }
         }
       } else {
         LB[atomicAdd(&S.nB, 1)] = en;
@@ -574,10 +585,15 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
     fm = wave_min_u32(fm);
     if (lane == 0 && fm != 0x7f800000u) atomicMin(&S.fnext, fm);
     if (allowed) atomicAdd(&S.n_allowed, allowed);
+    mk = wave_min_u64(mk);
+    if (lane == 0 && mk != ~0ull) atomicMin(&S.sel[0], mk);
     block_sync();
     // the shot schedule (HybridAStar.cpp:115-154): the counter advances by the round's
     // shot-allowed expansions; each time it reaches the interval one shot is due and the
     // interval decays.  The due shots go to the round's allowed nodes of lowest shot_key.
+    // Besides those, one shot goes to the frontier's most advanced node whenever its f - g has
+    // fallen to SHOT_ADVANCE of the last shooter's (a shot costs one wavefront for a few
+    // microseconds; a round without one can cost the search many rounds).
     if (tid == 0) {
       int c = S.since_shot + S.n_allowed, k = 0;
       while (c >= S.interval && k < RW) {
@@ -586,15 +602,19 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
         ++k;
       }
       S.since_shot = k == RW ? 0 : c;
-      S.n_sel = k;
-      for (int q = 0; q < RW; ++q) S.sel[q] = ~0ull;
+      const unsigned long long s0 = S.sel[0];
+      const float h0 = __uint_as_float((uint32_t)(s0 >> 32));
+      const bool advance = s0 != ~0ull && h0 <= SHOT_ADVANCE * S.last_shot_h;
+      if (s0 != ~0ull && (advance || k > 0)) S.last_shot_h = h0;
+      S.n_sel = k > 0 ? k : (advance ? 1 : 0);
     }
     block_sync();
-    const int nE = S.nE, n_due = S.n_sel, n_sel = max(n_due, S.n_allowed > 0 ? 1 : 0);
+    const int nE = S.nE, n_sel = S.n_sel;
     RPROG(0, 4);
     RPROG(2, nE);
-    unsigned long long prev_sel = 0;
-    for (int q = 0; q < n_sel; ++q) {
+    // further due shooters (rare: more than one due in a round), next-lowest shot_key each
+    unsigned long long prev_sel = S.sel[0];
+    for (int q = 1; q < n_sel; ++q) {
       unsigned long long m = ~0ull;
       for (int e = tid; e < nE; e += NT) {
         const Node3* nd = &A.nodes[LE[e]];
@@ -602,26 +622,13 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
         const float4 q1 = *(reinterpret_cast<const float4*>(nd) + 1);  // p, cc, g, vmin
         if (q1.w >= 1.0f) continue;
         const unsigned long long v = shot_key(__int_as_float(q0.y), q1.z, (uint32_t)q0.w);
-        if ((q == 0 || v > prev_sel) && v < m) m = v;
+        if (v > prev_sel && v < m) m = v;
       }
       m = wave_min_u64(m);
       if (lane == 0 && m != ~0ull) atomicMin(&S.sel[q], m);
       block_sync();
       prev_sel = S.sel[q];
-      if (q == 0) {
-        // besides the schedule's due shots: one from the frontier's most advanced node whenever
-        // its heuristic has fallen to SHOT_ADVANCE of the last shooter's (a shot costs one
-        // wavefront for a few microseconds; a round without one can cost the search many rounds)
-        const float h0 = __uint_as_float((uint32_t)(prev_sel >> 32));
-        if (tid == 0) {
-          const bool advance = prev_sel != ~0ull && h0 <= SHOT_ADVANCE * S.last_shot_h;
-          if (advance || n_due > 0) S.last_shot_h = h0;
-          S.n_sel = n_due > 0 ? n_due : (advance ? 1 : 0);
-        }
-        if (n_due == 0) break;
-      }
     }
-    block_sync();
     // one wavefront per expanded node
     for (;;) {
       int e = 0;
@@ -639,7 +646,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
     fm = 0x7f800000u;
     for (int e = tid; e < nN; e += NT) {
       const uint2 en = LA[e];
-      if (!node_current(A, (int)en.y, nullptr)) continue;
+      if (!node_current(A, (int)en.y)) continue;
       const int pos = atomicAdd(&S.nB, 1);
       if (pos < A.list_cap) {
         LB[pos] = en;
@@ -660,6 +667,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
       S.nN = 0;
       S.n_allowed = 0;
       S.n_sel = 0;
+      for (int q = 0; q < RW; ++q) S.sel[q] = ~0ull;
       S.eNext = 0;
       S.fmin = S.fnext;
       S.fnext = 0x7f800000u;
