@@ -362,9 +362,11 @@ def velocity_profile_phase(gpu, last, device, vels):
     fla = np.full(n_all, 2, np.uint8)
     lens_all = last.lens.astype(np.int64).copy()
     vg.profile_last_batch(lens_all, v0a, vma, fla)
-    t0 = time.perf_counter()
-    feas_a, vel_a = vg.profile_last_batch(lens_all, v0a, vma, fla)
-    ms_dev = (time.perf_counter() - t0) * 1e3
+    ms_dev = float("inf")  # best of 3 (host-side page faults on the output arrays vary)
+    for _ in range(3):
+        t0 = time.perf_counter()
+        feas_a, vel_a = vg.profile_last_batch(lens_all, v0a, vma, fla)
+        ms_dev = min(ms_dev, (time.perf_counter() - t0) * 1e3)
     lens = last.lens[idx].astype(np.int64)
     off = np.zeros(len(idx) + 1, np.int64)
     np.cumsum(lens, out=off[1:])
@@ -374,9 +376,11 @@ def velocity_profile_phase(gpu, last, device, vels):
     vm = np.full(len(idx), VEL_PARAMS[0], np.float32)
     flags = np.full(len(idx), 2, np.uint8)  # stop_at_goal
     vg.profile_packed(off, X, K, v0, vm, flags)
-    t0 = time.perf_counter()
-    feas, vel = vg.profile_packed(off, X, K, v0, vm, flags)
-    ms = (time.perf_counter() - t0) * 1e3
+    ms = float("inf")
+    for _ in range(3):
+        t0 = time.perf_counter()
+        feas, vel = vg.profile_packed(off, X, K, v0, vm, flags)
+        ms = min(ms, (time.perf_counter() - t0) * 1e3)
     # the oracle (1 thread) over the same paths: CPU time and bit parity
     from oracle import pyoracle
     cpu_s, same = 0.0, True
