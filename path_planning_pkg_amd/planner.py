@@ -37,6 +37,14 @@ def load_library():
         return _lib
     if not LIB_PATH.exists():
         raise FileNotFoundError(f"{LIB_PATH} missing: run __graft_entry__.build() (make -C path_planning_pkg_amd/csrc)")
+    # torch (when installed) bundles its own copy of the HIP runtime, under the same soname
+    # libamdhip64.so.7.  Loaded first, that copy also serves this library; loaded after
+    # /opt/rocm's, it would be a second runtime in the process and find no GPU.  Importing
+    # torch only loads its libraries; it does not touch the GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(str(LIB_PATH))
     vp, fp, ip = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int)
     L.hastar_create_f32.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
