@@ -13,19 +13,25 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 from path_planning_pkg_amd import planner as gpu  # noqa: E402
-from tests.scenarios import drive, synthetic  # noqa: E402
+from tests.scenarios import drive, synthetic, synthetic_ref  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--grid", type=int, default=1024)
 ap.add_argument("--bins", type=int, default=72)
 ap.add_argument("--obstacles", type=int, default=200)
 ap.add_argument("--seeds", type=int, nargs="+", default=[1])
+ap.add_argument("--generator", choices=["pcg64", "mt19937"], default="mt19937")
+ap.add_argument("--replan", action="store_true", help="profile the bench step: find_path, reset, find_path")
 args = ap.parse_args()
 names = ["pop", "expand", "open_bookkeeping", "astar", "shot", "reconstruct", "loop", "astar_hbm_mode"]
 for s in args.seeds:
-    cfg, proto = synthetic(args.grid, args.bins, args.obstacles, s)
+    gen = synthetic_ref if args.generator == "mt19937" else synthetic
+    cfg, proto = gen(args.grid, args.bins, args.obstacles, s)
     p = gpu.HybridAStar(cfg)
     drive(p, proto)
+    if args.replan:
+        gpu.find_path_batch([p], [proto["vel"]], [proto["start"]])
+        p.reset()
     res, ms = gpu.find_path_batch([p], [proto["vel"]], [proto["start"]])
     cyc = p.cycles()
     st = res[0]["stats"]

@@ -19,6 +19,7 @@ from path_planning_pkg_amd import planner as gpu  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=23552)
 ap.add_argument("--steps", type=int, default=2)
+ap.add_argument("--clock", action="store_true", help="stamps build: shader clock of the searches under load")
 a = ap.parse_args()
 args = bench.parse_args(["--batch", str(a.batch)])
 if args.grid is None:
@@ -38,7 +39,15 @@ for step in range(a.steps):
     span = (t1 - t0) * 1e-5
     grid = np.linspace(t0, t1, 11)
     busy = [int(((t[:, 0] <= g) & (t[:, 1] > g)).sum()) for g in grid[:-1]]
-    print(json.dumps({"step": step, "kernel_ms": r.kernel_ms, "span_ms": span, "slots_used": slots,
+    clock = None
+    if a.clock:  # stamps build: s_memtime (shader clock) cycles of the search loop / its realtime span
+        li = int(np.argmax(dur))
+        cyc = np.array([planners[i].cycles()[6] for i in range(len(planners))], dtype=np.float64)
+        mhz = cyc / np.maximum(dur * 1e3, 1e-9)  # cycles per us
+        long_ix = np.argsort(-dur)[:16]
+        clock = {"longest_mhz": float(mhz[li]), "top16_mhz_mean": float(mhz[long_ix].mean()),
+                 "median_mhz_over_searches_gt_1ms": float(np.median(mhz[dur > 1.0]))}
+    print(json.dumps({"clock": clock, "step": step, "kernel_ms": r.kernel_ms, "span_ms": span, "slots_used": slots,
                       "sum_dur_ms": float(dur.sum()), "ideal_ms": float(dur.sum() / slots),
                       "busy_frac": float(dur.sum() / (slots * span)), "longest_ms": float(dur.max()),
                       "busy_slots_by_decile": busy}), flush=True)
