@@ -45,6 +45,20 @@ def algorithmic_bytes(st, K):
                  + 208 * st["astar_pops"].astype(np.float64).sum() + 12.0 * K * len(st))
 
 
+def step_balance(planners):
+    """What bounds the last timed step: the resident slots' busy time (the bulk of the
+    batch) or the longest search (its straggler).  From every search's start/end stamps
+    (s_memrealtime, 10 ns ticks) and the slot that ran it."""
+    t = np.array([p.timing() for p in planners], dtype=np.float64)
+    dur = (t[:, 1] - t[:, 0]) * 1e-5  # ms
+    span = (t[:, 1].max() - t[:, 0].min()) * 1e-5
+    slots = len(set(int(s) for s in t[:, 2]))
+    li = int(np.argmax(dur))
+    return {"span_ms": float(span), "slots_used": slots, "slot_busy_mean_ms": float(dur.sum() / slots),
+            "busy_frac": float(dur.sum() / (slots * span)), "longest_search_under_load_ms": float(dur[li]),
+            "longest_search_start_ms": float((t[li, 0] - t[:, 0].min()) * 1e-5)}
+
+
 def shard_query_ids(rank, world, batch):
     """Queries of one rank: weak scaling, B per GPU, disjoint across ranks, no exchange."""
     assert 0 <= rank < world
@@ -105,7 +119,9 @@ def parse_args(argv=None):
     ap.add_argument("--grid", type=int, default=None, help="default 1024 (cfg3, cfg5) or 2048 (cfg4)")
     ap.add_argument("--bins", type=int, default=72)
     ap.add_argument("--obstacles", type=int, default=200)
-    ap.add_argument("--max-pops", type=int, default=0, help="initial arena of a search in pops (0 = 262144)")
+    ap.add_argument("--max-pops", type=int, default=None,
+                    help="initial arena of a search in pops (0 = the library's 262144; default: 196608 for cfg3 "
+                         "so that ~1984 arenas of 46 MiB fit next to the planners' maps, 0 otherwise)")
     ap.add_argument("--max-astar-nodes", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -130,6 +146,11 @@ def parse_args(argv=None):
     args = ap.parse_args(argv)
     if args.grid is None:
         args.grid = 2048 if args.workload == "cfg4" else 1024
+    if args.max_pops is None:
+        # cfg3: 8 search wavefronts per CU need ~2048 arenas; at 196608 pops (the batch's longest
+        # search needs 172207) they take 46 MiB each and 1984 fit beside 23552 planners' maps.
+        # A search that outgrows its arena parks and resumes in a 4x one, so this is no limit.
+        args.max_pops = 196608 if args.workload == "cfg3" else 0
     if args.workload == "cfg4" and "--batch" not in sys.argv and "HASTAR_BENCH_BATCH" not in os.environ:
         args.batch = 6144  # 2048^2 maps: 32 MiB per planner; the arena pool takes the rest of the HBM
     return args
@@ -217,6 +238,8 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         avg_kernel_ms = float(np.mean(kernel_ms))
         achieved = float(np.mean(alg_bytes)) / (avg_kernel_ms * 1e-3) / 1e9
+        balance = step_balance(planners)  # before any other find_path overwrites the timings
+        balance["pool"] = planners[0].slots()
         vel_prof = velocity_profile_phase(gpu, last, device, vels)  # before any other find_path
         lat_ids = list(range(min(args.latency_queries, B)))
         lat = []
@@ -267,6 +290,7 @@ def main():
             "plan_latency_ms": {"gpu_median": float(np.median(lat)) if lat else None, "queries": [qids[i] for i in lat_ids],
                                 "gpu": lat},
             "longest_query": longest,
+            "step_balance": balance,
             "pops_per_step": pops_all / args.steps,
             "success_rate": oks / (B * args.steps),
             "search_status": sorted(statuses),

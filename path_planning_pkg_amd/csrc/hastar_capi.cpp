@@ -333,7 +333,7 @@ ArenaLayout arena_layout(const ArenaReq& r) {
   L.dub = align256((size_t)r.dub * 3 * sizeof(float));
   L.dubc = align256((size_t)r.dub * sizeof(float));
   L.chain = align256((size_t)r.chain * sizeof(int));
-  L.prevl = align256((size_t)ASTAR_LDS_CAP * sizeof(int));
+  L.prevl = align256((size_t)ASTAR_LDS_CAP * 2 * sizeof(int));  // {prev, g} per LDS A* node
   return L;
 }
 // Carve the arena at `q` and queue the clearing of its generation-stamped tables.

@@ -171,28 +171,34 @@ __device__ __forceinline__ void closed3_rebuild(SearchCtx& c, int n) {
 
 // -------------------------------------------------------- holonomic A* (AStar.cpp) -----
 // Each lazy A* search (AStar::find_path(int, int), AStar.cpp:100-113) keeps its open
-// tree in LDS as compact nodes (16-bit links, 20 B per node, A_CAP nodes per wavefront);
-// the closed records, the cell -> closed-record map and the nodes' prev links live in
-// the HBM slot arena, so every pop needs exactly one HBM round trip (the popped cell's
-// closed state, its prev link and the 8 neighbour probes, all in flight together).  A
-// search whose tree outgrows LDS is migrated once (same pool indices) to HBM nodes and
-// continues there.  Both modes run the same templated loop.
+// tree in LDS as compact nodes: {key, f} (8 B), the links {l, r} (16 bit each) and p
+// (16 bit), and one colour bit per node, 16 B per node with the f-ordered ring, so that
+// 8 search wavefronts fit a CU's 160 KiB LDS (2 per SIMD, the register budget).  Each
+// node's g and prev link live in the HBM slot arena (`pvg`, 8 B per node: read together
+// with the popped node's prev at the pop, written once per insert after the expansion);
+// so do the closed records and the cell -> closed-record map, and every pop needs exactly
+// one HBM round trip (the popped node's {prev, g}, its cell's closed state and the 8
+// neighbour probes, all in flight together).  A search whose tree outgrows LDS is
+// migrated once (same pool indices) to HBM nodes and continues there.  Both modes run
+// the same templated loop.
 constexpr int A_CAP = ASTAR_LDS_CAP;  // LDS open-tree nodes (index 0 = header)
 
-struct NodeA2 {
+typedef int v2i __attribute__((ext_vector_type(2)));
+struct NodeKF {
   uint32_t key;
   float f;
-  float g;
-  int16_t l, r;
 };
-struct NodeB2 {
-  int16_t p, color;
+struct LinkLR {
+  int16_t l, r;  // NIL = -1
 };
 struct AStarLds {
-  NodeA2 a[A_CAP];
-  NodeB2 b[A_CAP];
+  NodeKF kf[A_CAP];
+  LinkLR lr[A_CAP];
+  int16_t p[A_CAP];
+  uint32_t black[A_CAP / 32];    // colour bits (1 = black)
   int16_t ring[A_CAP];  // live node indices in f order (a ring: rank r at ring[(head + r) % A_CAP])
 };
+static_assert(sizeof(AStarLds) == 16 * A_CAP + A_CAP / 8, "LDS node layout");
 
 #define LAS __attribute__((address_space(3)))
 template <class T>
@@ -200,45 +206,54 @@ __device__ __forceinline__ LAS T* lp(T* p) {
   return (LAS T*)p;
 }
 
-// compact LDS layout for RBT<>: {key, f, g, l|r} (16 B) + {p, color} (4 B), prev in HBM
+// the compact LDS layout for RBT<>; g and prev (HBM) are read by the search loop itself
 struct LdsAcc {
   static constexpr bool kPathWalk = false;
-  LAS NodeA2* a;
-  LAS NodeB2* b;
-  GAS int* pv;
-  __device__ __forceinline__ int L(int x) const { return ufi(a[x].l); }
-  __device__ __forceinline__ int R(int x) const { return ufi(a[x].r); }
-  __device__ __forceinline__ int P(int x) const { return ufi(b[x].p); }
-  __device__ __forceinline__ int C(int x) const { return ufi(b[x].color); }
-  __device__ __forceinline__ void sL(int x, int v) { a[x].l = (int16_t)v; }
-  __device__ __forceinline__ void sR(int x, int v) { a[x].r = (int16_t)v; }
-  __device__ __forceinline__ void sP(int x, int v) { b[x].p = (int16_t)v; }
-  __device__ __forceinline__ void sC(int x, int v) { b[x].color = (int16_t)v; }
-  __device__ __forceinline__ uint32_t K(int x) const { return ufu(a[x].key); }
-  __device__ __forceinline__ float F(int x) const { return uff(a[x].f); }
-  __device__ __forceinline__ float G(int x) const { return uff(a[x].g); }
-  __device__ __forceinline__ int PV(int x) const { return pv[x]; }
+  LAS AStarLds* s;
+  int lane;
+  // every field is accessed through its own type (no type punning: with strict aliasing a
+  // 16-bit store through an int* view would not be ordered against int loads)
+  __device__ __forceinline__ int L(int x) const { return ufi(s->lr[x].l); }
+  __device__ __forceinline__ int R(int x) const { return ufi(s->lr[x].r); }
+  __device__ __forceinline__ int P(int x) const { return ufi(s->p[x]); }
+  __device__ __forceinline__ int C(int x) const { return ufi((int)((s->black[x >> 5] >> (x & 31)) & 1u)); }
+  __device__ __forceinline__ void sL(int x, int v) { s->lr[x].l = (int16_t)v; }
+  __device__ __forceinline__ void sR(int x, int v) { s->lr[x].r = (int16_t)v; }
+  __device__ __forceinline__ void sP(int x, int v) { s->p[x] = (int16_t)v; }
+  // one lane updates the colour word (LDS atomics, no return value: nothing waits on them;
+  // the wave's later LDS reads are ordered after them)
+  __device__ __forceinline__ void sC(int x, int v) {
+    const uint32_t bit = 1u << (x & 31);
+    if (lane == 0) {
+      if (v == RB_BLACK) __hip_atomic_fetch_or(&s->black[x >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      else __hip_atomic_fetch_and(&s->black[x >> 5], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __device__ __forceinline__ uint32_t K(int x) const { return ufu(s->kf[x].key); }
+  __device__ __forceinline__ float F(int x) const { return uff(s->kf[x].f); }
   __device__ __forceinline__ Quad quad(int x) const {
-    typedef int v4 __attribute__((ext_vector_type(4)));
-    const v4 v = *(const LAS v4*)&a[x];
+    const uint32_t k = s->kf[x].key;
+    const float f = s->kf[x].f;
+    const int l = s->lr[x].l, r = s->lr[x].r;
     Quad q;
-    const int w = ufi(v.w);
-    q.key = ufu((uint32_t)v.x);
-    q.f = __int_as_float(ufi(v.y));
-    q.l = (w << 16) >> 16;
-    q.r = w >> 16;
+    q.key = ufu(k);
+    q.f = uff(f);
+    q.l = ufi(l);
+    q.r = ufi(r);
     return q;
   }
   __device__ __forceinline__ Quad quad_at(int x, int) const { return quad(x); }
   __device__ __forceinline__ void leaf(int x, int p) {
-    *(LAS int*)&a[x].l = -1;  // l = r = NIL
-    *(LAS int*)&b[x] = (RB_RED << 16) | (p & 0xffff);
+    s->lr[x].l = (int16_t)NIL;
+    s->lr[x].r = (int16_t)NIL;
+    s->p[x] = (int16_t)p;
+    sC(x, RB_RED);
   }
   __device__ __forceinline__ void payload(int x, uint32_t key, float f, float g, int prev) {
-    a[x].key = key;
-    a[x].f = f;
-    a[x].g = g;
-    (void)prev;  // pv[x] is stored by the caller after the expansion (see astar_loop_lds)
+    s->kf[x].key = key;
+    s->kf[x].f = f;
+    (void)g;     // pvg[x] = {prev, g} is stored by the caller after the expansion
+    (void)prev;  // (see astar_loop_lds)
   }
 };
 // ---- f-ordered index of the LDS tree -------------------------------------------------
@@ -303,7 +318,7 @@ __device__ __forceinline__ void rank2(const AStarLds& L, const Ring& rg, float v
   const int s_r = lane * SR;
   const bool h1 = s_r < n;
   const int i1 = (int)L.ring[(rg.head + s_r) & M] & M;  // unconditional loads, masked use
-  const float f1 = L.a[i1].f;
+  const float f1 = L.kf[i1].f;
   const int bA = __popcll(__ballot(h1 && f1 < vA)), bB = __popcll(__ballot(h1 && f1 < vB));
   const bool forA = lane < SR;
   const int bb = forA ? bA : bB;
@@ -311,7 +326,7 @@ __device__ __forceinline__ void rank2(const AStarLds& L, const Ring& rg, float v
   const int r2 = (bb - 1) * SR + sub;
   const bool h2 = lane < 2 * SR && bb > 0 && r2 < n;
   const int i2 = (int)L.ring[(rg.head + r2) & M] & M;
-  const float f2 = L.a[i2].f;
+  const float f2 = L.kf[i2].f;
   const uint64_t m2 = __ballot(h2 && f2 < (forA ? vA : vB));
   const int cA = __popcll(m2 & SMASK), cB = __popcll((m2 >> SR) & SMASK);
   // lanes of level 2 hold ranks base..base+SR-1; rank base+SR is level-1 sample lane b
@@ -379,7 +394,7 @@ __device__ __forceinline__ SameCell same_cell(const AStarLds& L, int used, uint3
   // all loads unconditional (in-bounds by construction) so they issue back to back
   uint32_t kk[A_CAP / 64];
 #pragma unroll
-  for (int q = 0; q < A_CAP / 64; ++q) kk[q] = L.a[lane + 64 * q].key;
+  for (int q = 0; q < A_CAP / 64; ++q) kk[q] = L.kf[lane + 64 * q].key;
   uint32_t m = 0;
 #pragma unroll
   for (int q = 0; q < A_CAP / 64; ++q) m |= (uint32_t)((lane + 64 * q < used) & (kk[q] == key)) << q;
@@ -401,7 +416,7 @@ __device__ __forceinline__ SameCell same_cell(const AStarLds& L, int used, uint3
   }
   sc.cnt = 1;
   sc.idx = ln + 64 * (__ffs(mm) - 1);
-  sc.f = uff(L.a[sc.idx].f);
+  sc.f = uff(L.kf[sc.idx].f);
   return sc;
 }
 
@@ -422,7 +437,8 @@ struct HbmAcc : AosAcc<Node2, GAS Node2*> {
 __device__ __forceinline__ void memoise(SearchCtx& c, float total, int from) {
   const PlannerDev& P = *c.P;
   const GAS Cell2* cells = gp(c.A->cell2);
-  for (int i = from; i != NIL;) {
+  const uint32_t NN = (uint32_t)P.N * (uint32_t)P.N;
+  for (int i = from; i != NIL && (uint32_t)i < NN;) {  // (the bound only guards a corrupted chain)
     const Cell2 r = gload(&cells[i]);
     GAS uint32_t* vw = &gp(P.visited)[(uint32_t)i >> 5];
     *vw = *vw | (1u << (i & 31));  // one wave owns the planner: a plain read-modify-write
@@ -584,8 +600,19 @@ __device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc>& tr, AStarL
 }
 
 __device__ __forceinline__ void free_lds(SearchCtx& c, RBT<LdsAcc>& tr, int x) {
-  tr.a[x].key = 0xffffffffu;  // dead: never matches a cell
+  tr.s->kf[x].key = 0xffffffffu;  // dead: never matches a cell
   tpool_free(tr, c.ps2, x);
+}
+
+// g of open node `hit` (the find result for neighbour k): a node inserted earlier in this
+// expansion (its {prev, g} store is still pending in the inserting lane), the g prefetched
+// for lane k's hinted node, or the node's HBM record.
+__device__ __forceinline__ float hit_g(const SearchCtx& c, int hit, int k, int hy, float hg, bool st_pv, int st_node,
+                                       float st_g) {
+  const uint64_t pend = __ballot(st_pv && st_node == hit);
+  if (pend) return rl_f(st_g, (int)__ffsll((unsigned long long)pend) - 1);
+  if (rl_i(hy, k) == hit) return rl_f(hg, k);  // not reused in this expansion (else pending)
+  return uff(__int_as_float(gp(c.A->prevl)[2 * (hit & (A_CAP - 1)) + 1]));
 }
 
 // AStar::a_star_search (AStar.cpp:118-186) on the LDS tree.  Returns false (without
@@ -598,16 +625,16 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
   GAS Cell2* cells = gp(A.cell2);
+  GAS int* pvg = gp(A.prevl);  // {prev, g bits} per LDS node
   while (rg.n > 0) {
     if (c.ps2.next + 8 > A_CAP) return false;
     STAMP_T t_pop = STAMP_NOW();
     const int b = tr.begin();
     const Quad top = tr.quad(b);
-    const float top_g = uff(tr.G(b));
     const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
     const uint32_t tcell = (uint32_t)tx * (uint32_t)P.N + (uint32_t)ty;
+    const v2i tpg = *(const GAS v2i*)&pvg[2 * (b & (A_CAP - 1))];  // the popped node's {prev, g}
     const Cell2 tc = gload(&cells[tcell]);
-    const int tprev = ufi(tr.PV(b));
     const int ni = tx + adx, nj = ty + ady;
     bool valid = false, vis = false, closed = false;
     float nf = 0.0f;
@@ -627,6 +654,16 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     // reuse has to wait on a store (vmcnt counts loads and stores in issue order)
     const uint64_t vmask = __ballot(valid), vismask = c.cost_only ? __ballot(vis) : 0ull, cmask = __ballot(closed);
     nf = __builtin_amdgcn_readfirstlane(0) + nf;  // keep nf live in a VGPR (no-op)
+    const int tprev = ufi(tpg.x);
+    const float top_g = uff(__int_as_float(tpg.y));
+    // g of this lane's hinted open node (the node a find of this cell usually returns): its
+    // load overlaps the erase below, and a node's g never changes while it is open
+    int hy = NIL;
+    float hg = 0.0f;
+    if (ohint != 0xffffffffu && !((ohint >> 16) & 1u)) {
+      hy = (int)(ohint & 0xffffu);
+      hg = __int_as_float(pvg[2 * (hy & (A_CAP - 1)) + 1]);
+    }
     tr.unlink(b);
     free_lds(c, tr, b);
     ring_erase(L, rg, 0, lane);
@@ -655,9 +692,9 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     // collected in lane k and issued together after the loop: a global store inside the
     // loop would make every later register reuse wait for its completion (vmcnt).
     uint32_t st_cell = 0, st_hint = 0;
-    float st_f = 0.0f;
+    float st_f = 0.0f, st_g = 0.0f;
     int st_node = NIL;
-    bool st_on = false;
+    bool st_on = false, st_pv = false;  // st_pv: pvg[st_node] = {ci, st_g} is still due
     for (int k = 0; k < nact; ++k) {
       if (!((vmask >> k) & 1ull)) continue;
       const float kcost = rl_f(acost, k);
@@ -666,7 +703,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
         if (st_on) {  // this expansion's earlier node-map writes happen before the return
           gp(P.nm_f)[st_cell] = st_f;
           if (st_node != NIL) {
-            gp(A.prevl)[st_node] = ci;
+            if (st_pv) *(GAS v2i*)&pvg[2 * (st_node & (A_CAP - 1))] = v2i{ci, __float_as_int(st_g)};
             cells[st_cell].oinfo = ((c.gen2 & CELL2_OGEN_MASK) << CELL2_OGEN_SHIFT) | st_hint;
           }
         }
@@ -694,7 +731,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
           sc = same_cell(L, c.ps2.next, key, lane);
         } else {
           const int y = (int)(hint & 0xffffu);
-          if (ufu(L.a[y].key) == key) sc = SameCell{1, y, uff(L.a[y].f)};
+          if (ufu(L.kf[y].key) == key) sc = SameCell{1, y, uff(L.kf[y].f)};
         }
       }
       RankOut ra, rb;
@@ -715,11 +752,13 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
           st_on = true;   // when the insert is dropped (AStar.cpp:172-183)
           st_cell = (uint32_t)ki * (uint32_t)P.N + (uint32_t)kj;
           st_f = fn;
+          st_g = gn;
           st_node = nn;
+          st_pv = nn != NIL;
           st_hint = nn == NIL ? ohint : ((uint32_t)nn | (uint32_t)(dup || sc.cnt > 0) << 16);
         }
         STAMP_ADD(10, t_i);
-      } else if (gn < tr.G(hit)) {
+      } else if (gn < hit_g(c, hit, k, hy, hg, st_pv, st_node, st_g)) {
         STAMP_T t_u = STAMP_NOW();
         if (hit_rank < 0) {
           const float hf = tr.F(hit);
@@ -730,6 +769,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
         tr.unlink(hit);
         free_lds(c, tr, hit);
         ring_erase(L, rg, hit_rank, lane);
+        if (st_node == hit) st_pv = false;  // a node inserted earlier in this expansion is gone
         STAMP_ADD(11, t_u);
         if (dup) sc = same_cell(L, c.ps2.next, key, lane);
         else if (hit == sc.idx) sc = SameCell{0, NIL, 0.0f};
@@ -741,7 +781,9 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
           st_on = true;
           st_cell = (uint32_t)ki * (uint32_t)P.N + (uint32_t)kj;
           st_f = fn;
+          st_g = gn;
           st_node = nn;
+          st_pv = nn != NIL;
           st_hint = nn == NIL ? ohint : ((uint32_t)nn | (uint32_t)(dup || sc.cnt > 0) << 16);
         }
       }
@@ -749,7 +791,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     if (st_on) {
       gp(P.nm_f)[st_cell] = st_f;
       if (st_node != NIL) {
-        gp(A.prevl)[st_node] = ci;
+        if (st_pv) *(GAS v2i*)&pvg[2 * (st_node & (A_CAP - 1))] = v2i{ci, __float_as_int(st_g)};
         cells[st_cell].oinfo = ((c.gen2 & CELL2_OGEN_MASK) << CELL2_OGEN_SHIFT) | st_hint;
       }
     }
@@ -774,18 +816,17 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   c.ps2.next = 1;
   c.ps2.free = NIL;
   RBT<LdsAcc> tl;
-  tl.a = lp(L.a);
-  tl.b = lp(L.b);
-  tl.pv = gp(A.prevl);
+  tl.s = lp(&L);
+  tl.lane = lane;
   tl.clear();
-  L.a[0].key = 0xffffffffu;
+  L.kf[0].key = 0xffffffffu;
   Ring rg{0, 0};
   {
     const SameCell none{0, NIL, 0.0f};
     const RankOut at0{0, NIL, 0.0f, NIL};
     int n0;
     insert_lds(c, tl, L, rg, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL, none, at0, &n0);
-    gp(A.prevl)[n0] = NIL;
+    *(GAS v2i*)&gp(A.prevl)[2 * n0] = v2i{NIL, __float_as_int(0.0f)};  // {prev, g} of the start
     gp(A.cell2)[s_cell].oinfo = ((c.gen2 & CELL2_OGEN_MASK) << CELL2_OGEN_SHIFT) | (uint32_t)n0;
   }
   wave_lds_sync();
@@ -806,14 +847,15 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   GAS Node2* o2 = gp(A.open2);
   for (int i = lane; i < c.ps2.next; i += 64) {
     Node2 n;
-    n.key = L.a[i].key;
-    n.f = L.a[i].f;
-    n.g = L.a[i].g;
-    n.l = L.a[i].l;
-    n.r = L.a[i].r;
-    n.p = L.b[i].p;
-    n.color = L.b[i].color;
-    n.prev = gp(A.prevl)[i];
+    const v2i pg = *(const GAS v2i*)&gp(A.prevl)[2 * i];
+    n.key = L.kf[i].key;
+    n.f = L.kf[i].f;
+    n.g = __int_as_float(pg.y);
+    n.l = L.lr[i].l;
+    n.r = L.lr[i].r;
+    n.p = L.p[i];
+    n.color = (int)((L.black[i >> 5] >> (i & 31)) & 1u);
+    n.prev = pg.x;
     gstore(&o2[i], n);
   }
   wave_lds_sync();
@@ -1396,7 +1438,7 @@ __global__ __launch_bounds__(64) void k_astar_query(const PlannerDev* __restrict
     // the predecessor chain of the goal's closed record (cell indices)
     int cur = cells[goal].prev;
     while (cur != NIL) {
-      if (n >= cap) {
+      if (n >= cap || cur < 0 || cur >= Pd.N * Pd.N) {
         n = -1;
         break;
       }

@@ -213,7 +213,7 @@ struct SlotArena {
   uint32_t* gens;   // [0] closed-set generation, [1] A* closed generation
   float* dub_xyh; float* dub_curv; int dub_cap; int pad5;
   int* out_chain;   int chain_cap;   int pad6;
-  int* prevl;       // prev links of the LDS-resident A* tree nodes (A_CAP)
+  int* prevl;       // {prev link, g bits} of the LDS-resident A* tree nodes (2 x A_CAP)
 };
 
 // Scratch of one planner in the RELAXED (non-parity) search mode (hastar_relaxed.hip,
