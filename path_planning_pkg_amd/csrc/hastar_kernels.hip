@@ -195,10 +195,10 @@ struct AStarLds {
   NodeKF kf[A_CAP];
   LinkLR lr[A_CAP];
   int16_t p[A_CAP];
-  uint32_t black[A_CAP / 32];    // colour bits (1 = black)
   int16_t ring[A_CAP];  // live node indices in f order (a ring: rank r at ring[(head + r) % A_CAP])
 };
-static_assert(sizeof(AStarLds) == 16 * A_CAP + A_CAP / 8, "LDS node layout");
+static_assert(sizeof(AStarLds) == 16 * A_CAP, "LDS node layout");
+static_assert(A_CAP <= 64 * 32, "one colour VGPR holds 32 nodes per lane");
 
 #define LAS __attribute__((address_space(3)))
 template <class T>
@@ -206,28 +206,29 @@ __device__ __forceinline__ LAS T* lp(T* p) {
   return (LAS T*)p;
 }
 
-// the compact LDS layout for RBT<>; g and prev (HBM) are read by the search loop itself
+// the compact LDS layout for RBT<>; g and prev (HBM) are read by the search loop itself.
+// The colours are bits of one VGPR (lane j: nodes 32 j .. 32 j + 31, 1 = black): a colour
+// read is one v_readlane, a colour write one masked VALU update, no LDS round trip.
 struct LdsAcc {
   static constexpr bool kPathWalk = false;
   LAS AStarLds* s;
   int lane;
+  uint32_t cb;
   // every field is accessed through its own type (no type punning: with strict aliasing a
   // 16-bit store through an int* view would not be ordered against int loads)
   __device__ __forceinline__ int L(int x) const { return ufi(s->lr[x].l); }
   __device__ __forceinline__ int R(int x) const { return ufi(s->lr[x].r); }
   __device__ __forceinline__ int P(int x) const { return ufi(s->p[x]); }
-  __device__ __forceinline__ int C(int x) const { return ufi((int)((s->black[x >> 5] >> (x & 31)) & 1u)); }
+  __device__ __forceinline__ int C(int x) const {
+    return (int)(((uint32_t)__builtin_amdgcn_readlane((int)cb, x >> 5) >> (x & 31)) & 1u);
+  }
   __device__ __forceinline__ void sL(int x, int v) { s->lr[x].l = (int16_t)v; }
   __device__ __forceinline__ void sR(int x, int v) { s->lr[x].r = (int16_t)v; }
   __device__ __forceinline__ void sP(int x, int v) { s->p[x] = (int16_t)v; }
-  // one lane updates the colour word (LDS atomics, no return value: nothing waits on them;
-  // the wave's later LDS reads are ordered after them)
   __device__ __forceinline__ void sC(int x, int v) {
     const uint32_t bit = 1u << (x & 31);
-    if (lane == 0) {
-      if (v == RB_BLACK) __hip_atomic_fetch_or(&s->black[x >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      else __hip_atomic_fetch_and(&s->black[x >> 5], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    const uint32_t nw = v == RB_BLACK ? (cb | bit) : (cb & ~bit);
+    cb = lane == (x >> 5) ? nw : cb;
   }
   __device__ __forceinline__ uint32_t K(int x) const { return ufu(s->kf[x].key); }
   __device__ __forceinline__ float F(int x) const { return uff(s->kf[x].f); }
@@ -818,6 +819,7 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   RBT<LdsAcc> tl;
   tl.s = lp(&L);
   tl.lane = lane;
+  tl.cb = 0;
   tl.clear();
   L.kf[0].key = 0xffffffffu;
   Ring rg{0, 0};
@@ -854,7 +856,7 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
     n.l = L.lr[i].l;
     n.r = L.lr[i].r;
     n.p = L.p[i];
-    n.color = (int)((L.black[i >> 5] >> (i & 31)) & 1u);
+    n.color = (int)(((uint32_t)__shfl((int)tl.cb, i >> 5, 64) >> (i & 31)) & 1u);
     n.prev = pg.x;
     gstore(&o2[i], n);
   }
