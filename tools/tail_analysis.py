@@ -45,7 +45,16 @@ for step in range(a.steps):
         cyc = np.array([planners[i].cycles()[6] for i in range(len(planners))], dtype=np.float64)
         mhz = cyc / np.maximum(dur * 1e3, 1e-9)  # cycles per us
         long_ix = np.argsort(-dur)[:16]
-        clock = {"longest_mhz": float(mhz[li]), "top16_mhz_mean": float(mhz[long_ix].mean()),
+        cl = planners[li].cycles()
+        pops = float(r.stats["pops"][li])
+        names = {0: "pop", 1: "expand", 2: "bookkeeping(incl A*)", 3: "astar", 4: "shot", 7: "astar_hbm",
+                 13: "find3", 14: "insert3", 16: "succ_gen", 17: "apf", 18: "dubins", 19: "insert_walk",
+                 20: "insert_link", 21: "probe_wait"}
+        longest_phases = {n: round(cl[i] / max(pops, 1)) for i, n in names.items()}
+        longest_phases.update(loop_per_pop=round(cl[6] / max(pops, 1)), fills_per_pop=cl[22] / max(pops, 1),
+                              cycles_per_fill=cl[26] / max(cl[22], 1))
+        clock = {"longest_phases_per_pop": longest_phases,
+                 "longest_mhz": float(mhz[li]), "top16_mhz_mean": float(mhz[long_ix].mean()),
                  "median_mhz_over_searches_gt_1ms": float(np.median(mhz[dur > 1.0]))}
     print(json.dumps({"clock": clock, "step": step, "kernel_ms": r.kernel_ms, "span_ms": span, "slots_used": slots,
                       "sum_dur_ms": float(dur.sum()), "ideal_ms": float(dur.sum() / slots),
