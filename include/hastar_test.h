@@ -36,6 +36,8 @@ int hastar_debug_astar_modes(hastar_handle h, long long* out2);
 int hastar_debug_timing(hastar_handle h, unsigned long long* out3);
 /* Search-slot pool of the handle's device: {resident wavefronts, search waves per CU, arenas, MiB per arena}. */
 int hastar_debug_slots(hastar_handle h, long long* out4);
+/* resume arenas carved from idle slot arenas of the pool so far (process-wide count) */
+int hastar_debug_pooled_resumes(long long* out);
 /* The relaxed kernel's per-wave progress words (4 per wave: phase, round, expansion-set size,
  * expansion index; workgroup b, wave w at [(b * 8 + w) * 4]) in pinned host memory, readable
  * while a launch runs; null unless HASTAR_RELAXED_PROGRESS was set before the first relaxed call. */

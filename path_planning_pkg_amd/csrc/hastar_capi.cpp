@@ -215,10 +215,12 @@ struct DeviceCtx {
 
 // A larger arena that continues one parked search (hastar_find_path_batch).
 struct ResumeArena {
-  void* slab = nullptr;
+  void* slab = nullptr;  // own allocation (nullptr: carved from idle slot arenas of the pool)
   SlotArena desc{};
   int planner = -1;
+  int pool_first = -1, pool_count = 0;  // pool arenas [first, first + count) it occupies
 };
+long long g_pooled_resumes = 0;  // resume arenas carved from the slot pool (diagnostics)
 DeviceCtx g_dev[64];
 
 template <class T>
@@ -1646,6 +1648,9 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   // planners no wave took run in a new queue pass: until every search has ended.
   {
     std::vector<char> in_resume(n, 0);      // 1: the planner's last launch was a resume launch
+    std::vector<int> pool_used;             // {first, count} of pool arenas lent to resume arenas
+    const char* rp_env = std::getenv("HASTAR_RESUME_POOL");
+    const bool pool_first = rp_env && std::atoi(rp_env) != 0;
     std::vector<ResumeArena> cur, nxt;      // resume arenas of the last resume launch, by index
     std::vector<int> notrun, parked;
     for (;;) {
@@ -1657,8 +1662,34 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
         else if (stt == SEARCH_PARKED) parked.push_back(i);
       }
       if (notrun.empty() && parked.empty()) break;
-      // 1. move every parked search into an arena 4x its current outer capacity
+      // 1. move every parked search into an arena 4x its current outer capacity: its own
+      // allocation, or (when that fails, or HASTAR_RESUME_POOL=1 asks for it first) idle slot
+      // arenas of the pool, as long as no queue pass needs them in this round.  Pool arenas
+      // that hold a parked state (or a live resume arena) are not idle.
       nxt.clear();
+      std::vector<char> pool_busy((size_t)DC.n_arenas, 0);
+      for (int i : parked)
+        if (!in_resume[i] && DC.h_results[i].park_arena >= 0 && DC.h_results[i].park_arena < DC.n_arenas)
+          pool_busy[(size_t)DC.h_results[i].park_arena] = 1;
+      for (const ResumeArena& ra : cur)
+        for (int q = 0; q < ra.pool_count; ++q) pool_busy[(size_t)(ra.pool_first + q)] = 1;
+      auto carve_from_pool = [&](size_t bytes, ResumeArena& ra) -> bool {
+        if (!notrun.empty() || DC.arena_bytes == 0) return false;
+        const int k = (int)((bytes + DC.arena_bytes - 1) / DC.arena_bytes);
+        for (int j = 0, run = 0; j < DC.n_arenas; ++j) {
+          run = pool_busy[(size_t)j] ? 0 : run + 1;
+          if (run == k) {
+            ra.pool_first = j - k + 1;
+            ra.pool_count = k;
+            for (int q = ra.pool_first; q <= j; ++q) pool_busy[(size_t)q] = 1;
+            pool_used.push_back(ra.pool_first);
+            pool_used.push_back(k);
+            ++g_pooled_resumes;
+            return true;
+          }
+        }
+        return false;
+      };
       for (int i : parked) {
         const SearchResult& R = DC.h_results[i];
         const SlotArena* from = nullptr;
@@ -1678,16 +1709,28 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
         size_outer(r, pops, hs[i]->span);
         ResumeArena ra;
         const size_t bytes = arena_layout(r).total();
-        if (pops <= was || hipMalloc(&ra.slab, bytes) != hipSuccess) {
+        bool have = false;
+        if (pops > was) {
+          if (pool_first) have = carve_from_pool(bytes, ra);
+          if (!have) {
+            have = hipMalloc(&ra.slab, bytes) == hipSuccess;
+            if (!have) {
+              ra.slab = nullptr;
+              have = carve_from_pool(bytes, ra);
+            }
+          }
+        }
+        if (!have) {
           // no larger arena can be had: this search ends here, reported as an overflow
-          if (ra.slab) hipFree(ra.slab);
           DC.h_results[i].status = HASTAR_EOVERFLOW;
           DC.h_results[i].ok = 0;
           DC.h_results[i].path_len = 0;
           HIPCHK(hipMemcpyAsync(DC.d_results + i, DC.h_results + i, sizeof(SearchResult), hipMemcpyHostToDevice, st));
           continue;
         }
-        HIPCHK(carve_arena(static_cast<char*>(ra.slab), r, arena_layout(r), &ra.desc, st));
+        char* where = ra.slab ? static_cast<char*>(ra.slab)
+                              : static_cast<char*>(DC.slab) + DC.arena_bytes * (size_t)ra.pool_first;
+        HIPCHK(carve_arena(where, r, arena_layout(r), &ra.desc, st));
         HIPCHK(hipMemcpyAsync(ra.desc.open3, from->open3, (size_t)R.ps3_next * sizeof(Node3), hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpyAsync(ra.desc.closed3, from->closed3, (size_t)R.n_closed3 * sizeof(Closed3),
                               hipMemcpyDeviceToDevice, st));
@@ -1695,7 +1738,8 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
         nxt.push_back(ra);
       }
       HIPCHK(hipStreamSynchronize(st));
-      for (ResumeArena& ra : cur) hipFree(ra.slab);  // their states have been copied out
+      for (ResumeArena& ra : cur)
+        if (ra.slab) hipFree(ra.slab);  // their states have been copied out
       cur.swap(nxt);
       // 2. planners no wave took: a new queue pass over the slot arenas (free again)
       if (!notrun.empty()) {
@@ -1734,7 +1778,19 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
         break;
       }
     }
-    for (ResumeArena& ra : cur) hipFree(ra.slab);
+    for (ResumeArena& ra : cur)
+      if (ra.slab) hipFree(ra.slab);
+    // pool arenas lent to resume arenas get their generation-stamped tables back to a fresh
+    // arena's state (same layout, so the device descriptors stay valid)
+    if (!pool_used.empty()) {
+      const ArenaLayout lay = arena_layout(DC.areq);
+      for (size_t u = 0; u < pool_used.size(); u += 2)
+        for (int q = pool_used[u]; q < pool_used[u] + pool_used[u + 1]; ++q) {
+          SlotArena tmp;
+          HIPCHK(carve_arena(static_cast<char*>(DC.slab) + DC.arena_bytes * (size_t)q, DC.areq, lay, &tmp, st));
+        }
+      HIPCHK(hipStreamSynchronize(st));
+    }
   }
   g_last_ms = ms_total;
   return finish_batch(DC, hs, n, xyh, curv, cap, len, cost, ok, stats, true);
@@ -2394,6 +2450,12 @@ int hastar_debug_timing(hastar_handle h, unsigned long long* out3) {
 
 // Search-slot pool of the handle's device: {resident wavefronts (occupancy x CUs), search
 // waves per CU, arenas in the pool, MiB per arena}.
+int hastar_debug_pooled_resumes(long long* out) {
+  if (!out) return fail(HASTAR_EINVAL, "null output");
+  *out = g_pooled_resumes;
+  return HASTAR_OK;
+}
+
 int hastar_debug_slots(hastar_handle h, long long* out4) {
   if (!h || !h->dc) return fail(HASTAR_EINVAL, "bad handle");
   const DeviceCtx& D = *h->dc;

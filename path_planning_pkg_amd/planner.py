@@ -80,6 +80,7 @@ def load_library():
     L.hastar_debug_astar_modes.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_timing.argtypes = [vp, C.POINTER(C.c_ulonglong)]
     L.hastar_debug_slots.argtypes = [vp, C.POINTER(C.c_longlong)]
+    L.hastar_debug_pooled_resumes.argtypes = [C.POINTER(C.c_longlong)]
     L.hastar_velocity_profile_batch.argtypes = [C.c_int, C.POINTER(HastarVelocityParams), C.c_int,
                                                 C.POINTER(C.c_longlong), fp, fp, fp, fp, C.POINTER(C.c_ubyte), fp,
                                                 C.POINTER(C.c_ubyte)]
@@ -365,6 +366,13 @@ class HybridAStar:
         out = (C.c_longlong * 2)()
         _check(load_library().hastar_debug_astar_modes(self.h, out))
         return {"migrations": out[0], "astar_pops_hbm": out[1]}
+
+    @staticmethod
+    def pooled_resumes():
+        """Resume arenas carved from idle slot arenas so far (process-wide)."""
+        out = C.c_longlong(0)
+        _check(load_library().hastar_debug_pooled_resumes(C.byref(out)))
+        return out.value
 
     def slots(self):
         """Search-slot pool of this planner's device (after a find_path)."""

@@ -71,6 +71,32 @@ def test_park_resume_with_fewer_slots(gpu, oracle_lib, monkeypatch):
     assert sum(r["stats"]["parks"] for r in res) > 0
 
 
+def test_resume_arenas_carved_from_the_pool(gpu, oracle_lib, monkeypatch):
+    """Resume arenas taken from idle slot arenas of the pool (what happens when a resume
+    arena cannot be allocated; HASTAR_RESUME_POOL=1 makes it the first choice).  The parked
+    searches must still end with the oracle's results, and the lent pool arenas must come
+    back as fresh ones: a second batch on the same pool is checked too."""
+    monkeypatch.setenv("HASTAR_RESUME_POOL", "1")
+    cases = [synthetic(128, 36, 6, s) for s in (41, 42, 43, 44, 45)]
+    gs, os_ = [], []
+    for cfg, proto in cases:
+        cfg.values["max_pops"] = 64
+        g, o = _pair(gpu, oracle_lib, cfg, proto)
+        gs.append(g)
+        os_.append(o)
+    before = gpu.HybridAStar.pooled_resumes()
+    for rep in range(2):
+        for g in gs:
+            g.reset()
+        for o in os_:
+            o.reset()
+        res, _ = gpu.find_path_batch(gs, [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases])
+        for i, ((cfg, proto), o) in enumerate(zip(cases, os_)):
+            compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"pooled resume, rep {rep}, planner {i}")
+        assert sum(r["stats"]["parks"] for r in res) > 0
+    assert gpu.HybridAStar.pooled_resumes() > before, "no resume arena was carved from the pool"
+
+
 def test_statuses_reported_per_planner(gpu, oracle_lib, monkeypatch):
     """One batch, two outcomes: planner 0 exceeds an explicit pop budget
     (HASTAR_MAX_POPS_HARD -> HASTAR_EOVERFLOW, a failed search), planner 1 finishes with a
