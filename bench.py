@@ -152,7 +152,10 @@ def parse_args(argv=None):
         # A search that outgrows its arena parks and resumes in a 4x one, so this is no limit.
         args.max_pops = 196608 if args.workload == "cfg3" else 0
     if args.workload == "cfg4" and "--batch" not in sys.argv and "HASTAR_BENCH_BATCH" not in os.environ:
-        args.batch = 6144  # 2048^2 maps: 32 MiB per planner; the arena pool takes the rest of the HBM
+        # 2048^2 maps: 32 MiB per planner.  The step is bound by the batch's longest search (597k
+        # pops), so planners are worth more than arenas: 7680 planners leave ~360 arenas of 107 MiB,
+        # which finish the rest of the batch in ~65 % of the step (profiles/r02w_cfg4_*).
+        args.batch = 7680
     return args
 
 

@@ -221,6 +221,7 @@ struct ResumeArena {
   int pool_first = -1, pool_count = 0;  // pool arenas [first, first + count) it occupies
 };
 long long g_pooled_resumes = 0;  // resume arenas carved from the slot pool (diagnostics)
+constexpr size_t kHeadroom = (size_t)2 << 30;  // HBM the arena pool and resume arenas leave free
 DeviceCtx g_dev[64];
 
 template <class T>
@@ -401,6 +402,9 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
     double frac = 0.8;
     if (const char* e = std::getenv("HASTAR_ARENA_FRAC")) frac = std::min(0.97, std::max(0.05, std::atof(e)));
     budget = (size_t)((double)fr * frac);
+    // leave kHeadroom free for the runtime (code objects loaded at a kernel's first launch,
+    // staging) and for the batch buffers
+    budget = std::min(budget, fr > kHeadroom ? fr - kHeadroom : (size_t)0);
   }
   const int n_want = n;
   n = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, budget / per));
@@ -1712,6 +1716,9 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
         bool have = false;
         if (pops > was) {
           if (pool_first) have = carve_from_pool(bytes, ra);
+          size_t fr = 0, tot = 0;
+          if (!have && hipMemGetInfo(&fr, &tot) == hipSuccess && fr < bytes + kHeadroom)
+            have = carve_from_pool(bytes, ra);  // an allocation would eat the runtime's headroom
           if (!have) {
             have = hipMalloc(&ra.slab, bytes) == hipSuccess;
             if (!have) {
