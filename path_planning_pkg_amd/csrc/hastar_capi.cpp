@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <unordered_map>
 #include <numeric>
@@ -220,7 +221,7 @@ struct ResumeArena {
   int planner = -1;
   int pool_first = -1, pool_count = 0;  // pool arenas [first, first + count) it occupies
 };
-long long g_pooled_resumes = 0;  // resume arenas carved from the slot pool (diagnostics)
+std::atomic<long long> g_pooled_resumes{0};  // resume arenas carved from the slot pool (diagnostics)
 constexpr size_t kHeadroom = (size_t)2 << 30;  // HBM the arena pool and resume arenas leave free
 DeviceCtx g_dev[64];
 
@@ -2459,7 +2460,7 @@ int hastar_debug_timing(hastar_handle h, unsigned long long* out3) {
 // waves per CU, arenas in the pool, MiB per arena}.
 int hastar_debug_pooled_resumes(long long* out) {
   if (!out) return fail(HASTAR_EINVAL, "null output");
-  *out = g_pooled_resumes;
+  *out = g_pooled_resumes.load();
   return HASTAR_OK;
 }
 
