@@ -76,7 +76,8 @@ typedef struct hastar_stats {
   unsigned long long closed_digest; /* order-independent digest of the closed-set keys */
   int via_shot;                /* success came from an analytic Dubins shot */
   int status;                  /* this planner's outcome: 0, HASTAR_EOVERFLOW (HASTAR_MAX_POPS_HARD
-                                  budget or device memory exhausted), HASTAR_ENOSPC (path longer
+                                  budget, or no larger arena could be allocated nor lent by idle
+                                  slot arenas of the pool), HASTAR_ENOSPC (path longer
                                   than the caller's cap: *len is the length needed) */
   int parks;                   /* times the search outgrew its arena and was resumed in a larger one */
   int pad;
