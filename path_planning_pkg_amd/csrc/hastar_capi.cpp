@@ -1669,17 +1669,20 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
       if (notrun.empty() && parked.empty()) break;
       // 1. move every parked search into an arena 4x its current outer capacity: its own
       // allocation, or (when that fails, or HASTAR_RESUME_POOL=1 asks for it first) idle slot
-      // arenas of the pool, as long as no queue pass needs them in this round.  Pool arenas
-      // that hold a parked state (or a live resume arena) are not idle.
+      // arenas of the pool.  Not idle: the arenas this round's queue pass will use (the first
+      // min(slots, not-run planners)), those that hold a parked state, and those lent to a live
+      // resume arena.
       nxt.clear();
       std::vector<char> pool_busy((size_t)DC.n_arenas, 0);
+      const int wq = notrun.empty() ? 0 : std::min<int>(slots, (int)notrun.size());
+      for (int q = 0; q < wq && q < DC.n_arenas; ++q) pool_busy[(size_t)q] = 1;
       for (int i : parked)
         if (!in_resume[i] && DC.h_results[i].park_arena >= 0 && DC.h_results[i].park_arena < DC.n_arenas)
           pool_busy[(size_t)DC.h_results[i].park_arena] = 1;
       for (const ResumeArena& ra : cur)
         for (int q = 0; q < ra.pool_count; ++q) pool_busy[(size_t)(ra.pool_first + q)] = 1;
       auto carve_from_pool = [&](size_t bytes, ResumeArena& ra) -> bool {
-        if (!notrun.empty() || DC.arena_bytes == 0) return false;
+        if (DC.arena_bytes == 0) return false;
         const int k = (int)((bytes + DC.arena_bytes - 1) / DC.arena_bytes);
         for (int j = 0, run = 0; j < DC.n_arenas; ++j) {
           run = pool_busy[(size_t)j] ? 0 : run + 1;

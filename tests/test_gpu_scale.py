@@ -71,12 +71,16 @@ def test_park_resume_with_fewer_slots(gpu, oracle_lib, monkeypatch):
     assert sum(r["stats"]["parks"] for r in res) > 0
 
 
-def test_resume_arenas_carved_from_the_pool(gpu, oracle_lib, monkeypatch):
+@pytest.mark.parametrize("slots", [None, "2"])
+def test_resume_arenas_carved_from_the_pool(gpu, oracle_lib, monkeypatch, slots):
     """Resume arenas taken from idle slot arenas of the pool (what happens when a resume
     arena cannot be allocated; HASTAR_RESUME_POOL=1 makes it the first choice).  The parked
     searches must still end with the oracle's results, and the lent pool arenas must come
-    back as fresh ones: a second batch on the same pool is checked too."""
+    back as fresh ones: a second batch on the same pool is checked too.  With 2 slots the
+    host also re-queues planners no wave took, beside resume arenas lent from the pool."""
     monkeypatch.setenv("HASTAR_RESUME_POOL", "1")
+    if slots:
+        monkeypatch.setenv("HASTAR_SLOTS", slots)
     cases = [synthetic(128, 36, 6, s) for s in (41, 42, 43, 44, 45)]
     gs, os_ = [], []
     for cfg, proto in cases:
