@@ -1,0 +1,47 @@
+"""Host-side logic of bench.py (no GPU): workload defaults and the step-balance summary.
+
+bench.py's cfg3 default arena size (196,608 pops) must cover the batch's longest search
+(query 2395: 172,207 pops in the oracle census, profiles/census_cfg3_mt19937_r02.csv), or that
+search would park and resume after the rest of the batch; cfg4 fills the HBM with 7680
+planners (its step is bound by one 597k-pop search).
+"""
+import csv
+from pathlib import Path
+
+import bench
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_workload_defaults():
+    a = bench.parse_args([])
+    assert a.workload == "cfg3" and a.grid == 1024 and a.batch == 23552 and a.max_pops == 196608
+    c4 = bench.parse_args(["--workload", "cfg4"])
+    assert c4.grid == 2048 and c4.max_pops == 0
+    assert bench.parse_args(["--max-pops", "0"]).max_pops == 0  # the library's default arena
+
+
+def test_cfg3_arena_covers_the_longest_search():
+    with open(ROOT / "profiles" / "census_cfg3_mt19937_r02.csv") as f:
+        pops = [int(r["pops"]) for r in csv.DictReader(f)]
+    assert len(pops) == 23552
+    assert max(pops) < bench.parse_args([]).max_pops
+
+
+class _Planner:
+    def __init__(self, t0, t1, slot):
+        self._t = (t0, t1, slot)
+
+    def timing(self):
+        return self._t
+
+
+def test_step_balance():
+    # two slots; slot 0 runs a 3-ms search and a 1-ms one, slot 1 one 2-ms search (10 ns ticks)
+    ps = [_Planner(0, 300000, 0), _Planner(300000, 400000, 0), _Planner(50000, 250000, 1)]
+    b = bench.step_balance(ps)
+    assert b["slots_used"] == 2
+    assert abs(b["span_ms"] - 4.0) < 1e-9
+    assert abs(b["slot_busy_mean_ms"] - 3.0) < 1e-9
+    assert abs(b["busy_frac"] - 0.75) < 1e-9
+    assert abs(b["longest_search_under_load_ms"] - 3.0) < 1e-9 and b["longest_search_start_ms"] == 0.0
