@@ -59,10 +59,24 @@ def step_balance(planners):
             "longest_search_start_ms": float((t[li, 0] - t[:, 0].min()) * 1e-5)}
 
 
-def shard_query_ids(rank, world, batch):
-    """Queries of one rank: weak scaling, B per GPU, disjoint across ranks, no exchange."""
+def shard_query_ids(rank, world, batch, pred=None):
+    """Queries of one rank: weak scaling, B per GPU, disjoint across ranks, no exchange.  The
+    global queries 0 .. world * B - 1 are dealt by predicted cost (`pred`, one value per global
+    query, larger = costlier; every rank computes the same values from the inputs alone): sorted
+    costliest first, then dealt in snake order (0, 1, .., W-1, W-1, .., 0, ...), so every rank
+    gets the same number of queries and a like share of the predicted-long ones, and no rank's
+    block collects the tail.  Each rank's ids come back costliest-predicted first, which is also
+    the longest-first order of a batch with no history.  pred None: contiguous blocks."""
     assert 0 <= rank < world
-    return [rank * batch + i for i in range(batch)]
+    if pred is None:
+        return [rank * batch + i for i in range(batch)]
+    pred = np.asarray(pred, np.float64)
+    assert len(pred) == world * batch
+    order = np.argsort(-pred, kind="stable")
+    pos = np.arange(world * batch)
+    rnd, k = pos // world, pos % world
+    owner = np.where(rnd % 2 == 0, k, world - 1 - k)
+    return [int(q) for q in order[owner == rank]]
 
 
 def shard_global_ids(rank, world, total):
@@ -140,6 +154,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-relaxed", action="store_true", help="cfg5: skip the relaxed-mode comparison")
     ap.add_argument("--relaxed-batch", type=int, default=4096,
                     help="cfg3/cfg4: queries of the batch also planned in one relaxed call (query rate)")
+    ap.add_argument("--no-deal", action="store_true",
+                    help="cfg3/cfg4: contiguous query blocks per rank instead of the predicted-cost deal")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: exercises the launcher, sharding and reductions only (CPU rehearsal)")
@@ -187,7 +203,15 @@ def main():
         return run_cfg5(args, gpu, dist, torch, rank, world, device)
     B = args.batch
     map_build = map_build_phase(args, gpu, dist, torch, rank, world, device) if args.workload == "cfg4" else None
-    qids = shard_query_ids(rank, world, B)
+    # every rank derives the same predicted costs of all world * B queries from their inputs
+    # (no exchange); the deal balances predicted cost and orders each rank's batch by it
+    t_pred = time.perf_counter()
+    pred = None
+    if args.generator == "mt19937" and not args.no_deal:
+        from tests.scenarios import predicted_cost
+        pred = predicted_cost(args.grid, args.obstacles, np.arange(world * B))
+    t_pred = time.perf_counter() - t_pred
+    qids = shard_query_ids(rank, world, B, pred)
     t_gen = time.perf_counter()
     cfgs = [query_case(args, q) for q in qids]
     t_gen = time.perf_counter() - t_gen
@@ -244,7 +268,10 @@ def main():
         balance = step_balance(planners)  # before any other find_path overwrites the timings
         balance["pool"] = planners[0].slots()
         vel_prof = velocity_profile_phase(gpu, last, device, vels)  # before any other find_path
-        lat_ids = list(range(min(args.latency_queries, B)))
+        # latency queries: the survey's first seeds (query ids 0, 1, ..) where this rank has them
+        pos = {q: i for i, q in enumerate(qids)}
+        lat_ids = [pos[q] for q in range(args.latency_queries) if q in pos]
+        lat_ids += [i for i in range(B) if i not in lat_ids][:max(0, min(args.latency_queries, B) - len(lat_ids))]
         lat = []
         for i in lat_ids:  # single-query plan latency (the second half of the metric)
             planners[i].reset()
@@ -262,7 +289,10 @@ def main():
         if pmc.exists():
             try:
                 pm = json.loads(pmc.read_text())
-                if pm.get("batch") == B and pm.get("grid") == args.grid:
+                # only for the kernel it was measured on (sources hash), else traffic = null
+                from path_planning_pkg_amd.buildinfo import search_kernel_hash
+                if (pm.get("batch") == B and pm.get("grid") == args.grid
+                        and pm.get("kernel_src_sha") == search_kernel_hash()):
                     traffic = pm.get("hbm_bytes_per_launch")
             except (ValueError, OSError):
                 traffic = None
@@ -299,7 +329,9 @@ def main():
             "search_status": sorted(statuses),
             "parks_per_step": parks / args.steps,
             "setup_s_per_gpu": t_setup,
-            "setup_split_s": dict(setup_split, inputs_generated_s=t_gen),
+            "setup_split_s": dict(setup_split, inputs_generated_s=t_gen, cost_prediction_s=t_pred),
+            "query_deal": "predicted-cost snake deal (tests/scenarios.py:predicted_cost)" if pred is not None
+                          else "contiguous blocks",
             "roofline": {"bound": "latency", "roof": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                          "kernel": "hastar_search_kernel", "kernel_ms": avg_kernel_ms,
@@ -312,7 +344,10 @@ def main():
         out["velocity_profile"] = vel_prof
         out["relaxed_mode"] = relaxed
         if not args.no_cpu_baseline:
-            cb = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps, lat_ids)
+            # the CPU sample runs the rank's queries in query-id order (a representative sample,
+            # not the predicted-costliest head of the GPU batch), latency queries first
+            sample = lat_ids + [i for i in np.argsort(qids, kind="stable") if i not in lat_ids]
+            cb = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps, lat_ids, sample)
             out["cpu_baseline"] = cb
             out["plan_latency_ms"]["cpu_same_queries_median"] = cb.pop("latency_same_queries_ms", None)
     if dist:
@@ -638,41 +673,56 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
 
 
 def cpu_baseline_cfg5(pairs, budget_s, ticks):
-    """The oracle replaying the same pairs' replan loops (1 thread per pair, find_path timed
-    only): a tick's pairs are independent, so the CPU's tick takes as long as its slowest pair
-    when it has a core per pair; reported as the single-thread rate and that tick time."""
+    """The oracle replaying the same pairs' replan loops on `cpu_threads()` host threads, one
+    private planner per thread (find_path timed only; ctypes calls release the GIL).  Pairs are
+    taken in order, one thread per pair, in rounds of T pairs until the rounds' parallel wall time
+    reaches the budget.  value = pops / parallel find_path wall.  A tick's pairs are independent,
+    so with a core per pair the CPU's tick takes as long as its slowest pair
+    (tick_ms_one_core_per_pair)."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle.pyoracle import OraclePlanner
     from tests.scenarios import drive, replan_tick, replan_tick_inputs
-    pops, wall, n = 0, 0.0, 0
-    tick_max = np.zeros(ticks)
-    for cfg, proto, v in pairs:
+    T = cpu_threads()
+
+    def run_pair(pv):
+        cfg, proto, v = pv
         o = OraclePlanner(cfg)
         drive(o, proto)
+        ms, pops = [], 0
         for t in range(ticks):
             r = o.find_path(proto["vel"], replan_tick_inputs(proto, v, t)[0])
             pops += r["stats"]["pops"]
-            wall += r["wall_ms"] * 1e-3
-            tick_max[t] = max(tick_max[t], r["wall_ms"])
+            ms.append(r["wall_ms"])
             replan_tick(o, proto, v, t)
         o.close()
-        n += 1
-        if wall >= budget_s:
-            break
-    return {"value": pops / wall if wall > 0 else None, "unit": "expansions/s", "cores": 1, "kind": "port",
+        return pops, ms
+
+    pops, wall, n = 0, 0.0, 0
+    tick_max = np.zeros(ticks)
+    with ThreadPoolExecutor(T) as ex:
+        while n < len(pairs) and wall < budget_s:
+            rnd = list(ex.map(run_pair, pairs[n:n + T]))
+            # the round's find_path time on T cores: its slowest pair's summed find_path time
+            wall += max(sum(ms) for _, ms in rnd) * 1e-3
+            for p, ms in rnd:
+                pops += p
+                tick_max = np.maximum(tick_max, ms)
+            n += len(rnd)
+    return {"value": pops / wall if wall > 0 else None, "unit": "expansions/s", "cores": T, "kind": "port",
             "sample": f"first {n} pairs of rank 0 x {ticks} ticks (same call sequence as the GPU run), find_path only, "
-                      f"1 thread (oracle/hastar_oracle.cpp)",
+                      f"{T} threads with one private planner each (oracle/hastar_oracle.cpp, -O3)",
             "tick_ms_one_core_per_pair": float(tick_max.mean()) if n else None}
 
 
-def cpu_baseline(cfgs, gpu_results, budget_s, replans, lat_ids):
+def cpu_baseline(cfgs, gpu_results, budget_s, replans, lat_ids, sample=None):
     """The oracle (CPU restatement, 'port') on `cpu_threads()` host threads, one private
     planner per thread at a time (BASELINE.md "Plan for the CPU baseline"), find_path timed
     only, as the reference harness times it (test_hybrid_astar.cpp:123-126).  Each sampled
     query replays the GPU planner's exact call sequence — the map drive, then `replans` x
     (reset + find_path), warm-up and timed steps alike (the node map's f values persist across
     reset, HybridAStar.cpp:49-52, so later replans differ from the first).  Queries are taken
-    in the GPU batch's order, in chunks of 16 per thread, until the chunks' parallel wall time
-    reaches the budget.  value = pops / parallel wall (chunk tails included).  Each query's
+    in `sample` order (planner indices; default the batch's order), in chunks of 16 per thread,
+    until the chunks' parallel wall time reaches the budget.  value = pops / parallel wall (chunk tails included).  Each query's
     last replan is compared with the GPU's last timed step (pop digest, success, cost bits)."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle.pyoracle import OraclePlanner, run_batch_threads
@@ -681,6 +731,7 @@ def cpu_baseline(cfgs, gpu_results, budget_s, replans, lat_ids):
     chunk = 16 * T
     pops, wall, plans, plan_s = 0, 0.0, 0, 0.0
     n, parity, lat = 0, True, []
+    sample = list(range(len(cfgs))) if sample is None else list(sample)
 
     def make(c):
         o = OraclePlanner(c[0])
@@ -688,8 +739,9 @@ def cpu_baseline(cfgs, gpu_results, budget_s, replans, lat_ids):
         return o
 
     with ThreadPoolExecutor(T) as ex:
-        while n < len(cfgs) and wall < budget_s:
-            sub = cfgs[n:n + chunk]
+        while n < len(sample) and wall < budget_s:
+            idx = sample[n:n + chunk]
+            sub = [cfgs[i] for i in idx]
             ors = list(ex.map(make, sub))
             r = run_batch_threads(ors, [c[1]["vel"] for c in sub], [c[1]["start"] for c in sub], replans, T)
             pops += r["pops"]
@@ -697,10 +749,10 @@ def cpu_baseline(cfgs, gpu_results, budget_s, replans, lat_ids):
             plans += r["plans"]
             plan_s += r["plan_s_sum"]
             for j in range(len(sub)):
-                g = gpu_results.result(n + j)
+                g = gpu_results.result(idx[j])
                 parity &= (int(r["digest"][j]) == g["stats"]["pop_digest"] and bool(r["ok"][j]) == g["ok"]
                            and np.float32(r["cost"][j]).tobytes() == np.float32(g["cost"]).tobytes())
-                if n + j in lat_ids:
+                if idx[j] in lat_ids:
                     lat.append(float(np.median(r["plan_ms"][j])))
             for o in ors:
                 o.close()

@@ -25,6 +25,7 @@
 #ifndef HYBRID_ASTAR
 #define HYBRID_ASTAR
 
+#include <cstdio>
 #include <cstdlib>
 #include <limits>
 #include <stdexcept>
@@ -77,8 +78,18 @@ class HybridAStar<float> {
     p.curvature_weights = curvature_weights.data();
     const char* dev = std::getenv("HASTAR_DEVICE");
     check(hastar_create_f32(&p, dev ? std::atoi(dev) : 0, &_h));
+    // The unchanged caller cannot call set_relaxed(), so it may opt in through the
+    // environment; since that silently changes find_path's results (a different algorithm),
+    // the switch is announced once on stderr.
     const char* rel = std::getenv("HASTAR_RELAXED");
     _relaxed = rel && std::atoi(rel) != 0;
+    if (_relaxed) {
+      static bool announced = false;
+      if (!announced) {
+        announced = true;
+        std::fprintf(stderr, "HybridAStar: HASTAR_RELAXED=1 selects the relaxed (non-reference) search mode\n");
+      }
+    }
   }
   // extension (not in the reference): select the relaxed search mode for find_path
   void set_relaxed(bool on) { _relaxed = on; }

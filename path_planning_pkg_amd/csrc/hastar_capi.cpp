@@ -784,6 +784,8 @@ int hastar_create_batch_f32(const hastar_params* p, int n, int device, hastar_ha
   if (he == hipSuccess) he = launch_init_nodemap_batch(out[0]->desc, static_cast<char*>(bs->slab) + b_map, stride, n, st);
   if (he == hipSuccess) he = hipStreamSynchronize(st);
   if (he != hipSuccess) {
+    // h0 is out[0] unless an async call failed before the handle loop stored it
+    if (out[0] != h0) delete h0;
     for (int i = 0; i < n; ++i) {
       if (out[i]) delete out[i];
       out[i] = nullptr;
@@ -1536,20 +1538,24 @@ static int finish_batch(DeviceCtx& DC, const hastar_handle* hs, int n, float* xy
     } else if (R.status == -28 && rc == HASTAR_OK) {
       rc = fail(HASTAR_ENOSPC, "path longer than the planner's output buffer");
     }
-    int take = R.path_len;
-    if (take > cap) {
-      take = 0;  // the caller fetches it with hastar_copy_path
-      if (stats) stats[i].status = HASTAR_ENOSPC;
+    // every path is packed on the device whatever `cap` is (the device-resident velocity
+    // profile of this batch reads len[i] points at offset i); only the host copy is limited
+    // to the caller's buffer
+    if (R.path_len > cap) {
+      if (stats) stats[i].status = HASTAR_ENOSPC;  // the caller fetches it with hastar_copy_path
       if (rc == HASTAR_OK) rc = fail(HASTAR_ENOSPC, "path buffer too small");
     }
     h_off[i] = total;
-    h_len[i] = take;
-    total += take;
+    h_len[i] = R.path_len;
+    total += R.path_len;
   }
   if (rc == HASTAR_OK && rc_over != HASTAR_OK) rc = rc_over;
   h_off[n] = total;
   DC.last_n = n;
   DC.last_total = total;
+  // the offsets go to the device even when no path came back, so that a velocity profile of
+  // this batch never reads a previous batch's offsets
+  HIPCHK(hipMemcpyAsync(DC.d_off, h_off, ((size_t)n + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
   if (total > 0) {
     if ((size_t)total > DC.pts_cap) {
       if (DC.d_pxyh) hipFree(DC.d_pxyh);
@@ -1565,14 +1571,13 @@ static int finish_batch(DeviceCtx& DC, const hastar_handle* hs, int n, float* xy
       HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_pcurv), c2 * sizeof(float)));
       DC.pts_cap = c2;
     }
-    HIPCHK(hipMemcpyAsync(DC.d_off, h_off, ((size_t)n + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(DC.d_len, h_len, (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
     HIPCHK(launch_gather_paths(DC.d_descs, DC.d_off, DC.d_len, n, DC.d_pxyh, DC.d_pcurv, st));
     HIPCHK(hipMemcpyAsync(DC.h_pxyh, DC.d_pxyh, (size_t)total * 3 * sizeof(float), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(DC.h_pcurv, DC.d_pcurv, (size_t)total * sizeof(float), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     for (int i = 0; i < n; ++i) {
-      if (h_len[i] == 0) continue;
+      if (h_len[i] == 0 || h_len[i] > cap) continue;
       std::memcpy(xyh + (size_t)i * cap * 3, DC.h_pxyh + 3 * h_off[i], (size_t)h_len[i] * 3 * sizeof(float));
       std::memcpy(curv + (size_t)i * cap, DC.h_pcurv + h_off[i], (size_t)h_len[i] * sizeof(float));
     }
@@ -2063,7 +2068,11 @@ int hastar_velocity_profile_last_batch(int device, const hastar_velocity_params*
   if (n != D->last_n) return fail(HASTAR_EINVAL, "velocity_profile_last_batch: n differs from the last batch");
   if (n == 0) return HASTAR_OK;
   const size_t pts = (size_t)D->last_total;
-  if (pts > 0 && !velocity) return fail(HASTAR_EINVAL, "velocity_profile_last_batch: null velocity");
+  if (pts == 0) {  // the last batch returned no path: nothing to profile, nothing feasible
+    std::memset(feasible, 0, (size_t)n);
+    return HASTAR_OK;
+  }
+  if (!velocity) return fail(HASTAR_EINVAL, "velocity_profile_last_batch: null velocity");
   HIPCHK(hipSetDevice(device));
   const size_t b_pt = align256(std::max<size_t>(pts, 1) * sizeof(float)), b_pf = align256(n * sizeof(float)),
                b_pb = align256(n);

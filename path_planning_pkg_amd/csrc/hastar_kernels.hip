@@ -122,8 +122,9 @@ __device__ __forceinline__ bool closed3_contains(const SearchCtx& c, uint32_t ke
   }
 }
 
-// next closed-set generation of this slot; when the 12-bit generation wraps, the wave
-// zeroes its hash table (every 4095 searches)
+// next closed-set generation of this slot; when the 8-bit generation (SLOT3_GEN_MASK) wraps,
+// the wave zeroes its hash table: every 255 searches, a pass over the whole table (several
+// MiB for a 196k-pop arena: ~2 x max_pops slots of 8 B), amortised over those searches
 __device__ __forceinline__ void closed3_next_gen(SearchCtx& c) {
   c.gen3 = (c.gen3 + 1) & SLOT3_GEN_MASK;
   if (c.gen3 == 0) {

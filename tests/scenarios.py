@@ -158,6 +158,103 @@ def synthetic_ref_boxes_scalar(N, K, seed, res=0.5, clear=8.0):
     return np.array(boxes, np.float32).reshape(-1, 4), float(stx)
 
 
+def _mt19937_words(seeds, n_words):
+    """The first n_words raw 32-bit outputs of std::mt19937(seed) for every seed at once
+    (uint32, shape (len(seeds), n_words)): init_genrand seeding and the twist as libstdc++
+    defines them, vectorised over the seeds.  The twist's in-place recurrence splits into four
+    block steps: words 0..226 read old words only, 227..453 read the new words 0..226,
+    454..622 the new words 227..395, and word 623 the new words 0 and 396."""
+    s = np.asarray(seeds, np.uint64) & np.uint64(0xffffffff)
+    S = len(s)
+    mt = np.empty((624, S), np.uint64)
+    mt[0] = s
+    for i in range(1, 624):
+        p = mt[i - 1]
+        mt[i] = (np.uint64(1812433253) * (p ^ (p >> np.uint64(30))) + np.uint64(i)) & np.uint64(0xffffffff)
+    mt = mt.astype(np.uint32)
+    up, lo, ma = np.uint32(0x80000000), np.uint32(0x7fffffff), np.uint32(0x9908b0df)
+
+    def f(a, b):  # y = upper bit of a | lower bits of b; (y >> 1) ^ (y & 1 ? MATRIX_A : 0)
+        y = (a & up) | (b & lo)
+        return (y >> np.uint32(1)) ^ np.where((y & np.uint32(1)) != 0, ma, np.uint32(0))
+
+    out = np.empty((S, n_words), np.uint32)
+    got = 0
+    while got < n_words:
+        old = mt
+        new = np.empty_like(old)
+        new[0:227] = old[397:624] ^ f(old[0:227], old[1:228])
+        new[227:454] = new[0:227] ^ f(old[227:454], old[228:455])
+        new[454:623] = new[227:396] ^ f(old[454:623], old[455:624])
+        new[623] = new[396] ^ f(old[623], new[0])
+        mt = new
+        y = mt.copy()
+        y ^= y >> np.uint32(11)
+        y ^= (y << np.uint32(7)) & np.uint32(0x9d2c5680)
+        y ^= (y << np.uint32(15)) & np.uint32(0xefc60000)
+        y ^= y >> np.uint32(18)
+        take = min(624, n_words - got)
+        out[:, got:got + take] = y[:take].T
+        got += take
+    return out
+
+
+def _ref_candidates(N, K, seeds, res=0.5, clear=8.0):
+    """The first 2K + 16 box candidates of synthetic_ref_boxes for every seed at once, with the
+    same float32 arithmetic: (cx, cy, sx, sy, sel, stx); sel marks the first K accepted ones.
+    Rows whose candidates hold fewer than K accepted ones have sel.sum() < K."""
+    f = np.float32
+    W = f(N) * f(res)
+    ax, bx = f(-0.8 * float(W)), f(0.2 * float(W))
+    ay, by = f(-0.5 * float(W)), f(0.5 * float(W))
+    stx = f(-0.6 * float(W))
+    M = 2 * K + 16
+    u = _mt19937_words(seeds, 4 * M).reshape(len(seeds), M, 4).astype(np.uint64)
+    cx, cy = _uniform_f32_vec(u[..., 0], ax, bx), _uniform_f32_vec(u[..., 1], ay, by)
+    sx, sy = _uniform_f32_vec(u[..., 2], f(1), f(6)), _uniform_f32_vec(u[..., 3], f(1), f(6))
+    keep = ~((np.hypot((cx - stx).astype(np.float32), cy) < f(clear)) | (np.hypot(cx, cy) < f(clear)))
+    sel = keep & (np.cumsum(keep, axis=1) <= K)
+    return cx, cy, sx, sy, sel, float(stx)
+
+
+def synthetic_ref_boxes_many(N, K, seeds, res=0.5, clear=8.0):
+    """synthetic_ref_boxes for many seeds at once: boxes float32 (len(seeds), K, 4) and stx.  A
+    seed whose first 2K + 16 candidates hold fewer than K accepted ones (a near-impossible draw)
+    falls back to the per-seed generator."""
+    cx, cy, sx, sy, sel, stx = _ref_candidates(N, K, seeds, res, clear)
+    out = np.empty((len(seeds), K, 4), np.float32)
+    full = sel.sum(axis=1) == K
+    r, c = np.nonzero(sel[full])
+    out[full] = np.stack([a[full][r, c] for a in (cx, cy, sx, sy)], 1).reshape(-1, K, 4)
+    for i in np.nonzero(~full)[0]:
+        out[i] = synthetic_ref_boxes(N, K, int(seeds[i]), res, clear)[0]
+    return out, stx
+
+
+def predicted_cost(N, K, query_ids, res=0.5, apf_r=2.5, chunk=8192):
+    """A cheap predictor of a synthetic_ref query's search cost (query q = seed q + 1): the
+    clearance between the start-goal segment and the nearest box, minus that box's APF reach
+    (half-diagonal + apf_r).  A box close to the straight route makes the search work around
+    it; Spearman -0.62 against the oracle's plan time over the 23,552 bench queries
+    (profiles/census_cfg3_mt19937_r02.csv).  Returned negated, so larger = costlier."""
+    ids = np.asarray(query_ids, np.int64)
+    out = np.empty(len(ids), np.float64)
+    for a in range(0, len(ids), chunk):
+        seeds = ids[a:a + chunk] + 1
+        cx, cy, sx, sy, sel, stx = _ref_candidates(N, K, seeds, res)
+        cx, cy = cx.astype(np.float64), cy.astype(np.float64)
+        r = np.hypot(sx, sy).astype(np.float64) / 2 + apf_r
+        d = np.where(sel, np.hypot(cx - np.clip(cx, stx, 0.0), cy) - r, np.inf).min(axis=1)
+        short = sel.sum(axis=1) < K
+        for i in np.nonzero(short)[0]:  # the per-seed fallback of synthetic_ref_boxes_many
+            b, _ = synthetic_ref_boxes(N, K, int(seeds[i]), res)
+            bx, by = b[:, 0].astype(np.float64), b[:, 1].astype(np.float64)
+            rr = np.hypot(b[:, 2], b[:, 3]).astype(np.float64) / 2 + apf_r
+            d[i] = (np.hypot(bx - np.clip(bx, stx, 0.0), by) - rr).min()
+        out[a:a + chunk] = -d
+    return out
+
+
 def synthetic_ref(N, bins, K, seed, res=0.5, clear=8.0):
     """SURVEY.md §8d's synthetic case drawn the way the survey's reference runs drew it:
     std::mt19937(seed) and std::uniform_real_distribution<float>; per candidate box the centre

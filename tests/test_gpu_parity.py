@@ -11,24 +11,10 @@ import math
 import numpy as np
 import pytest
 
+from tests.parity_util import assert_bits_equal, bits  # noqa: F401 (re-exported)
 from tests.scenarios import drive, harness, synthetic
 
 pytestmark = pytest.mark.gpu
-
-
-def bits(a):
-    a = np.ascontiguousarray(a, np.float32)
-    b = a.view(np.uint32).copy()
-    b[np.isnan(a)] = 0x7FC00000  # NaN == NaN regardless of payload
-    return b
-
-
-def assert_bits_equal(x, y, what):
-    bx, by = bits(x), bits(y)
-    assert bx.shape == by.shape, f"{what}: shape {bx.shape} vs {by.shape}"
-    bad = np.nonzero(bx != by)
-    assert len(bad[0]) == 0, f"{what}: {len(bad[0])} mismatches, first at {tuple(i[0] for i in bad)}: " \
-                             f"{np.asarray(x)[tuple(i[0] for i in bad)]} vs {np.asarray(y)[tuple(i[0] for i in bad)]}"
 
 
 @pytest.fixture(scope="module")

@@ -245,6 +245,59 @@ def test_velocity_profile_of_last_batch(gpu, oracle_lib):
         assert_bits_equal(vel[a:b], vo, f"velocity of path {i}")
 
 
+def test_velocity_last_batch_after_all_failed(gpu):
+    """A batch whose searches all fail returns no path: profiling it must report every planner
+    infeasible and must not read the previous batch's path offsets."""
+    cases = [synthetic(256, 36, 10, s) for s in (1, 2)]
+    gs = []
+    for cfg, proto in cases:
+        g = gpu.HybridAStar(cfg)
+        drive(g, proto)
+        gs.append(g)
+    br = gpu.find_path_batch_arrays(gs, [2.0, 2.0], [c[1]["start"] for c in cases], cap=4096)
+    assert br.ok.all() and (br.lens > 0).all()  # a previous batch with paths packed in HBM
+    blocked = []
+    for _ in range(3):  # goal cell walled in (test_edge_cases): every search fails
+        cfg, proto = synthetic(48, 36, 0, 1)
+        proto["boxes"] = np.array([[0.0, 0.0, 4.0, 4.0]], np.float32)
+        proto["start"] = [-14.0, 0.0, 0.0]
+        g = gpu.HybridAStar(cfg)
+        drive(g, proto)
+        blocked.append(g)
+    bb = gpu.find_path_batch_arrays(blocked, [2.0] * 3, [[-14.0, 0.0, 0.0]] * 3, cap=4096)
+    assert not bb.ok.any() and (bb.lens == 0).all()
+    vg = gpu.VelocityGenerator(10.0, 3.0, 2.5, 1.5, 3.0)
+    feas, vel = vg.profile_last_batch(bb.lens.astype(np.int64), np.full(3, 2.0, np.float32),
+                                      np.full(3, 10.0, np.float32), np.full(3, 2, np.uint8))
+    assert (feas == 0).all() and len(vel) == 0
+
+
+def test_velocity_last_batch_with_short_caller_buffer(gpu, oracle_lib):
+    """A planner whose path exceeds the caller's `cap` (ENOSPC, fetched with copy_path) is still
+    packed on the device at its full length, so the device-resident velocities of the planners
+    after it line up with the returned lengths."""
+    cases = [synthetic(256, 36, 10, s) for s in (1, 2, 3)]
+    gs = []
+    for cfg, proto in cases:
+        g = gpu.HybridAStar(cfg)
+        drive(g, proto)
+        gs.append(g)
+    full = gpu.find_path_batch(gs, [2.0] * 3, [c[1]["start"] for c in cases], cap=4096)[0]
+    lens = np.array([len(r["path"]) for r in full], np.int64)
+    cap = int(lens[0]) - 1  # planner 0's path does not fit; the others do
+    assert (lens[1:] <= cap).all(), lens
+    res, _ = gpu.find_path_batch(gs, [2.0] * 3, [c[1]["start"] for c in cases], cap=cap)
+    assert res[0]["stats"]["status"] == gpu.HASTAR_ENOSPC and len(res[0]["path"]) == lens[0]
+    prm = (10.0, 3.0, 2.5, 1.5, 3.0)
+    feas, vel = gpu.VelocityGenerator(*prm).profile_last_batch(lens, np.full(3, 2.0, np.float32),
+                                                              np.full(3, 10.0, np.float32), np.full(3, 2, np.uint8))
+    off = np.concatenate([[0], np.cumsum(lens)])
+    for i in range(3):
+        ok_o, vo = oracle_lib.velocity_profile(prm, 2.0, 10.0, res[i]["path"], res[i]["curvature"], False, True)
+        assert bool(feas[i]) == ok_o
+        assert_bits_equal(vel[off[i]:off[i + 1]], vo, f"velocity of path {i}")
+
+
 # ---------------------------------------------------------- batched map updates --------
 def test_batched_map_updates_equal_single_calls(gpu, oracle_lib):
     """hastar_update_goal_batch / hastar_decay_batch / hastar_update_boxes_batch over planners

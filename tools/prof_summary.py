@@ -51,8 +51,11 @@ def pmc(args):
     write = per_dispatch(args.write, "WRITE_SIZE")
     i = args.dispatch
     f_kib, w_kib = fetch[i], write[i]
+    import sys
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from path_planning_pkg_amd.buildinfo import search_kernel_hash
     out = {"kernel": KERNEL, "batch": args.batch, "grid": args.grid, "dispatch_index": i,
-           "fetch_size_kib": f_kib, "write_size_kib": w_kib,
+           "kernel_src_sha": search_kernel_hash(), "fetch_size_kib": f_kib, "write_size_kib": w_kib,
            "hbm_bytes_per_launch": (2 * f_kib + w_kib) * 1024.0,
            "note": "traffic = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 B per MI355X_MICROARCH.md §HBM; the search "
                    "kernel's loads are mostly narrow scattered accesses, for which the guide's gfx950 FETCH_SIZE "
