@@ -163,6 +163,7 @@ struct DeviceCtx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int resident_slots = 0;       // W: resident wavefronts of the search kernel
+  int n_cu = 0;                 // compute units: workgroups of the latency (one-search-per-CU) kernel
   // map-update scratch (relocation target + claim table, raster hit counters)
   size_t scratch_cap = 0;
   float* tmp = nullptr;
@@ -245,6 +246,7 @@ int device_ctx(int dev, DeviceCtx** out) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, dev));
     D.resident_slots = search_slots_per_cu() * prop.multiProcessorCount;
+    D.n_cu = prop.multiProcessorCount;
     HIPCHK(dalloc(&D.d_next, 4));  // [0] work counter, [1] head placement, [2] head done
     D.init = true;
   }
@@ -337,7 +339,7 @@ ArenaLayout arena_layout(const ArenaReq& r) {
   L.dub = align256((size_t)r.dub * 3 * sizeof(float));
   L.dubc = align256((size_t)r.dub * sizeof(float));
   L.chain = align256((size_t)r.chain * sizeof(int));
-  L.prevl = align256((size_t)ASTAR_LDS_CAP * 2 * sizeof(int));  // {prev, g} per LDS A* node
+  L.prevl = align256((size_t)2048 * 2 * sizeof(int));  // {prev, g} per LDS A* node (any LDS pool size)
   return L;
 }
 // Carve the arena at `q` and queue the clearing of its generation-stamped tables.
@@ -1607,7 +1609,12 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   DeviceCtx& DC = *hs[0]->dc;
   std::lock_guard<std::mutex> lk(DC.mu);
   hipStream_t st = DC.stream;
-  int W = std::max(1, std::min(n, DC.resident_slots));
+  // A batch no larger than the CU count runs on the latency kernel: one search per CU with the
+  // CU's whole LDS (outer open tree, 2048-node holonomic pool) and its SIMD to itself.  Larger
+  // batches fill every CU with 8 searches (the batch kernel).  HASTAR_WIDE=0/1 forces either.
+  bool wide = n <= DC.n_cu;
+  if (const char* e = std::getenv("HASTAR_WIDE")) wide = std::atoi(e) != 0;
+  int W = std::max(1, std::min(n, wide ? DC.n_cu : DC.resident_slots));
   if (const char* e = std::getenv("HASTAR_SLOTS")) W = std::max(1, std::min(W, std::atoi(e)));
   if (int rc = arenas_acquire(DC, need, W)) return rc;
   const int slots = std::min(W, DC.n_arenas);
@@ -1651,8 +1658,11 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     ms_total += ms;
     return 0;
   };
-  if (int r = timed([&] { return launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next,
-                                               hard_pops, iso, st); }))
+  if (int r = timed([&] {
+        return wide ? launch_search_wide(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, DC.d_next, hard_pops, st)
+                    : launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, hard_pops, iso,
+                                    st);
+      }))
     return r;
   // Parked searches (their arena could not take one more pop) continue in larger arenas,
   // planners no wave took run in a new queue pass: until every search has ended.
@@ -1762,8 +1772,12 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
         HIPCHK(hipMemcpyAsync(DC.d_order, notrun.data(), notrun.size() * sizeof(int), hipMemcpyHostToDevice, st));
         for (int i : notrun) in_resume[i] = 0;
         const int w = std::min<int>(slots, (int)notrun.size());
-        if (int r = timed([&] { return launch_search(DC.d_descs, (int)notrun.size(), DC.d_arenas, w, DC.d_order, 0,
-                                                     DC.d_next, hard_pops, 0, st); }))
+        if (int r = timed([&] {
+              return wide ? launch_search_wide(DC.d_descs, (int)notrun.size(), DC.d_arenas, w, DC.d_order, DC.d_next,
+                                               hard_pops, st)
+                          : launch_search(DC.d_descs, (int)notrun.size(), DC.d_arenas, w, DC.d_order, 0, DC.d_next,
+                                          hard_pops, 0, st);
+            }))
           return r;
       }
       // 3. the parked searches continue, one wave each

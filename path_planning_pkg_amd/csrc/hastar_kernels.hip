@@ -12,6 +12,7 @@
 //                          node-map (heuristic) initialisation.
 //   test kernels           unit-level hooks used by the parity tests.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <type_traits>
 #include "hastar_device.h"
 #include "hastar_kernels.h"
@@ -182,7 +183,20 @@ __device__ __forceinline__ void closed3_rebuild(SearchCtx& c, int n) {
 // neighbour probes, all in flight together).  A search whose tree outgrows LDS is
 // migrated once (same pool indices) to HBM nodes and continues there.  Both modes run
 // the same templated loop.
-constexpr int A_CAP = ASTAR_LDS_CAP;  // LDS open-tree nodes (index 0 = header)
+//
+// The layout is a compile-time configuration (AStarCfg): the node capacity of the LDS pool
+// and where the {prev, g} pairs live.  The batch kernel's waves share a CU eight ways
+// (NarrowA: 1024 nodes, pairs in the HBM arena); the latency kernel gives one search a CU's
+// whole LDS (WideA: 2048 nodes, pairs in LDS too, no HBM round trip for them).
+template <int CAP_, bool PVG_LDS_>
+struct AStarCfg {
+  static constexpr int CAP = CAP_;          // LDS open-tree nodes (index 0 = header)
+  static constexpr bool PVG_LDS = PVG_LDS_;
+  static_assert(CAP >= 128 && CAP <= 64 * 32 && (CAP & (CAP - 1)) == 0,
+                "a power of two in 128..2048: one colour VGPR holds 32 nodes per lane");
+};
+using NarrowA = AStarCfg<ASTAR_LDS_CAP, false>;
+using WideA = AStarCfg<2048, true>;
 
 typedef int v2i __attribute__((ext_vector_type(2)));
 struct NodeKF {
@@ -192,14 +206,21 @@ struct NodeKF {
 struct LinkLR {
   int16_t l, r;  // NIL = -1
 };
-struct AStarLds {
-  NodeKF kf[A_CAP];
-  LinkLR lr[A_CAP];
-  int16_t p[A_CAP];
-  int16_t ring[A_CAP];  // live node indices in f order (a ring: rank r at ring[(head + r) % A_CAP])
+template <class CF, bool = CF::PVG_LDS>
+struct PvgPart {};  // {prev, g} pairs in the HBM arena (SlotArena::prevl)
+template <class CF>
+struct PvgPart<CF, true> {
+  v2i pg[CF::CAP];  // {prev, g bits} per node, in LDS
 };
-static_assert(sizeof(AStarLds) == 16 * A_CAP, "LDS node layout");
-static_assert(A_CAP <= 64 * 32, "one colour VGPR holds 32 nodes per lane");
+template <class CF>
+struct AStarLdsT : PvgPart<CF> {
+  NodeKF kf[CF::CAP];
+  LinkLR lr[CF::CAP];
+  int16_t p[CF::CAP];
+  int16_t ring[CF::CAP];  // live node indices in f order (a ring: rank r at ring[(head + r) % CAP])
+};
+static_assert(sizeof(AStarLdsT<NarrowA>) == 16 * NarrowA::CAP, "LDS node layout");
+static_assert(sizeof(AStarLdsT<WideA>) == 24 * WideA::CAP, "LDS node layout");
 
 #define LAS __attribute__((address_space(3)))
 template <class T>
@@ -210,9 +231,10 @@ __device__ __forceinline__ LAS T* lp(T* p) {
 // the compact LDS layout for RBT<>; g and prev (HBM) are read by the search loop itself.
 // The colours are bits of one VGPR (lane j: nodes 32 j .. 32 j + 31, 1 = black): a colour
 // read is one v_readlane, a colour write one masked VALU update, no LDS round trip.
+template <class CF>
 struct LdsAcc {
   static constexpr bool kPathWalk = false;
-  LAS AStarLds* s;
+  LAS AStarLdsT<CF>* s;
   int lane;
   uint32_t cb;
   // every field is accessed through its own type (no type punning: with strict aliasing a
@@ -282,11 +304,9 @@ struct RankOut {
   int pred;     // node at rank r - 1, NIL if r == 0
 };
 
-// Level 1 samples every SR-th rank (64 lanes cover A_CAP ranks); level 2 resolves the
-// SR ranks of one bucket per value (lanes [0, SR) for value A, [SR, 2 SR) for value B).
-constexpr int SR = A_CAP / 64;
-static_assert(SR >= 2 && SR <= 32 && (SR & (SR - 1)) == 0, "A_CAP must be 128..2048, a power of two");
-
+// Level 1 samples every SR-th rank (64 lanes cover CAP ranks, SR = CAP / 64); level 2 resolves
+// the SR ranks of one bucket per value (lanes [0, SR) for value A, [SR, 2 SR) for value B).
+template <int SR>
 __device__ __forceinline__ void rank_out(RankOut& O, int b, int cnt, int off, int n, int i1, float f1, int i2,
                                          float f2) {
   auto rl_i = [](int v, int l) { return __builtin_amdgcn_readlane(v, l); };
@@ -312,9 +332,11 @@ __device__ __forceinline__ void rank_out(RankOut& O, int b, int cnt, int off, in
   }
 }
 
-__device__ __forceinline__ void rank2(const AStarLds& L, const Ring& rg, float vA, float vB, int lane, RankOut& A,
+template <class CF>
+__device__ __forceinline__ void rank2(const AStarLdsT<CF>& L, const Ring& rg, float vA, float vB, int lane, RankOut& A,
                                       RankOut& B) {
-  constexpr int M = A_CAP - 1;
+  constexpr int SR = CF::CAP / 64;
+  constexpr int M = CF::CAP - 1;
   constexpr uint64_t SMASK = (SR == 32) ? 0xffffffffull : ((1ull << SR) - 1);
   const int n = rg.n;
   const int s_r = lane * SR;
@@ -332,8 +354,8 @@ __device__ __forceinline__ void rank2(const AStarLds& L, const Ring& rg, float v
   const uint64_t m2 = __ballot(h2 && f2 < (forA ? vA : vB));
   const int cA = __popcll(m2 & SMASK), cB = __popcll((m2 >> SR) & SMASK);
   // lanes of level 2 hold ranks base..base+SR-1; rank base+SR is level-1 sample lane b
-  rank_out(A, bA, cA, 0, n, i1, f1, i2, f2);
-  rank_out(B, bB, cB, SR, n, i1, f1, i2, f2);
+  rank_out<SR>(A, bA, cA, 0, n, i1, f1, i2, f2);
+  rank_out<SR>(B, bB, cB, SR, n, i1, f1, i2, f2);
 }
 
 // Shift `cnt` consecutive ring entries by one slot (dir = -1: entries at ring offsets
@@ -341,9 +363,10 @@ __device__ __forceinline__ void rank2(const AStarLds& L, const Ring& rg, float v
 // of a lane's loads (one per 64 entries, at most A_CAP / 2 entries: the shorter side) are
 // issued before its stores, so the shift costs one LDS round trip instead of one per 64
 // entries.  Positions are ring offsets relative to `head` (masked by A_CAP - 1).
-constexpr int RING_CH = A_CAP / 2 / 64;  // chunks of 64 entries in the shorter side
-__device__ __forceinline__ void ring_shift(AStarLds& L, int head, int from, int cnt, int dir, int lane) {
-  constexpr int M = A_CAP - 1;
+template <class CF>
+__device__ __forceinline__ void ring_shift(AStarLdsT<CF>& L, int head, int from, int cnt, int dir, int lane) {
+  constexpr int RING_CH = CF::CAP / 2 / 64;  // chunks of 64 entries in the shorter side
+  constexpr int M = CF::CAP - 1;
   const int nch = (cnt + 63) >> 6;
   int16_t v[RING_CH];
 #pragma unroll
@@ -362,8 +385,9 @@ __device__ __forceinline__ void ring_shift(AStarLds& L, int head, int from, int 
 }
 
 // ring insert of node x at rank r (shifts the shorter side by one)
-__device__ __forceinline__ void ring_insert(AStarLds& L, Ring& rg, int r, int x, int lane) {
-  constexpr int M = A_CAP - 1;
+template <class CF>
+__device__ __forceinline__ void ring_insert(AStarLdsT<CF>& L, Ring& rg, int r, int x, int lane) {
+  constexpr int M = CF::CAP - 1;
   if (r < rg.n - r) {  // ranks [0, r) move one slot down, head - 1
     if (r > 0) ring_shift(L, rg.head, 0, r, -1, lane);
     rg.head = (rg.head - 1) & M;
@@ -376,8 +400,9 @@ __device__ __forceinline__ void ring_insert(AStarLds& L, Ring& rg, int r, int x,
 }
 
 // ring erase of the node at rank r
-__device__ __forceinline__ void ring_erase(AStarLds& L, Ring& rg, int r, int lane) {
-  constexpr int M = A_CAP - 1;
+template <class CF>
+__device__ __forceinline__ void ring_erase(AStarLdsT<CF>& L, Ring& rg, int r, int lane) {
+  constexpr int M = CF::CAP - 1;
   if (r < rg.n - 1 - r) {  // ranks [0, r) move one slot up, head + 1
     if (r > 0) ring_shift(L, rg.head, 0, r, +1, lane);
     rg.head = (rg.head + 1) & M;
@@ -392,14 +417,16 @@ struct SameCell {
   int cnt, idx;
   float f;
 };
-__device__ __forceinline__ SameCell same_cell(const AStarLds& L, int used, uint32_t key, int lane) {
+template <class CF>
+__device__ __forceinline__ SameCell same_cell(const AStarLdsT<CF>& L, int used, uint32_t key, int lane) {
   // all loads unconditional (in-bounds by construction) so they issue back to back
-  uint32_t kk[A_CAP / 64];
+  constexpr int Q = CF::CAP / 64;
+  uint32_t kk[Q];
 #pragma unroll
-  for (int q = 0; q < A_CAP / 64; ++q) kk[q] = L.kf[lane + 64 * q].key;
+  for (int q = 0; q < Q; ++q) kk[q] = L.kf[lane + 64 * q].key;
   uint32_t m = 0;
 #pragma unroll
-  for (int q = 0; q < A_CAP / 64; ++q) m |= (uint32_t)((lane + 64 * q < used) & (kk[q] == key)) << q;
+  for (int q = 0; q < Q; ++q) m |= (uint32_t)((lane + 64 * q < used) & (kk[q] == key)) << q;
   const uint64_t any = __ballot(m != 0);
   SameCell sc;
   sc.cnt = 0;
@@ -471,9 +498,9 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
   GAS Cell2* cells = gp(A.cell2);
-  const int cap = G ? A.open2_cap : A_CAP;
+  static_assert(G, "the LDS mode is astar_loop_lds");
+  const int cap = A.open2_cap;
   while (!tr.empty()) {
-    if (!G && c.ps2.next + 8 > A_CAP) return false;
     STAMP_T t_pop = STAMP_NOW();
     const int b = tr.begin();
     const Quad top = tr.quad(b);
@@ -567,7 +594,8 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
 }
 
 // insert (AStar.cpp:172-183) into the LDS tree: rank-decided unless shape-dependent
-__device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc>& tr, AStarLds& L, Ring& rg, uint32_t key,
+template <class CF>
+__device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AStarLdsT<CF>& L, Ring& rg, uint32_t key,
                                            float fn, float gn, int prev, const SameCell& sc, const RankOut& rb,
                                            int* node_out) {
   *node_out = NIL;
@@ -592,7 +620,7 @@ __device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc>& tr, AStarL
       left = true;
     }
   }
-  const int n = tpool_alloc(tr, c.ps2, A_CAP);
+  const int n = tpool_alloc(tr, c.ps2, CF::CAP);
   if (n == NIL) return false;
   tr.payload(n, key, fn, gn, prev);
   tr.link(left, n, parent);
@@ -601,46 +629,78 @@ __device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc>& tr, AStarL
   return true;
 }
 
-__device__ __forceinline__ void free_lds(SearchCtx& c, RBT<LdsAcc>& tr, int x) {
+template <class CF>
+__device__ __forceinline__ void free_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, int x) {
   tr.s->kf[x].key = 0xffffffffu;  // dead: never matches a cell
   tpool_free(tr, c.ps2, x);
 }
 
+// The record of a cell whose node was just inserted into the open tree (one 16-B store): not
+// closed (cgen != this search's generation), the node's g and prev link, and the hint.
+__device__ __forceinline__ void open_cell(GAS Cell2* cells, uint32_t cell, uint32_t open_cgen, float g, int prev,
+                                          uint32_t gen2, uint32_t hint) {
+  Cell2 r;
+  r.cgen = open_cgen;
+  r.g = g;
+  r.prev = prev;
+  r.oinfo = ((gen2 & CELL2_OGEN_MASK) << CELL2_OGEN_SHIFT) | hint;
+  gstore(&cells[cell], r);
+}
+
 // g of open node `hit` (the find result for neighbour k): a node inserted earlier in this
-// expansion (its {prev, g} store is still pending in the inserting lane), the g prefetched
-// for lane k's hinted node, or the node's HBM record.
-__device__ __forceinline__ float hit_g(const SearchCtx& c, int hit, int k, int hy, float hg, bool st_pv, int st_node,
-                                       float st_g) {
+// expansion (its {prev, g} store is still pending in the inserting lane), lane k's hinted node
+// when it is still that cell's node (own: its g is the cell record's, loaded with the neighbour
+// probes; a hinted index that now holds another cell's node has a g of its own), or the node's
+// {prev, g} pair.
+// {prev, g} of LDS-tree node x: in LDS (WideA) or in the HBM arena (NarrowA)
+template <class CF>
+__device__ __forceinline__ v2i pvg_load(const SearchCtx& c, AStarLdsT<CF>& L, int x) {
+  if constexpr (CF::PVG_LDS) return *lp(&L.pg[x & (CF::CAP - 1)]);
+  else return *(const GAS v2i*)&gp(c.A->prevl)[2 * (x & (CF::CAP - 1))];
+}
+template <class CF>
+__device__ __forceinline__ void pvg_store(const SearchCtx& c, AStarLdsT<CF>& L, int x, int prev, float g) {
+  if constexpr (CF::PVG_LDS) *lp(&L.pg[x & (CF::CAP - 1)]) = v2i{prev, __float_as_int(g)};
+  else *(GAS v2i*)&gp(c.A->prevl)[2 * (x & (CF::CAP - 1))] = v2i{prev, __float_as_int(g)};
+}
+
+template <class CF>
+__device__ __forceinline__ float hit_g(const SearchCtx& c, AStarLdsT<CF>& L, int hit, int k, int hy, float hg,
+                                       bool own, bool st_pv, int st_node, float st_g) {
   const uint64_t pend = __ballot(st_pv && st_node == hit);
   if (pend) return rl_f(st_g, (int)__ffsll((unsigned long long)pend) - 1);
-  if (rl_i(hy, k) == hit) return rl_f(hg, k);  // not reused in this expansion (else pending)
-  return uff(__int_as_float(gp(c.A->prevl)[2 * (hit & (A_CAP - 1)) + 1]));
+  if (own && rl_i(hy, k) == hit) return rl_f(hg, k);  // not reused in this expansion (else pending)
+  return uff(__int_as_float(pvg_load(c, L, hit).y));
 }
 
 // AStar::a_star_search (AStar.cpp:118-186) on the LDS tree.  Returns false (without
 // popping) when the next pop could overflow the LDS pool; true when the search finished
 // (*result = cost-to-goal or FLT_MAX).
-__device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AStarLds& L, Ring& rg, int adx,
+template <class CF>
+__device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AStarLdsT<CF>& L, Ring& rg, int adx,
                                                int ady, float acost, float* result) {
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
   GAS Cell2* cells = gp(A.cell2);
-  GAS int* pvg = gp(A.prevl);  // {prev, g bits} per LDS node
+  // an open (not closed) cell's record holds its hinted node's g and prev link, written with
+  // the hint; cgen = any value but this search's generation
+  const uint32_t open_cgen = c.gen2 - 1u;
   while (rg.n > 0) {
-    if (c.ps2.next + 8 > A_CAP) return false;
+    if (c.ps2.next + 8 > CF::CAP) return false;
     STAMP_T t_pop = STAMP_NOW();
     const int b = tr.begin();
     const Quad top = tr.quad(b);
     const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
     const uint32_t tcell = (uint32_t)tx * (uint32_t)P.N + (uint32_t)ty;
-    const v2i tpg = *(const GAS v2i*)&pvg[2 * (b & (A_CAP - 1))];  // the popped node's {prev, g}
+    const v2i tpg = pvg_load(c, L, b);  // the popped node's {prev, g}
     const Cell2 tc = gload(&cells[tcell]);
     const int ni = tx + adx, nj = ty + ady;
     bool valid = false, vis = false, closed = false;
     float nf = 0.0f;
     uint32_t ohint = 0xffffffffu;  // this lane's cell: last open node (| dup << 16), or none
+    float hg = 0.0f;               // g of that node (the open cell's record)
     if (lane < nact && ni > -1 && ni < P.N && nj > -1 && nj < P.N) {
       const uint32_t cell = (uint32_t)ni * (uint32_t)P.N + (uint32_t)nj;
       const float occv = gp(P.occ)[cell];
@@ -651,6 +711,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
       vis = valid && ((visw >> (cell & 31)) & 1u);
       closed = valid && cr.cgen == c.gen2;
       if ((cr.oinfo >> CELL2_OGEN_SHIFT) == (c.gen2 & CELL2_OGEN_MASK)) ohint = cr.oinfo & CELL2_HINT_MASK;
+      hg = cr.g;
     }
     // consume every probe before the first store of this pop, so that no later register
     // reuse has to wait on a store (vmcnt counts loads and stores in issue order)
@@ -658,14 +719,9 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     nf = __builtin_amdgcn_readfirstlane(0) + nf;  // keep nf live in a VGPR (no-op)
     const int tprev = ufi(tpg.x);
     const float top_g = uff(__int_as_float(tpg.y));
-    // g of this lane's hinted open node (the node a find of this cell usually returns): its
-    // load overlaps the erase below, and a node's g never changes while it is open
-    int hy = NIL;
-    float hg = 0.0f;
-    if (ohint != 0xffffffffu && !((ohint >> 16) & 1u)) {
-      hy = (int)(ohint & 0xffffu);
-      hg = __int_as_float(pvg[2 * (hy & (A_CAP - 1)) + 1]);
-    }
+    // this lane's hinted open node (the node a find of this cell usually returns); its g came
+    // with the probe (hg), and a node's g never changes while it is open
+    const int hy = (ohint != 0xffffffffu && !((ohint >> 16) & 1u)) ? (int)(ohint & 0xffffu) : NIL;
     tr.unlink(b);
     free_lds(c, tr, b);
     ring_erase(L, rg, 0, lane);
@@ -705,8 +761,8 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
         if (st_on) {  // this expansion's earlier node-map writes happen before the return
           gp(P.nm_f)[st_cell] = st_f;
           if (st_node != NIL) {
-            if (st_pv) *(GAS v2i*)&pvg[2 * (st_node & (A_CAP - 1))] = v2i{ci, __float_as_int(st_g)};
-            cells[st_cell].oinfo = ((c.gen2 & CELL2_OGEN_MASK) << CELL2_OGEN_SHIFT) | st_hint;
+            if (st_pv) pvg_store(c, L, st_node, ci, st_g);
+            open_cell(cells, st_cell, open_cgen, st_g, ci, c.gen2, st_hint);
           }
         }
         STAMP_T t_m = STAMP_NOW();
@@ -737,13 +793,20 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
         }
       }
       RankOut ra, rb;
-      rank2(L, rg, fprobe, fn, lane, ra, rb);
       int hit = 0, hit_rank = -1;
-      if (sc.cnt >= 2 || (sc.cnt == 1 && sc.f < fprobe)) {
-        hit = tr.find(key, fprobe);  // shape-dependent: the exact tree walk
-      } else if (ra.at != NIL && (ra.at_f == fprobe || ra.at == sc.idx)) {
-        hit = ra.at;
-        hit_rank = ra.r;
+      if (sc.cnt == 1 && sc.f == fprobe) {
+        // the cell's only open node carries the probed f: the in-order f sequence is strictly
+        // increasing, so every node left of it fails the lower_bound predicate and it passes
+        // (equal key): find returns it whatever the tree shape, no rank query needed
+        hit = sc.idx;
+      } else {
+        rank2(L, rg, fprobe, fn, lane, ra, rb);
+        if (sc.cnt >= 2 || (sc.cnt == 1 && sc.f < fprobe)) {
+          hit = tr.find(key, fprobe);  // shape-dependent: the exact tree walk
+        } else if (ra.at != NIL && (ra.at_f == fprobe || ra.at == sc.idx)) {
+          hit = ra.at;
+          hit_rank = ra.r;
+        }
       }
       STAMP_ADD(9, t_f);
       if (hit == 0) {
@@ -760,7 +823,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
           st_hint = nn == NIL ? ohint : ((uint32_t)nn | (uint32_t)(dup || sc.cnt > 0) << 16);
         }
         STAMP_ADD(10, t_i);
-      } else if (gn < hit_g(c, hit, k, hy, hg, st_pv, st_node, st_g)) {
+      } else if (gn < hit_g(c, L, hit, k, hy, hg, sc.cnt == 1 && sc.idx == hit, st_pv, st_node, st_g)) {
         STAMP_T t_u = STAMP_NOW();
         if (hit_rank < 0) {
           const float hf = tr.F(hit);
@@ -793,8 +856,8 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
     if (st_on) {
       gp(P.nm_f)[st_cell] = st_f;
       if (st_node != NIL) {
-        if (st_pv) *(GAS v2i*)&pvg[2 * (st_node & (A_CAP - 1))] = v2i{ci, __float_as_int(st_g)};
-        cells[st_cell].oinfo = ((c.gen2 & CELL2_OGEN_MASK) << CELL2_OGEN_SHIFT) | st_hint;
+        if (st_pv) pvg_store(c, L, st_node, ci, st_g);
+        open_cell(cells, st_cell, open_cgen, st_g, ci, c.gen2, st_hint);
       }
     }
     wave_lds_sync();
@@ -805,7 +868,8 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc>& tr, AS
 
 // AStar::find_path(int, int) (AStar.cpp:100-113); check_start = false: a_star_search from
 // the soft-reset start node without the memo test of the start (AStar.cpp:88-95)
-__device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, int sj, bool check_start = true) {
+template <class CF>
+__device__ __forceinline__ float holonomic(SearchCtx& c, AStarLdsT<CF>& L, int si, int sj, bool check_start = true) {
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
@@ -817,7 +881,7 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   c.gen2++;
   c.ps2.next = 1;
   c.ps2.free = NIL;
-  RBT<LdsAcc> tl;
+  RBT<LdsAcc<CF>> tl;
   tl.s = lp(&L);
   tl.lane = lane;
   tl.cb = 0;
@@ -829,8 +893,8 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
     const RankOut at0{0, NIL, 0.0f, NIL};
     int n0;
     insert_lds(c, tl, L, rg, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL, none, at0, &n0);
-    *(GAS v2i*)&gp(A.prevl)[2 * n0] = v2i{NIL, __float_as_int(0.0f)};  // {prev, g} of the start
-    gp(A.cell2)[s_cell].oinfo = ((c.gen2 & CELL2_OGEN_MASK) << CELL2_OGEN_SHIFT) | (uint32_t)n0;
+    pvg_store(c, L, n0, NIL, 0.0f);  // {prev, g} of the start
+    open_cell(gp(A.cell2), (uint32_t)s_cell, c.gen2 - 1u, 0.0f, NIL, c.gen2, (uint32_t)n0);
   }
   wave_lds_sync();
   const int nact = P.diag ? 8 : 4;
@@ -848,18 +912,25 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   // migrate the LDS tree to HBM nodes (identical indices) and continue there
   c.amigr++;
   GAS Node2* o2 = gp(A.open2);
-  for (int i = lane; i < c.ps2.next; i += 64) {
-    Node2 n;
-    const v2i pg = *(const GAS v2i*)&gp(A.prevl)[2 * i];
-    n.key = L.kf[i].key;
-    n.f = L.kf[i].f;
-    n.g = __int_as_float(pg.y);
-    n.l = L.lr[i].l;
-    n.r = L.lr[i].r;
-    n.p = L.p[i];
-    n.color = (int)(((uint32_t)__shfl((int)tl.cb, i >> 5, 64) >> (i & 31)) & 1u);
-    n.prev = pg.x;
-    gstore(&o2[i], n);
+  for (int base = 0; base < c.ps2.next; base += 64) {
+    const int i = base + lane;
+    // the colour shuffle runs with every lane active: a ds_bpermute reads 0 from a lane that
+    // is off in EXEC, and lanes (i >> 5) of the last chunk can be (with a 2048-node pool the
+    // colours of nodes 1984.. live in lanes 62, 63)
+    const int col = (int)(((uint32_t)__shfl((int)tl.cb, i >> 5, 64) >> (i & 31)) & 1u);
+    if (i < c.ps2.next) {
+      Node2 n;
+      const v2i pg = pvg_load(c, L, i);
+      n.key = L.kf[i].key;
+      n.f = L.kf[i].f;
+      n.g = __int_as_float(pg.y);
+      n.l = L.lr[i].l;
+      n.r = L.lr[i].r;
+      n.p = L.p[i];
+      n.color = col;
+      n.prev = pg.x;
+      gstore(&o2[i], n);
+    }
   }
   wave_lds_sync();
   RBT<HbmAcc> th;
@@ -870,14 +941,18 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLds& L, int si, in
   return result;
 }
 
-__device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, int prev) {
+// std::set<Node3D>::insert (HybridAStar.cpp:173, 191) into the outer open tree (HBM nodes
+// behind the register cache, or the LDS tree of the latency kernel; the full 48-B record
+// always goes to the arena's open3[n], the LDS tree keeps key/f/g/links of its nodes).
+template <class OT>
+__device__ __forceinline__ bool insert3(SearchCtx& c, OT& o3, const Succ& s, float f, int prev, int cap) {
   bool left;
   const uint32_t key = key3(s.cx, s.cy, s.bin);
   STAMP_T tw = STAMP_NOW();
-  const int pos = c.o3.insert_pos(key, f, &left);
+  const int pos = o3.insert_pos(key, f, &left);
   STAMP_ADD(19, tw);
   if (pos == -2) return true;
-  const int n = tpool_alloc(c.o3, c.ps3, c.A->open3_cap);
+  const int n = tpool_alloc(o3, c.ps3, cap);
   if (n == NIL) return false;
   Node3 d;
   d.key = key;
@@ -893,92 +968,175 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, const Succ& s, float f, in
   d.h = s.h;
   d.prev = prev;
   gstore(&gp(c.A->open3)[n], d);
-  c.o3.fresh(n, d);
+  o3.fresh(n, d);
   STAMP_T tl = STAMP_NOW();
-  c.o3.link(left, n, pos);
+  o3.link(left, n, pos);
   STAMP_ADD(20, tl);
   return true;
 }
 
-// ------------------------------------------------------------------- the search -------
-// One find_path (HybridAStar.cpp:68-88 incl. hybrid_a_star_search 93-199 and
-// reconstruct_path 208-262) of planner *c.P in arena *c.A, run by one wavefront.
-// Returns true when the search parked (its arena could not take one more pop; the state
-// stays in this arena, see SearchResult).  resume: continue a parked search whose records
-// the host copied into this (larger) arena.  hard_pops > 0 ends a search after that many
-// pops with HASTAR_EOVERFLOW (an explicit budget; 0 = none, the reference's behaviour).
-__device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLds& alds, long long hard_pops,
-                                           bool resume) {
+// ---- the outer open tree in LDS (latency kernel) ------------------------------------------
+// One search owns a CU: its outer open set (std::set<Node3D>, HybridAStar.h:72) keeps every
+// node's tree part in LDS, 20 B per node: {key, f, l, r, p, colour} in one 16-B record (a walk
+// step is one ds_read_b128) and g (the find-hit replacement test, HybridAStar.cpp:178).  The
+// pose / vmin / prev payload stays in the arena's 48-B open3 record, read at the pop.  The
+// open set of a cfg3 search peaks at a few hundred nodes (oracle census: 296 for query 0),
+// of the batch's longest at 9,414; when the pool cannot take one more pop the tree moves to
+// the HBM records (same indices: only links and colours are copied) and the search continues
+// behind the register cache (RBT<CachedAcc3>).
+constexpr int OUTER_LDS_CAP = 5504;
+struct alignas(16) Q3L {
+  uint32_t key;
+  float f;
+  int16_t l, r, p;  // NIL = -1; indices < OUTER_LDS_CAP
+  uint8_t col, pad;
+};
+static_assert(sizeof(Q3L) == 16, "one quad per outer LDS node");
+struct OuterLds {
+  Q3L q[OUTER_LDS_CAP];
+  float g[OUTER_LDS_CAP];
+};
+struct LdsAcc3 {
+  static constexpr bool kPathWalk = false;
+  LAS Q3L* q;
+  LAS float* gg;
+  GAS Node3* t;  // payload records (open3)
+  __device__ __forceinline__ int L(int x) const { return ufi(q[x].l); }
+  __device__ __forceinline__ int R(int x) const { return ufi(q[x].r); }
+  __device__ __forceinline__ int P(int x) const { return ufi(q[x].p); }
+  __device__ __forceinline__ int C(int x) const { return ufi(q[x].col); }
+  __device__ __forceinline__ void sL(int x, int v) { q[x].l = (int16_t)v; }
+  __device__ __forceinline__ void sR(int x, int v) { q[x].r = (int16_t)v; }
+  __device__ __forceinline__ void sP(int x, int v) { q[x].p = (int16_t)v; }
+  __device__ __forceinline__ void sC(int x, int v) { q[x].col = (uint8_t)v; }
+  __device__ __forceinline__ uint32_t K(int x) const { return ufu(q[x].key); }
+  __device__ __forceinline__ float F(int x) const { return uff(q[x].f); }
+  __device__ __forceinline__ float G(int x) const { return uff(gg[x]); }
+  __device__ __forceinline__ Quad quad(int x) const {
+    // one 16-B load (ds_read_b128) through memcpy: a byte-wise copy aliases every field
+    // store, so it stays ordered after the 16-bit link stores (a vector-typed view of the
+    // record would not, under type-based alias analysis)
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u w;
+    __builtin_memcpy(&w, (const Q3L*)&q[x], sizeof(Q3L));
+    Quad o;
+    o.key = ufu(w.x);
+    o.f = uff(__uint_as_float(w.y));
+    o.l = ufi((int)(int16_t)(w.z & 0xffffu));  // {l, r}: little-endian int16 pair
+    o.r = ufi((int)(int16_t)(w.z >> 16));
+    return o;
+  }
+  __device__ __forceinline__ Quad quad_at(int x, int) const { return quad(x); }
+  __device__ __forceinline__ void leaf(int x, int p) {
+    q[x].l = (int16_t)NIL;
+    q[x].r = (int16_t)NIL;
+    q[x].p = (int16_t)p;
+    q[x].col = (uint8_t)RB_RED;
+  }
+  // a node just written to open3[x] by insert3: its tree part (links come with link())
+  __device__ __forceinline__ void fresh(int x, const Node3& n) {
+    q[x].key = n.key;
+    q[x].f = n.f;
+    gg[x] = n.g;
+  }
+  __device__ __forceinline__ void reset_cache() {}
+  // the popped node: key/f/links from LDS, the payload from its HBM record
+  __device__ __forceinline__ Node3 node(int x) const {
+    typedef int v4 __attribute__((ext_vector_type(4)));
+    const GAS v4* h = (const GAS v4*)&t[x];
+    const v4 b = h[1], d = h[2];
+    const Quad a = quad(x);
+    Node3 n;
+    n.key = a.key;
+    n.f = a.f;
+    n.l = a.l;
+    n.r = a.r;
+    n.p = ufi(b.x);
+    n.cc = ufu((uint32_t)b.y);
+    n.g = uff(__int_as_float(b.z));
+    n.vmin = uff(__int_as_float(b.w));
+    n.x = uff(__int_as_float(d.x));
+    n.y = uff(__int_as_float(d.y));
+    n.h = uff(__int_as_float(d.z));
+    n.prev = ufi(d.w);
+    return n;
+  }
+};
+__device__ __forceinline__ RBT<LdsAcc3> lds_tree(OuterLds& ol, const SlotArena& A) {
+  RBT<LdsAcc3> t;
+  t.q = lp(ol.q);
+  t.gg = lp(ol.g);
+  t.t = gp(A.open3);
+  return t;
+}
+// LDS tree -> HBM records (links and colours; key, f, g and the payload are there already),
+// for every pool index in use, the header (0) and free-list nodes included
+__device__ __forceinline__ void lds_outer_store(SearchCtx& c, OuterLds& ol, int lane) {
+  GAS Node3* t = gp(c.A->open3);
+  const LAS Q3L* q = lp(ol.q);
+  for (int i = lane; i < c.ps3.next; i += 64) {
+    t[i].l = q[i].l;
+    t[i].r = q[i].r;
+    t[i].p = q[i].p;
+    *(GAS uint8_t*)&t[i].cc = q[i].col;  // byte 0 only: the curvature index stays
+  }
+  wave_lds_sync();
+}
+// HBM records -> LDS tree (a resumed search whose pool fits); false when it does not fit
+__device__ __forceinline__ bool lds_outer_load(SearchCtx& c, OuterLds& ol, int lane) {
+  if (c.ps3.next > OUTER_LDS_CAP - 64) return false;
+  const GAS Node3* t = gp(c.A->open3);
+  LAS Q3L* q = lp(ol.q);
+  LAS float* g = lp(ol.g);
+  for (int i = lane; i < c.ps3.next; i += 64) {
+    const Node3 n = gload(&t[i]);
+    q[i].key = n.key;
+    q[i].f = n.f;
+    q[i].l = (int16_t)n.l;
+    q[i].r = (int16_t)n.r;
+    q[i].p = (int16_t)n.p;
+    q[i].col = (uint8_t)(n.cc & 0xffu);
+    q[i].pad = 0;
+    g[i] = n.g;
+  }
+  wave_lds_sync();
+  return true;
+}
+
+// The loop of hybrid_a_star_search (HybridAStar.cpp:107-194) over outer open tree OT: the
+// HBM tree behind the register cache (RBT<CachedAcc3>) or the latency kernel's LDS tree
+// (RBT<LdsAcc3>).  Returns LOOP_DONE (the search ended: goal, shot, empty open set or a
+// status), LOOP_PARKED (the arena cannot take one more pop) or LOOP_MIGRATE (LDS tree only:
+// its pool or the closed records are about to fill; the caller moves the tree to HBM and
+// continues there, at the same pop).
+constexpr int LOOP_DONE = 0, LOOP_PARKED = 1, LOOP_MIGRATE = 2;
+struct LoopState {
+  int counter, interval;
+  bool shot_allowed;
+  uint64_t dig;
+  int ok, via_shot, terminal, dub_n;
+  float cost;
+};
+template <class CF, bool kLdsOuter, class OT>
+__device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs, AStarLdsT<CF>& alds, LoopState& S,
+                                           long long hard_pops, int closed_lim, int open_lim, int open_cap) {
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
-#ifdef HASTAR_STAMPS
-  for (int q = 0; q < NSTAMP; ++q) c.cyc[q] = 0;
-#endif
-  unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  apf_stage(P, apfs, lane);
-  c.o3.t = gp(A.open3);
-  c.o3.lane = lane;
-  c.o3.reset_cache();
-  closed3_next_gen(c);
-  c.status = 0;
-  int counter = 0, interval = P.shot_interval;
-  bool shot_allowed = false;
-  uint64_t dig = 0x243f6a8885a308d3ull;
-  int parks = 0;
-  if (!resume) {
-    c.n_closed3 = 0;
-    c.pops = c.succ = c.apops = c.asearch = c.shots = c.amigr = c.apops_g = 0;
-    c.o3.clear();
-    c.ps3.next = 1;
-    c.ps3.free = NIL;
-    // Grid3D::set_start_node soft-resets the start cell's node (Grid3D.cpp:145-148 / 153-154)
-    gp(P.nm_f)[(size_t)P.start_cx * P.N + P.start_cy] = euclid_h(P, P.start_cx, P.start_cy);
-    Succ s0;
-    s0.x = P.start_x;
-    s0.y = P.start_y;
-    s0.h = P.start_h;
-    s0.g = 0.0f;
-    s0.vmin = P.start_vmin;
-    s0.ci = P.start_ci;
-    s0.bin = P.start_bin;
-    s0.cx = P.start_cx;
-    s0.cy = P.start_cy;
-    insert3(c, s0, FLT_MAX, NIL);
-  } else {
-    // the loop state of the parked search; its open tree (header = node 0) and closed
-    // records were copied into this arena by index
-    const GAS SearchResult* R = gp(P.result);
-    c.pops = R->pops;
-    c.succ = R->successors;
-    c.apops = R->astar_pops;
-    c.asearch = R->astar_searches;
-    c.shots = R->shots;
-    c.amigr = R->astar_migrations;
-    c.apops_g = R->astar_pops_hbm;
-    dig = R->pop_digest;
-    t_start = R->t_start;
-    counter = R->counter;
-    interval = R->interval;
-    shot_allowed = R->shot_allowed != 0;
-    c.n_closed3 = R->n_closed3;
-    c.ps3.next = R->ps3_next;
-    c.ps3.free = R->ps3_free;
-    parks = R->parks;
-    closed3_rebuild(c, c.n_closed3);
-  }
-  // goal circles are the same for every Dubins evaluation of this search
+  int& counter = S.counter;
+  int& interval = S.interval;
+  bool& shot_allowed = S.shot_allowed;
+  uint64_t& dig = S.dig;
+  int& ok = S.ok;
+  int& via_shot = S.via_shot;
+  int& terminal = S.terminal;
+  int& dub_n = S.dub_n;
+  float& cost = S.cost;
+  bool parked = false;
   const float r = P.r_min;
   const GoalC GC = goal_centres(r, P.goal_x, P.goal_y, P.goal_h);
-  int ok = 0, via_shot = 0, terminal = NIL, dub_n = 0;
-  float cost = FLT_MAX;
-  bool parked = false;
   const int span = 2 * P.na + 1;
-  // the planner's outer capacity after `parks` resumes (4x each), bounded by this arena: a
-  // search parks at the same pop whatever arena the pool happens to hand it
-  const long long pcap = min((long long)P.arena_pops << (2 * min(parks, 12)), (long long)SLOT3_IDX_MASK - 1);
-  const int closed_lim = (int)min((long long)A.closed3_cap, pcap + 1);
-  const int open_lim = (int)min((long long)A.open3_cap, 2 + (long long)(P.span_alloc - 1) * pcap + 64);
+  const int open_lim_t = kLdsOuter ? min(open_lim, open_cap) : open_lim;
   // lanes per candidate action: 16 when the window has at most 4 actions (the Dubins
   // libm calls then spread over the group), else 4 (one Dubins word per lane)
 #ifdef HASTAR_DBG_NARROW
@@ -986,25 +1144,24 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
 #else
   const int gsh = span <= 4 ? 4 : 2, gs = 1 << gsh;
 #endif
-  STAMP_T tloop = STAMP_NOW();
-
-  while (!c.o3.empty()) {
+  while (!o3.empty()) {
     if (hard_pops > 0 && c.pops >= hard_pops) { c.status = -75; break; }
     // one more pop needs a closed record and at most `span` open nodes (the pop frees one)
-    if (c.n_closed3 + 1 >= closed_lim || c.ps3.next + span + 1 > open_lim) {
+    if (c.n_closed3 + 1 >= closed_lim || c.ps3.next + span + 1 > open_lim_t) {
+      if (kLdsOuter) return LOOP_MIGRATE;  // the HBM loop continues (and parks if it must)
       parked = true;
       break;
     }
     STAMP_T tp = STAMP_NOW();
-    const int b = c.o3.begin();
-    const Node3 top = c.o3.node(b);  // usually cached: the leftmost node was touched by the last walks
+    const int b = o3.begin();
+    const Node3 top = o3.node(b);  // usually cached: the leftmost node was touched by the last walks
     // the closed-set probe is issued first; its HBM latency overlaps the erase, which
     // does not depend on it (HybridAStar.cpp:109-111 order is kept: the insert itself
     // reads the popped node's fields, captured in `top`)
     uint32_t ph;
     const v2u p0 = closed3_probe(c, top.key, &ph);
-    c.o3.unlink(b);
-    tpool_free(c.o3, c.ps3, b);
+    o3.unlink(b);
+    tpool_free(o3, c.ps3, b);
     bool fresh;
     const int ci = closed3_insert(c, top, &fresh, ph, p0);
     if (ci == NIL) { c.status = -75; break; }
@@ -1176,19 +1333,19 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
       // leftmost node whatever the shape, and it matches iff its key is k or f == g.
       int hit;
       {
-        const int lm = c.o3.begin();
-        const float lf = lm != 0 ? c.o3.F(lm) : 0.0f;
+        const int lm = o3.begin();
+        const float lf = lm != 0 ? o3.F(lm) : 0.0f;
         if (lm == 0) hit = 0;
-        else if (s.g <= lf) hit = (c.o3.K(lm) == key || s.g >= lf) ? lm : 0;
-        else hit = c.o3.find(key, s.g);
+        else if (s.g <= lf) hit = (o3.K(lm) == key || s.g >= lf) ? lm : 0;
+        else hit = o3.find(key, s.g);
       }
       STAMP_ADD(13, tf3);
-      const bool repl = hit != 0 && s.g < c.o3.G(hit);
+      const bool repl = hit != 0 && s.g < o3.G(hit);
       if (hit == 0 || repl) {
         if (repl) {
           STAMP_T tu3 = STAMP_NOW();
-          c.o3.unlink(hit);
-          tpool_free(c.o3, c.ps3, hit);
+          o3.unlink(hit);
+          tpool_free(o3, c.ps3, hit);
           STAMP_ADD(15, tu3);
         }
         // AStar::find_path(int, int): a memo hit probed above is still valid while no
@@ -1205,7 +1362,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
         STAMP_ADD(3, ta);
         const float f = s.g + stl_max(h1, s.dub);
         STAMP_T ti3 = STAMP_NOW();
-        if (!insert3(c, s, f, ci)) { fail = true; break; }
+        if (!insert3(c, o3, s, f, ci, open_cap)) { fail = true; break; }
         STAMP_ADD(14, ti3);
       }
       if (c.status != 0) break;
@@ -1215,6 +1372,126 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     if (fail) c.status = -75;
     if (c.status != 0) break;
   }
+  return parked ? LOOP_PARKED : LOOP_DONE;
+}
+
+// ------------------------------------------------------------------- the search -------
+// One find_path (HybridAStar.cpp:68-88 incl. hybrid_a_star_search 93-199 and
+// reconstruct_path 208-262) of planner *c.P in arena *c.A, run by one wavefront.
+// Returns true when the search parked (its arena could not take one more pop; the state
+// stays in this arena, see SearchResult).  resume: continue a parked search whose records
+// the host copied into this (larger) arena.  hard_pops > 0 ends a search after that many
+// pops with HASTAR_EOVERFLOW (an explicit budget; 0 = none, the reference's behaviour).
+template <class CF, bool kWide>
+__device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLdsT<CF>& alds, OuterLds* ol,
+                                           long long hard_pops, bool resume, int dbg = 0) {
+  const PlannerDev& P = *c.P;
+  const SlotArena& A = *c.A;
+  const int lane = c.lane;
+#ifdef HASTAR_STAMPS
+  for (int q = 0; q < NSTAMP; ++q) c.cyc[q] = 0;
+#endif
+  unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  apf_stage(P, apfs, lane);
+  c.o3.t = gp(A.open3);
+  c.o3.lane = lane;
+  c.o3.reset_cache();
+  closed3_next_gen(c);
+  c.status = 0;
+  int counter = 0, interval = P.shot_interval;
+  bool shot_allowed = false;
+  uint64_t dig = 0x243f6a8885a308d3ull;
+  int parks = 0;
+  if (!resume) {
+    c.n_closed3 = 0;
+    c.pops = c.succ = c.apops = c.asearch = c.shots = c.amigr = c.apops_g = 0;
+    c.ps3.next = 1;
+    c.ps3.free = NIL;
+    // Grid3D::set_start_node soft-resets the start cell's node (Grid3D.cpp:145-148 / 153-154)
+    gp(P.nm_f)[(size_t)P.start_cx * P.N + P.start_cy] = euclid_h(P, P.start_cx, P.start_cy);
+    Succ s0;
+    s0.x = P.start_x;
+    s0.y = P.start_y;
+    s0.h = P.start_h;
+    s0.g = 0.0f;
+    s0.vmin = P.start_vmin;
+    s0.ci = P.start_ci;
+    s0.bin = P.start_bin;
+    s0.cx = P.start_cx;
+    s0.cy = P.start_cy;
+    if (kWide && !(dbg & 1)) {  // the latency kernel starts in its LDS tree
+      RBT<LdsAcc3> lt = lds_tree(*ol, A);
+      lt.clear();
+      insert3(c, lt, s0, FLT_MAX, NIL, OUTER_LDS_CAP);
+    } else {
+      c.o3.clear();
+      insert3(c, c.o3, s0, FLT_MAX, NIL, A.open3_cap);
+    }
+  } else {
+    // the loop state of the parked search; its open tree (header = node 0) and closed
+    // records were copied into this arena by index
+    const GAS SearchResult* R = gp(P.result);
+    c.pops = R->pops;
+    c.succ = R->successors;
+    c.apops = R->astar_pops;
+    c.asearch = R->astar_searches;
+    c.shots = R->shots;
+    c.amigr = R->astar_migrations;
+    c.apops_g = R->astar_pops_hbm;
+    dig = R->pop_digest;
+    t_start = R->t_start;
+    counter = R->counter;
+    interval = R->interval;
+    shot_allowed = R->shot_allowed != 0;
+    c.n_closed3 = R->n_closed3;
+    c.ps3.next = R->ps3_next;
+    c.ps3.free = R->ps3_free;
+    parks = R->parks;
+    closed3_rebuild(c, c.n_closed3);
+  }
+  int ok = 0, via_shot = 0, terminal = NIL, dub_n = 0;
+  float cost = FLT_MAX;
+  // the planner's outer capacity after `parks` resumes (4x each), bounded by this arena: a
+  // search parks at the same pop whatever arena the pool happens to hand it
+  const long long pcap = min((long long)P.arena_pops << (2 * min(parks, 12)), (long long)SLOT3_IDX_MASK - 1);
+  const int closed_lim = (int)min((long long)A.closed3_cap, pcap + 1);
+  const int open_lim = (int)min((long long)A.open3_cap, 2 + (long long)(P.span_alloc - 1) * pcap + 64);
+  STAMP_T tloop = STAMP_NOW();
+
+  LoopState S;
+  S.counter = counter;
+  S.interval = interval;
+  S.shot_allowed = shot_allowed;
+  S.dig = dig;
+  S.ok = ok;
+  S.via_shot = via_shot;
+  S.terminal = terminal;
+  S.dub_n = dub_n;
+  S.cost = cost;
+  int code = LOOP_MIGRATE;
+  if constexpr (kWide) {
+    // the latency kernel keeps the outer tree in LDS while it fits (a resumed search moves
+    // its tree in when it does), then continues in HBM
+    if ((!resume || lds_outer_load(c, *ol, lane)) && !(dbg & 1)) {
+      RBT<LdsAcc3> lt = lds_tree(*ol, A);
+      code = search_loop<CF, true>(c, lt, apfs, alds, S, hard_pops, closed_lim, open_lim, OUTER_LDS_CAP);
+      if (code == LOOP_MIGRATE) lds_outer_store(c, *ol, lane);
+    }
+  }
+  if (code == LOOP_MIGRATE) {
+    c.o3.reset_cache();
+    code = search_loop<CF, false>(c, c.o3, apfs, alds, S, hard_pops, closed_lim, open_lim, A.open3_cap);
+  }
+  const bool parked = code == LOOP_PARKED;
+  counter = S.counter;
+  interval = S.interval;
+  shot_allowed = S.shot_allowed;
+  dig = S.dig;
+  ok = S.ok;
+  via_shot = S.via_shot;
+  terminal = S.terminal;
+  dub_n = S.dub_n;
+  cost = S.cost;
   STAMP_ADD(6, tloop);
   if (parked) {
     if (lane == 0) {
@@ -1348,7 +1625,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HASTAR_WAVES
                                                            const int* __restrict__ order, int* __restrict__ next,
                                                            long long hard_pops, int n_prio, int iso, int resume) {
   __shared__ ApfStage apfs;
-  __shared__ AStarLds alds;
+  __shared__ AStarLdsT<NarrowA> alds;
   SearchCtx c;
   c.A = arenas + blockIdx.x;
   const SlotArena& A = *c.A;
@@ -1359,7 +1636,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HASTAR_WAVES
   if (resume) {
     if ((int)blockIdx.x < n_planners) {
       c.P = descs + order[blockIdx.x];
-      search_one(c, apfs, alds, hard_pops, true);
+      search_one<NarrowA, false>(c, apfs, alds, nullptr, hard_pops, true);
     }
     if (c.lane == 0) {
       gp(A.gens)[0] = c.gen3;
@@ -1405,7 +1682,57 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HASTAR_WAVES
     else __builtin_amdgcn_s_setprio(0);
     c.P = descs + order[q];
     // a parked search keeps its state in this wave's arena: the wave takes no more work
-    if (search_one(c, apfs, alds, hard_pops, false)) break;
+    if (search_one<NarrowA, false>(c, apfs, alds, nullptr, hard_pops, false)) break;
+  }
+  if (c.lane == 0) {
+    gp(A.gens)[0] = c.gen3;
+    gp(A.gens)[1] = c.gen2;
+  }
+}
+
+// The latency kernel: one search per CU.  A workgroup is one wavefront that takes the CU's
+// whole LDS (static, 163 KB: no other workgroup of any kernel fits beside it), so its search
+// keeps the outer open tree in LDS (OuterLds), the holonomic A* a 2048-node LDS pool with its
+// {prev, g} pairs (WideA), and the obstacle list, and its wave issues alone on its SIMD.  The
+// same search code as the batch kernel (search_one), so results are identical by
+// construction; used for batches no larger than the CU count (the replan loop's pairs, single
+// queries) and for resumed searches.  Persistent over the same work queue as
+// hastar_search_kernel; resume = 1: workgroup b continues parked planner order[b] in arena b.
+template <class CF>
+struct WideLdsT {
+  ApfStage apfs;
+  AStarLdsT<CF> alds;
+  OuterLds ol;
+};
+using WideLds = WideLdsT<WideA>;
+static_assert(sizeof(WideLds) <= 163840, "the latency kernel's LDS must fit one CU");
+template <class CF>
+__global__ __launch_bounds__(64) void hastar_search_wide_kernel(const PlannerDev* __restrict__ descs, int n_planners,
+                                                                const SlotArena* __restrict__ arenas,
+                                                                const int* __restrict__ order, int* __restrict__ next,
+                                                                long long hard_pops, int resume, int dbg) {
+  __shared__ WideLdsT<CF> W;
+  SearchCtx c;
+  c.A = arenas + blockIdx.x;
+  const SlotArena& A = *c.A;
+  c.lane = threadIdx.x;
+  c.cost_only = true;
+  c.gen3 = gp(A.gens)[0];
+  c.gen2 = gp(A.gens)[1];
+  if (resume) {
+    if ((int)blockIdx.x < n_planners) {
+      c.P = descs + order[blockIdx.x];
+      search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, true, dbg);
+    }
+  } else {
+    for (;;) {
+      int q = 0;
+      if (c.lane == 0) q = atomicAdd(next, 1);
+      q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
+      if (q >= n_planners) break;
+      c.P = descs + order[q];
+      if (search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, false, dbg)) break;
+    }
   }
   if (c.lane == 0) {
     gp(A.gens)[0] = c.gen3;
@@ -1423,7 +1750,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HASTAR_WAVES
 __global__ __launch_bounds__(64) void k_astar_query(const PlannerDev* __restrict__ P, const SlotArena* __restrict__ arena,
                                                     int si, int sj, int mode, float gwx, float gwy, float rc, float rs,
                                                     float* out_cost, float* xy, int cap, int* out_n) {
-  __shared__ AStarLds alds;
+  __shared__ AStarLdsT<NarrowA> alds;
   SearchCtx c;
   c.P = P;
   c.A = arena;
@@ -2047,11 +2374,28 @@ hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_ar
                      hard_pops, n_prio, iso, 0);
   return hipGetLastError();
 }
+// HASTAR_WIDE_DBG (diagnostics): bit 0 keeps the latency kernel's outer tree in HBM
+static int wide_dbg() {
+  const char* e = std::getenv("HASTAR_WIDE_DBG");
+  return e ? std::atoi(e) : 0;
+}
+static void launch_wide_cf(dim3 g, hipStream_t st, const PlannerDev* d, int n, const SlotArena* a, const int* o,
+                           int* nx, long long hp, int resume, int dbg) {
+  hipLaunchKernelGGL(hastar_search_wide_kernel<WideA>, g, dim3(64), 0, st, d, n, a, o, nx, hp, resume, dbg);
+}
 hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, const int* d_order,
                          long long hard_pops, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(hastar_search_kernel, dim3(n), dim3(64), 0, st, d_descs, n, d_arenas, d_order, (int*)nullptr,
-                     hard_pops, 0, 0, 1);
+  // a parked search is a long one: it continues on a CU of its own (the latency kernel)
+  launch_wide_cf(dim3(n), st, d_descs, n, d_arenas, d_order, (int*)nullptr, hard_pops, 1, wide_dbg());
+  return hipGetLastError();
+}
+hipError_t launch_search_wide(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots,
+                              const int* d_order, int* d_next, long long hard_pops, hipStream_t st) {
+  const int init[4] = {0, 0, 0, 0};
+  hipError_t e = hipMemcpyAsync(d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) return e;
+  launch_wide_cf(dim3(n_slots), st, d_descs, n, d_arenas, d_order, d_next, hard_pops, 0, wide_dbg());
   return hipGetLastError();
 }
 int search_slots_per_cu() {

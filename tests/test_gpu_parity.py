@@ -268,7 +268,9 @@ def test_batch_with_head_isolation(gpu, oracle_lib, monkeypatch):
         compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"iso batch {i}")
 
 
-def test_batch_equals_single(gpu, oracle_lib):
+@pytest.mark.parametrize("wide", ["1", "0"], ids=["latency_kernel", "batch_kernel"])
+def test_batch_equals_single(gpu, oracle_lib, monkeypatch, wide):
+    monkeypatch.setenv("HASTAR_WIDE", wide)
     cases = [synthetic(256, 36, 10, s) for s in (6, 7, 8)] + [harness()[:2]]
     planners, oracles = [], []
     for cfg, proto in cases:

@@ -125,10 +125,19 @@ def test_statuses_reported_per_planner(gpu, oracle_lib, monkeypatch):
 
 
 # ------------------------------------------------------------------ cfg3 (1024^2) ------
-def test_cfg3_parity_batch(gpu, oracle_lib):
+# Both search kernels run the same search code: the latency kernel (one search per CU, outer
+# open tree and a 2048-node holonomic pool in LDS; batches up to the CU count) and the batch
+# kernel (8 searches per CU).  HASTAR_WIDE forces one or the other for the same batch.
+KERNELS = [pytest.param("1", id="latency_kernel"), pytest.param("0", id="batch_kernel")]
+
+
+@pytest.mark.parametrize("wide", KERNELS)
+def test_cfg3_parity_batch(gpu, oracle_lib, monkeypatch, wide):
     """BASELINE configs[2]: 1024x1024x72, K = 200, bench query ids 0, 1, 2 and the longest
-    query of the bench batch (2395, 172,207 pops), searched in one batched launch, plus round 1's
+    query of the bench batch (2395, 172,207 pops: its open set outgrows the latency kernel's
+    LDS tree, which moves to HBM mid-search), searched in one batched launch, plus round 1's
     longest PCG64 query (10226, 177,407 pops)."""
+    monkeypatch.setenv("HASTAR_WIDE", wide)
     from tests.scenarios import synthetic_ref
     qs = [0, 1, 2, 2395, "pcg64:10226"]
     cases = [synthetic_ref(1024, 72, 200, seed=q + 1) if isinstance(q, int) else
@@ -149,10 +158,12 @@ def test_cfg3_parity_batch(gpu, oracle_lib):
     assert max(r["stats"]["pops"] for r in res) > 100000  # the long query is in the batch
 
 
-def test_cfg3_survey_reference_cases(gpu, oracle_lib):
+@pytest.mark.parametrize("wide", KERNELS)
+def test_cfg3_survey_reference_cases(gpu, oracle_lib, monkeypatch, wide):
     """The survey's own cases, 256² to 2048² including cfg3 seeds 1 and 3 (std::mt19937 inputs,
     tests/scenarios.py:synthetic_ref): GPU == oracle bit for bit, and both equal the counts the
     survey measured on the compiled reference (tests/golden/survey_reference_counts.json)."""
+    monkeypatch.setenv("HASTAR_WIDE", wide)
     import json
     from tests.scenarios import GOLDEN, synthetic_ref
     g = json.loads((GOLDEN / "survey_reference_counts.json").read_text())
@@ -276,24 +287,28 @@ def test_velocity_last_batch_with_short_caller_buffer(gpu, oracle_lib):
     """A planner whose path exceeds the caller's `cap` (ENOSPC, fetched with copy_path) is still
     packed on the device at its full length, so the device-resident velocities of the planners
     after it line up with the returned lengths."""
-    cases = [synthetic(256, 36, 10, s) for s in (1, 2, 3)]
+    from tests.scenarios import harness
+    cases = [synthetic(256, 36, 10, 1), harness()[:2], harness()[:2]]  # paths of 103, 43 and 43 poses
     gs = []
     for cfg, proto in cases:
         g = gpu.HybridAStar(cfg)
         drive(g, proto)
         gs.append(g)
-    full = gpu.find_path_batch(gs, [2.0] * 3, [c[1]["start"] for c in cases], cap=4096)[0]
+    vels, starts = [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases]
+    full = gpu.find_path_batch(gs, vels, starts, cap=4096)[0]
     lens = np.array([len(r["path"]) for r in full], np.int64)
     cap = int(lens[0]) - 1  # planner 0's path does not fit; the others do
     assert (lens[1:] <= cap).all(), lens
-    res, _ = gpu.find_path_batch(gs, [2.0] * 3, [c[1]["start"] for c in cases], cap=cap)
+    res, _ = gpu.find_path_batch(gs, vels, starts, cap=cap)
     assert res[0]["stats"]["status"] == gpu.HASTAR_ENOSPC and len(res[0]["path"]) == lens[0]
     prm = (10.0, 3.0, 2.5, 1.5, 3.0)
-    feas, vel = gpu.VelocityGenerator(*prm).profile_last_batch(lens, np.full(3, 2.0, np.float32),
-                                                              np.full(3, 10.0, np.float32), np.full(3, 2, np.uint8))
+    v0 = np.asarray(vels, np.float32)
+    feas, vel = gpu.VelocityGenerator(*prm).profile_last_batch(lens, v0, np.full(3, 10.0, np.float32),
+                                                              np.full(3, 2, np.uint8))
     off = np.concatenate([[0], np.cumsum(lens)])
     for i in range(3):
-        ok_o, vo = oracle_lib.velocity_profile(prm, 2.0, 10.0, res[i]["path"], res[i]["curvature"], False, True)
+        ok_o, vo = oracle_lib.velocity_profile(prm, float(v0[i]), 10.0, res[i]["path"], res[i]["curvature"], False,
+                                               True)
         assert bool(feas[i]) == ok_o
         assert_bits_equal(vel[off[i]:off[i + 1]], vo, f"velocity of path {i}")
 

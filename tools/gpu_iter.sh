@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU iteration on the box:  tools/gpu_iter.sh <tag> <stage>...   (stops at the first failure)
+#   test      pytest -m gpu (the parity suite, through the C-ABI)      -> gpurun_out/<tag>/pytest_gpu.txt
+#   smoke     __graft_entry__.smoke()                                   -> smoke.txt
+#   bench     python bench.py (defaults: cfg3, the headline line)       -> bench.json
+#   cfg5      bench.py --workload cfg5                                  -> bench_cfg5.json
+#   stamps    single-query phase stamps (lib_stamps build) of the bench's longest query and seed 1
+#   prof      tools/prof_r02.sh <tag>: rocprofv3 trace + PMC passes     -> trace_summary.json, pmc_*, counters_*
+set -o pipefail
+TAG=$1; shift
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/$TAG
+mkdir -p $O
+for st in "$@"; do
+  echo "== $st"
+  case $st in
+    test)  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 \
+             || { tail -40 $O/pytest_gpu.txt; exit 1; }; tail -2 $O/pytest_gpu.txt ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { tail -20 $O/smoke.txt; exit 1; }
+           tail -1 $O/smoke.txt ;;
+    bench) timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+           cut -c1-400 $O/bench.json ;;
+    cfg5)  timeout -k 10 600 python -u bench.py --workload cfg5 > $O/bench_cfg5.json 2> $O/bench_cfg5.err || { tail -30 $O/bench_cfg5.err; exit 1; }
+           cut -c1-400 $O/bench_cfg5.json ;;
+    stamps) HASTAR_LIB=path_planning_pkg_amd/lib_stamps/libhastar_amd.so timeout -k 10 300 python -u tools/profile_search.py --seeds 2396 1 2 3 > $O/stamps.jsonl 2>&1 \
+             || { tail -20 $O/stamps.jsonl; exit 1; }; cut -c1-300 $O/stamps.jsonl ;;
+    prof)  bash tools/prof_r02.sh $TAG || exit 1 ;;
+    *) echo "unknown stage $st"; exit 2 ;;
+  esac
+done
