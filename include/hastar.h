@@ -102,6 +102,14 @@ int hastar_reset(hastar_handle h);
 /* reset() of n planners in one call (batch drivers; same effect as n hastar_reset calls). */
 int hastar_reset_batch(const hastar_handle* hs, int n);
 
+/* Scheduling hint (no counterpart in the reference): the planner's expected search cost, the
+ * key of the longest-first order of its next batched find_path (larger first; equal keys keep
+ * the caller's order).  After every exact search the library sets it to that search's
+ * duration; 0 (a fresh planner) = unknown.  Results never depend on it, only the order in
+ * which a batch's searches start and, for a large batch, which of them run on the latency
+ * CUs. */
+int hastar_set_cost_hint(hastar_handle h, long long hint);
+
 /* update_obstacles(obstacles, confidence, apf_added_radius) (HybridAStar.cpp:29-33):
  * boxes = n x {center_x, center_y, dimension_x, dimension_y} (Obstacle.h:16-21). */
 int hastar_update_boxes(hastar_handle h, const float* boxes, const float* confidence, int n,

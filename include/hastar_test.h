@@ -34,8 +34,9 @@ int hastar_debug_astar_modes(hastar_handle h, long long* out2);
 /* Timing of the last search: {t_start, t_end} in s_memrealtime ticks (100 MHz, chip-wide
  * clock) and the slot (persistent wavefront) that ran it. */
 int hastar_debug_timing(hastar_handle h, unsigned long long* out3);
-/* Search-slot pool of the handle's device: {resident wavefronts, search waves per CU, arenas, MiB per arena}. */
-int hastar_debug_slots(hastar_handle h, long long* out4);
+/* Search-slot pool of the handle's device: {resident wavefronts, search waves per CU, arenas, MiB per arena,
+   latency CUs of a split launch (0: none)}. */
+int hastar_debug_slots(hastar_handle h, long long* out5);
 /* resume arenas carved from idle slot arenas of the pool so far (process-wide count) */
 int hastar_debug_pooled_resumes(long long* out);
 /* The relaxed kernel's per-wave progress words (4 per wave: phase, round, expansion-set size,

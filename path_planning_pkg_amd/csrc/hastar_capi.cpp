@@ -164,6 +164,14 @@ struct DeviceCtx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int resident_slots = 0;       // W: resident wavefronts of the search kernel
   int n_cu = 0;                 // compute units: workgroups of the latency (one-search-per-CU) kernel
+  // Split launch of a large batch: the head of the longest-first queue runs on the latency
+  // kernel on `head_cus` CUs, the rest on the batch kernel on the others, concurrently (two
+  // streams forked from and joined into `stream`).  Every workgroup of either kernel takes a
+  // whole CU's LDS, and the batch kernel gets n_cu - head_cus workgroups, so the two kernels
+  // land on disjoint CUs whichever is dispatched first.
+  int head_cus = 0;
+  hipStream_t head_st = nullptr, bulk_st = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_head = nullptr, ev_bulk = nullptr;
   // map-update scratch (relocation target + claim table, raster hit counters)
   size_t scratch_cap = 0;
   float* tmp = nullptr;
@@ -247,6 +255,17 @@ int device_ctx(int dev, DeviceCtx** out) {
     HIPCHK(hipGetDeviceProperties(&prop, dev));
     D.resident_slots = search_slots_per_cu() * prop.multiProcessorCount;
     D.n_cu = prop.multiProcessorCount;
+    // head CUs (HASTAR_HEAD_CUS, default 8; 0 = no split)
+    int hc = 8;
+    if (const char* e = std::getenv("HASTAR_HEAD_CUS")) hc = std::atoi(e);
+    if (hc > 0 && D.n_cu >= 8 * hc) {
+      if (hipStreamCreateWithFlags(&D.head_st, hipStreamNonBlocking) == hipSuccess &&
+          hipStreamCreateWithFlags(&D.bulk_st, hipStreamNonBlocking) == hipSuccess &&
+          hipEventCreateWithFlags(&D.ev_fork, hipEventDisableTiming) == hipSuccess &&
+          hipEventCreateWithFlags(&D.ev_head, hipEventDisableTiming) == hipSuccess &&
+          hipEventCreateWithFlags(&D.ev_bulk, hipEventDisableTiming) == hipSuccess)
+        D.head_cus = hc;
+    }
     HIPCHK(dalloc(&D.d_next, 4));  // [0] work counter, [1] head placement, [2] head done
     D.init = true;
   }
@@ -876,6 +895,12 @@ int hastar_reset(hastar_handle h) {
 
 // reset() of n planners: one kernel clears every bitmap of a device (planners grouped by
 // device and grid size)
+int hastar_set_cost_hint(hastar_handle h, long long hint) {
+  if (!h) return fail(HASTAR_EINVAL, "null handle");
+  h->last_pops = hint;
+  return HASTAR_OK;
+}
+
 int hastar_reset_batch(const hastar_handle* hs, int n) {
   if (!hs || n < 0) return fail(HASTAR_EINVAL, "bad argument");
   for (int i = 0; i < n; ++i)
@@ -1614,7 +1639,14 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   // batches fill every CU with 8 searches (the batch kernel).  HASTAR_WIDE=0/1 forces either.
   bool wide = n <= DC.n_cu;
   if (const char* e = std::getenv("HASTAR_WIDE")) wide = std::atoi(e) != 0;
-  int W = std::max(1, std::min(n, wide ? DC.n_cu : DC.resident_slots));
+  // A batch many times the CU count splits: its head (the longest expected searches, first in
+  // the queue) on `head_cus` latency CUs, the bulk on the batch kernel beside them.
+  // HASTAR_SPLIT=0/1 forces it off/on.
+  bool split = !wide && DC.head_cus > 0 && n > 4 * DC.n_cu;
+  if (const char* e = std::getenv("HASTAR_SPLIT")) split = !wide && DC.head_cus > 0 && std::atoi(e) != 0;
+  const int head = split ? std::min(DC.head_cus, n) : 0;
+  const int per_cu = DC.resident_slots / DC.n_cu;  // batch-kernel waves per CU
+  int W = std::max(1, std::min(n, wide ? DC.n_cu : split ? head + (DC.n_cu - head) * per_cu : DC.resident_slots));
   if (const char* e = std::getenv("HASTAR_SLOTS")) W = std::max(1, std::min(W, std::atoi(e)));
   if (int rc = arenas_acquire(DC, need, W)) return rc;
   const int slots = std::min(W, DC.n_arenas);
@@ -1634,12 +1666,6 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   // raised issue priority for the head of the longest-first queue (HASTAR_PRIO_N overrides)
   int n_prio = std::max(1, slots / 8);
   if (const char* e = std::getenv("HASTAR_PRIO_N")) n_prio = std::atoi(e);
-  // Isolation of the queue head (the longest expected search) from the waves sharing its
-  // CU: when the batch outnumbers the slots, the batch time is the head's latency under
-  // load, and a CU of its own cuts that by ~7 % (3.37 -> 3.13 s at B = 23552,
-  // profiles/iso_sweep_r01g.txt) for ~5 of 1536 slots.  HASTAR_ISO = 0 off, 1 SIMD, 2 CU.
-  int iso = n > slots ? 2 : 0;
-  if (const char* e = std::getenv("HASTAR_ISO")) iso = std::atoi(e);
   // an explicit pop budget (0 = none: a search runs until the reference's loop would end)
   long long hard_pops = 0;
   if (const char* e = std::getenv("HASTAR_MAX_POPS_HARD")) hard_pops = std::atoll(e);
@@ -1658,10 +1684,28 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     ms_total += ms;
     return 0;
   };
-  if (int r = timed([&] {
+  if (int r = timed([&]() -> hipError_t {
+        if (split && slots > head) {
+          // the head's queue entries 0 .. head-1 are taken statically by the latency workgroups
+          // (arenas 0 .. head-1); the batch kernel's waves count on from `head` (arenas head ..)
+          const int init[4] = {head, 0, 0, 0};
+          hipError_t e = hipMemcpyAsync(DC.d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
+          if (e == hipSuccess) e = hipEventRecord(DC.ev_fork, st);
+          if (e == hipSuccess) e = hipStreamWaitEvent(DC.head_st, DC.ev_fork, 0);
+          if (e == hipSuccess) e = hipStreamWaitEvent(DC.bulk_st, DC.ev_fork, 0);
+          if (e == hipSuccess)
+            e = launch_search_wide(DC.d_descs, n, DC.d_arenas, head, DC.d_order, DC.d_next, hard_pops, DC.head_st, 1);
+          if (e == hipSuccess)
+            e = launch_search(DC.d_descs, n, DC.d_arenas + head, std::min(slots - head, (DC.n_cu - head) * per_cu),
+                              DC.d_order, n_prio, DC.d_next, hard_pops, DC.bulk_st, head, -1);
+          if (e == hipSuccess) e = hipEventRecord(DC.ev_head, DC.head_st);
+          if (e == hipSuccess) e = hipEventRecord(DC.ev_bulk, DC.bulk_st);
+          if (e == hipSuccess) e = hipStreamWaitEvent(st, DC.ev_head, 0);
+          if (e == hipSuccess) e = hipStreamWaitEvent(st, DC.ev_bulk, 0);
+          return e;
+        }
         return wide ? launch_search_wide(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, DC.d_next, hard_pops, st)
-                    : launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, hard_pops, iso,
-                                    st);
+                    : launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, hard_pops, st);
       }))
     return r;
   // Parked searches (their arena could not take one more pop) continue in larger arenas,
@@ -1776,7 +1820,7 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
               return wide ? launch_search_wide(DC.d_descs, (int)notrun.size(), DC.d_arenas, w, DC.d_order, DC.d_next,
                                                hard_pops, st)
                           : launch_search(DC.d_descs, (int)notrun.size(), DC.d_arenas, w, DC.d_order, 0, DC.d_next,
-                                          hard_pops, 0, st);
+                                          hard_pops, st);
             }))
           return r;
       }
@@ -2490,13 +2534,14 @@ int hastar_debug_pooled_resumes(long long* out) {
   return HASTAR_OK;
 }
 
-int hastar_debug_slots(hastar_handle h, long long* out4) {
+int hastar_debug_slots(hastar_handle h, long long* out5) {
   if (!h || !h->dc) return fail(HASTAR_EINVAL, "bad handle");
   const DeviceCtx& D = *h->dc;
-  out4[0] = D.resident_slots;
-  out4[1] = search_slots_per_cu();
-  out4[2] = D.n_arenas;
-  out4[3] = (long long)(D.arena_bytes >> 20);
+  out5[0] = D.resident_slots;
+  out5[1] = search_slots_per_cu();
+  out5[2] = D.n_arenas;
+  out5[3] = (long long)(D.arena_bytes >> 20);
+  out5[4] = D.head_cus;
   return HASTAR_OK;
 }
 

@@ -4,13 +4,14 @@
 #include "hastar_layout.h"
 
 namespace hastar {
+// the batch kernel: 8 search waves per CU (n_slots arenas; slot s runs in d_arenas[s])
 hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots, const int* d_order, int n_prio,
-                         int* d_next, long long hard_pops, int iso, hipStream_t st);
+                         int* d_next, long long hard_pops, hipStream_t st, int arena_base = 0, int q0 = 0);
 hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, const int* d_order,
                          long long hard_pops, hipStream_t st);
 // the latency kernel: one search per CU (batches no larger than the CU count, resumes)
 hipError_t launch_search_wide(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots,
-                              const int* d_order, int* d_next, long long hard_pops, hipStream_t st);
+                              const int* d_order, int* d_next, long long hard_pops, hipStream_t st, int head = 0);
 int search_slots_per_cu();
 hipError_t launch_relaxed(const PlannerDev* d_descs, int n, const RelaxArena* d_arenas, int n_arenas, int* d_next,
                           const RelaxParams& rp, RelaxField* d_fields, hipStream_t st);

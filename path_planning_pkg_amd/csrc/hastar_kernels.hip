@@ -46,10 +46,47 @@ struct Succ {
   float dub;
 };
 
+// Pin a wave-uniform value in SGPRs.  The descriptors are read-only kernel arguments, so the
+// compiler may re-issue a field's scalar load wherever it runs short of SGPRs
+// (rematerialisation) instead of keeping it; each such s_load is followed by an lgkmcnt(0)
+// wait, which also drains the wave's outstanding LDS reads.  A value that went through an
+// empty asm is opaque: it is kept in a register or spilled to a VGPR lane, never re-loaded.
+template <class T>
+__device__ __forceinline__ GAS T* pin(GAS T* p) {
+  uint64_t v = (uint64_t)p;
+  asm volatile("" : "+s"(v));
+  return (GAS T*)v;
+}
+__device__ __forceinline__ uint32_t pin(uint32_t v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+__device__ __forceinline__ int pin(int v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+__device__ __forceinline__ float pin(float v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
 struct SearchCtx {
   const PlannerDev* __restrict__ P;   // planner descriptor in HBM (uniform, read-only: scalar loads)
   const SlotArena* __restrict__ A;    // this wave's search arena
   int lane;
+  int slot;                  // index of this wave's arena in the device's pool (parks, timing)
+  // the hot descriptor fields, pinned in registers for the whole search (bind_hot)
+  GAS float* occ;
+  GAS float* nm_f;
+  GAS uint32_t* visited;
+  GAS Cell2* cell2;
+  GAS int* prevl;
+  GAS Slot3* slots3;
+  GAS Closed3* closed3;
+  GAS Node3* open3;
+  uint32_t smask;
+  int N;
+  float thr;
   RBT<CachedAcc3> o3;        // outer open tree: HBM nodes behind a register node cache
   PoolState ps3, ps2;
   int n_closed3;
@@ -61,6 +98,23 @@ struct SearchCtx {
   unsigned long long cyc[NSTAMP];
 #endif
 };
+
+// the hot fields of c.P and c.A, once per search (or per A* query)
+__device__ __forceinline__ void bind_hot(SearchCtx& c) {
+  const PlannerDev& P = *c.P;
+  const SlotArena& A = *c.A;
+  c.occ = pin(gp(P.occ));
+  c.nm_f = pin(gp(P.nm_f));
+  c.visited = pin(gp(P.visited));
+  c.cell2 = pin(gp(A.cell2));
+  c.prevl = pin(gp(A.prevl));
+  c.slots3 = pin(gp(A.slots3));
+  c.closed3 = pin(gp(A.closed3));
+  c.open3 = pin(gp(A.open3));
+  c.smask = pin(A.slots3_mask);
+  c.N = pin(P.N);
+  c.thr = pin(P.thr);
+}
 
 // ---------------------------------------------------------------- closed sets --------
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
@@ -78,13 +132,13 @@ __device__ __forceinline__ uint32_t slot_hash(uint32_t k) {
 // The caller may issue the first probe early (closed3_probe) and pass it in.
 __device__ __forceinline__ v2u closed3_probe(const SearchCtx& c, uint32_t key, uint32_t* h) {
   *h = slot_hash(key) & c.A->slots3_mask;
-  return *(const GAS v2u*)&gp(c.A->slots3)[*h];
+  return *(const GAS v2u*)&c.slots3[*h];
 }
 __device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n, bool* fresh, uint32_t h, v2u first) {
   const SlotArena& A = *c.A;
   const uint32_t gbits = (c.gen3 & SLOT3_GEN_MASK) << SLOT3_IDX_BITS;
   for (bool at_first = true;; at_first = false) {
-    GAS v2u* s = (GAS v2u*)&gp(A.slots3)[h];
+    GAS v2u* s = (GAS v2u*)&c.slots3[h];
     const v2u sv = at_first ? first : *s;  // {key, gi}
     if ((sv.y & ~SLOT3_IDX_MASK) != gbits) {
       *fresh = true;
@@ -99,7 +153,7 @@ __device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n, bool
       r.y = n.y;
       r.h = n.h;
       r.ci = (int)(n.cc >> 8);
-      gstore(&gp(A.closed3)[idx], r);
+      gstore(&c.closed3[idx], r);
       *s = v2u{n.key, gbits | (uint32_t)idx};
       return idx;
     }
@@ -107,19 +161,18 @@ __device__ __forceinline__ int closed3_insert(SearchCtx& c, const Node3& n, bool
       *fresh = false;
       return (int)(sv.y & SLOT3_IDX_MASK);
     }
-    h = (h + 1) & A.slots3_mask;
+    h = (h + 1) & c.smask;
   }
 }
 
 __device__ __forceinline__ bool closed3_contains(const SearchCtx& c, uint32_t key) {
-  const SlotArena& A = *c.A;
-  uint32_t h = slot_hash(key) & A.slots3_mask;
+  uint32_t h = slot_hash(key) & c.smask;
   const uint32_t gbits = (c.gen3 & SLOT3_GEN_MASK) << SLOT3_IDX_BITS;
   for (;;) {
-    const v2u s = *(const GAS v2u*)&gp(A.slots3)[h];  // {key, gi}
+    const v2u s = *(const GAS v2u*)&c.slots3[h];  // {key, gi}
     if ((s.y & ~SLOT3_IDX_MASK) != gbits) return false;
     if (s.x == key) return true;
-    h = (h + 1) & A.slots3_mask;
+    h = (h + 1) & c.smask;
   }
 }
 
@@ -129,10 +182,9 @@ __device__ __forceinline__ bool closed3_contains(const SearchCtx& c, uint32_t ke
 __device__ __forceinline__ void closed3_next_gen(SearchCtx& c) {
   c.gen3 = (c.gen3 + 1) & SLOT3_GEN_MASK;
   if (c.gen3 == 0) {
-    const SlotArena& A = *c.A;
     typedef int v4 __attribute__((ext_vector_type(4)));
-    GAS v4* t = (GAS v4*)gp(A.slots3);
-    const size_t n4 = ((size_t)A.slots3_mask + 1) / 2;  // two 8-B slots per 16-B store
+    GAS v4* t = (GAS v4*)c.slots3;
+    const size_t n4 = ((size_t)c.smask + 1) / 2;  // two 8-B slots per 16-B store
     for (size_t i = c.lane; i < n4; i += 64) t[i] = v4{0, 0, 0, 0};
     wave_lds_sync();
     c.gen3 = 1;
@@ -144,17 +196,16 @@ __device__ __forceinline__ void closed3_next_gen(SearchCtx& c) {
 // different keys concurrently: a slot is claimed by a compare-and-swap of its generation
 // word, so every probe sequence stays contiguous (claims are never undone).
 __device__ __forceinline__ void closed3_rebuild(SearchCtx& c, int n) {
-  const SlotArena& A = *c.A;
   const uint32_t gbits = (c.gen3 & SLOT3_GEN_MASK) << SLOT3_IDX_BITS;
-  GAS Slot3* t = gp(A.slots3);
+  GAS Slot3* t = c.slots3;
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // after a generation-wrap zeroing of the table
   for (int i = c.lane; i < n; i += 64) {
-    const uint32_t key = gp(A.closed3)[i].key;
-    uint32_t h = slot_hash(key) & A.slots3_mask;
+    const uint32_t key = c.closed3[i].key;
+    uint32_t h = slot_hash(key) & c.smask;
     uint32_t cur = __hip_atomic_load((uint32_t*)&t[h].gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {
       if ((cur & ~SLOT3_IDX_MASK) == gbits) {
-        h = (h + 1) & A.slots3_mask;
+        h = (h + 1) & c.smask;
         cur = __hip_atomic_load((uint32_t*)&t[h].gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         continue;
       }
@@ -464,14 +515,13 @@ struct HbmAcc : AosAcc<Node2, GAS Node2*> {
 // AStar::update_visted + Grid2D::update_costs (AStar.cpp:209-218, Grid2D.cpp:219-227):
 // the prev chain of closed records, which are the cells' own records
 __device__ __forceinline__ void memoise(SearchCtx& c, float total, int from) {
-  const PlannerDev& P = *c.P;
-  const GAS Cell2* cells = gp(c.A->cell2);
-  const uint32_t NN = (uint32_t)P.N * (uint32_t)P.N;
+  const GAS Cell2* cells = c.cell2;
+  const uint32_t NN = (uint32_t)c.N * (uint32_t)c.N;
   for (int i = from; i != NIL && (uint32_t)i < NN;) {  // (the bound only guards a corrupted chain)
     const Cell2 r = gload(&cells[i]);
-    GAS uint32_t* vw = &gp(P.visited)[(uint32_t)i >> 5];
+    GAS uint32_t* vw = &c.visited[(uint32_t)i >> 5];
     *vw = *vw | (1u << (i & 31));  // one wave owns the planner: a plain read-modify-write
-    gp(P.nm_f)[i] = total - r.g;
+    c.nm_f[i] = total - r.g;
     i = r.prev;
   }
 }
@@ -497,7 +547,7 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
   const SlotArena& A = *c.A;
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
-  GAS Cell2* cells = gp(A.cell2);
+  GAS Cell2* cells = c.cell2;
   static_assert(G, "the LDS mode is astar_loop_lds");
   const int cap = A.open2_cap;
   while (!tr.empty()) {
@@ -506,7 +556,7 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     const Quad top = tr.quad(b);
     const float top_g = uff(tr.G(b));
     const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
-    const uint32_t tcell = (uint32_t)tx * (uint32_t)P.N + (uint32_t)ty;
+    const uint32_t tcell = (uint32_t)tx * (uint32_t)c.N + (uint32_t)ty;
     // one HBM round trip: the popped cell's closed state and prev link, and the
     // neighbour probes (bounds, occupancy, memo flag, node-map f, closed membership —
     // loop-invariant during this expansion; Grid2D::get_neighbors, Grid2D.cpp:72-96)
@@ -515,13 +565,13 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     const int ni = tx + adx, nj = ty + ady;
     bool valid = false, vis = false, closed = false;
     float nf = 0.0f;
-    if (lane < nact && ni > -1 && ni < P.N && nj > -1 && nj < P.N) {
-      const uint32_t cell = (uint32_t)ni * (uint32_t)P.N + (uint32_t)nj;
-      const float occv = gp(P.occ)[cell];
-      const uint32_t visw = gp(P.visited)[cell >> 5];
-      nf = gp(P.nm_f)[cell];
+    if (lane < nact && ni > -1 && ni < c.N && nj > -1 && nj < c.N) {
+      const uint32_t cell = (uint32_t)ni * (uint32_t)c.N + (uint32_t)nj;
+      const float occv = c.occ[cell];
+      const uint32_t visw = c.visited[cell >> 5];
+      nf = c.nm_f[cell];
       const uint32_t cg = cells[cell].cgen;
-      valid = occv < P.thr;
+      valid = occv < c.thr;
       vis = valid && ((visw >> (cell & 31)) & 1u);
       closed = valid && cg == c.gen2;
     }
@@ -573,7 +623,7 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
       const float gn = g0 + kcost;
       if (hit == 0) {
         const float fn = gn + euclid_h(P, ki, kj);
-        gp(P.nm_f)[(size_t)ki * P.N + kj] = fn;  // Node2D::set_accumulated_cost
+        c.nm_f[(size_t)ki * c.N + kj] = fn;  // Node2D::set_accumulated_cost
         STAMP_T t_i = STAMP_NOW();
         if (!insert2(c, tr, cap, key, fn, gn, ci)) { c.status = -75; *result = FLT_MAX; return true; }
         if (!G) STAMP_ADD(10, t_i);
@@ -583,7 +633,7 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
         tpool_free(tr, c.ps2, hit);
         if (!G) STAMP_ADD(11, t_u);
         const float fn = gn + euclid_h(P, ki, kj);
-        gp(P.nm_f)[(size_t)ki * P.N + kj] = fn;
+        c.nm_f[(size_t)ki * c.N + kj] = fn;
         if (!insert2(c, tr, cap, key, fn, gn, ci)) { c.status = -75; *result = FLT_MAX; return true; }
       }
     }
@@ -656,12 +706,12 @@ __device__ __forceinline__ void open_cell(GAS Cell2* cells, uint32_t cell, uint3
 template <class CF>
 __device__ __forceinline__ v2i pvg_load(const SearchCtx& c, AStarLdsT<CF>& L, int x) {
   if constexpr (CF::PVG_LDS) return *lp(&L.pg[x & (CF::CAP - 1)]);
-  else return *(const GAS v2i*)&gp(c.A->prevl)[2 * (x & (CF::CAP - 1))];
+  else return *(const GAS v2i*)&c.prevl[2 * (x & (CF::CAP - 1))];
 }
 template <class CF>
 __device__ __forceinline__ void pvg_store(const SearchCtx& c, AStarLdsT<CF>& L, int x, int prev, float g) {
   if constexpr (CF::PVG_LDS) *lp(&L.pg[x & (CF::CAP - 1)]) = v2i{prev, __float_as_int(g)};
-  else *(GAS v2i*)&gp(c.A->prevl)[2 * (x & (CF::CAP - 1))] = v2i{prev, __float_as_int(g)};
+  else *(GAS v2i*)&c.prevl[2 * (x & (CF::CAP - 1))] = v2i{prev, __float_as_int(g)};
 }
 
 template <class CF>
@@ -680,10 +730,9 @@ template <class CF>
 __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AStarLdsT<CF>& L, Ring& rg, int adx,
                                                int ady, float acost, float* result) {
   const PlannerDev& P = *c.P;
-  const SlotArena& A = *c.A;
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
-  GAS Cell2* cells = gp(A.cell2);
+  GAS Cell2* cells = c.cell2;
   // an open (not closed) cell's record holds its hinted node's g and prev link, written with
   // the hint; cgen = any value but this search's generation
   const uint32_t open_cgen = c.gen2 - 1u;
@@ -693,7 +742,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
     const int b = tr.begin();
     const Quad top = tr.quad(b);
     const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
-    const uint32_t tcell = (uint32_t)tx * (uint32_t)P.N + (uint32_t)ty;
+    const uint32_t tcell = (uint32_t)tx * (uint32_t)c.N + (uint32_t)ty;
     const v2i tpg = pvg_load(c, L, b);  // the popped node's {prev, g}
     const Cell2 tc = gload(&cells[tcell]);
     const int ni = tx + adx, nj = ty + ady;
@@ -701,13 +750,13 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
     float nf = 0.0f;
     uint32_t ohint = 0xffffffffu;  // this lane's cell: last open node (| dup << 16), or none
     float hg = 0.0f;               // g of that node (the open cell's record)
-    if (lane < nact && ni > -1 && ni < P.N && nj > -1 && nj < P.N) {
-      const uint32_t cell = (uint32_t)ni * (uint32_t)P.N + (uint32_t)nj;
-      const float occv = gp(P.occ)[cell];
-      const uint32_t visw = gp(P.visited)[cell >> 5];
-      nf = gp(P.nm_f)[cell];
+    if (lane < nact && ni > -1 && ni < c.N && nj > -1 && nj < c.N) {
+      const uint32_t cell = (uint32_t)ni * (uint32_t)c.N + (uint32_t)nj;
+      const float occv = c.occ[cell];
+      const uint32_t visw = c.visited[cell >> 5];
+      nf = c.nm_f[cell];
       const Cell2 cr = gload(&cells[cell]);
-      valid = occv < P.thr;
+      valid = occv < c.thr;
       vis = valid && ((visw >> (cell & 31)) & 1u);
       closed = valid && cr.cgen == c.gen2;
       if ((cr.oinfo >> CELL2_OGEN_SHIFT) == (c.gen2 & CELL2_OGEN_MASK)) ohint = cr.oinfo & CELL2_HINT_MASK;
@@ -759,7 +808,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
       if ((vismask >> k) & 1ull) {
         const float tot = rl_f(nf, k) + g0 + kcost;
         if (st_on) {  // this expansion's earlier node-map writes happen before the return
-          gp(P.nm_f)[st_cell] = st_f;
+          c.nm_f[st_cell] = st_f;
           if (st_node != NIL) {
             if (st_pv) pvg_store(c, L, st_node, ci, st_g);
             open_cell(cells, st_cell, open_cgen, st_g, ci, c.gen2, st_hint);
@@ -815,7 +864,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
         if (!insert_lds(c, tr, L, rg, key, fn, gn, ci, sc, rb, &nn)) { c.status = -75; *result = FLT_MAX; return true; }
         if (lane == k) {  // Node2D::set_accumulated_cost; the cell's nm_f is written even
           st_on = true;   // when the insert is dropped (AStar.cpp:172-183)
-          st_cell = (uint32_t)ki * (uint32_t)P.N + (uint32_t)kj;
+          st_cell = (uint32_t)ki * (uint32_t)c.N + (uint32_t)kj;
           st_f = fn;
           st_g = gn;
           st_node = nn;
@@ -844,7 +893,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
         if (!insert_lds(c, tr, L, rg, key, fn, gn, ci, sc, rb, &nn)) { c.status = -75; *result = FLT_MAX; return true; }
         if (lane == k) {
           st_on = true;
-          st_cell = (uint32_t)ki * (uint32_t)P.N + (uint32_t)kj;
+          st_cell = (uint32_t)ki * (uint32_t)c.N + (uint32_t)kj;
           st_f = fn;
           st_g = gn;
           st_node = nn;
@@ -854,7 +903,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
       }
     }
     if (st_on) {
-      gp(P.nm_f)[st_cell] = st_f;
+      c.nm_f[st_cell] = st_f;
       if (st_node != NIL) {
         if (st_pv) pvg_store(c, L, st_node, ci, st_g);
         open_cell(cells, st_cell, open_cgen, st_g, ci, c.gen2, st_hint);
@@ -873,10 +922,10 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLdsT<CF>& L, int s
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
-  const size_t s_cell = (size_t)si * P.N + sj;
-  if (check_start && ((gp(P.visited)[s_cell >> 5] >> (s_cell & 31)) & 1u)) return gp(P.nm_f)[s_cell];
+  const size_t s_cell = (size_t)si * c.N + sj;
+  if (check_start && ((c.visited[s_cell >> 5] >> (s_cell & 31)) & 1u)) return c.nm_f[s_cell];
   const float h0 = euclid_h(P, si, sj);
-  gp(P.nm_f)[s_cell] = h0;  // Grid2D::set_start_node_grid -> Node2D::soft_reset
+  c.nm_f[s_cell] = h0;  // Grid2D::set_start_node_grid -> Node2D::soft_reset
   c.asearch++;
   c.gen2++;
   c.ps2.next = 1;
@@ -894,7 +943,7 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLdsT<CF>& L, int s
     int n0;
     insert_lds(c, tl, L, rg, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL, none, at0, &n0);
     pvg_store(c, L, n0, NIL, 0.0f);  // {prev, g} of the start
-    open_cell(gp(A.cell2), (uint32_t)s_cell, c.gen2 - 1u, 0.0f, NIL, c.gen2, (uint32_t)n0);
+    open_cell(c.cell2, (uint32_t)s_cell, c.gen2 - 1u, 0.0f, NIL, c.gen2, (uint32_t)n0);
   }
   wave_lds_sync();
   const int nact = P.diag ? 8 : 4;
@@ -967,7 +1016,7 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, OT& o3, const Succ& s, flo
   d.y = s.y;
   d.h = s.h;
   d.prev = prev;
-  gstore(&gp(c.A->open3)[n], d);
+  gstore(&c.open3[n], d);
   o3.fresh(n, d);
   STAMP_T tl = STAMP_NOW();
   o3.link(left, n, pos);
@@ -1062,17 +1111,17 @@ struct LdsAcc3 {
     return n;
   }
 };
-__device__ __forceinline__ RBT<LdsAcc3> lds_tree(OuterLds& ol, const SlotArena& A) {
+__device__ __forceinline__ RBT<LdsAcc3> lds_tree(OuterLds& ol, const SearchCtx& c) {
   RBT<LdsAcc3> t;
   t.q = lp(ol.q);
   t.gg = lp(ol.g);
-  t.t = gp(A.open3);
+  t.t = c.open3;
   return t;
 }
 // LDS tree -> HBM records (links and colours; key, f, g and the payload are there already),
 // for every pool index in use, the header (0) and free-list nodes included
 __device__ __forceinline__ void lds_outer_store(SearchCtx& c, OuterLds& ol, int lane) {
-  GAS Node3* t = gp(c.A->open3);
+  GAS Node3* t = c.open3;
   const LAS Q3L* q = lp(ol.q);
   for (int i = lane; i < c.ps3.next; i += 64) {
     t[i].l = q[i].l;
@@ -1085,7 +1134,7 @@ __device__ __forceinline__ void lds_outer_store(SearchCtx& c, OuterLds& ol, int 
 // HBM records -> LDS tree (a resumed search whose pool fits); false when it does not fit
 __device__ __forceinline__ bool lds_outer_load(SearchCtx& c, OuterLds& ol, int lane) {
   if (c.ps3.next > OUTER_LDS_CAP - 64) return false;
-  const GAS Node3* t = gp(c.A->open3);
+  const GAS Node3* t = c.open3;
   LAS Q3L* q = lp(ol.q);
   LAS float* g = lp(ol.g);
   for (int i = lane; i < c.ps3.next; i += 64) {
@@ -1177,7 +1226,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
       cur.h = top.h;
       cur.ci = (int)(top.cc >> 8);
     } else {
-      cur = gload(&gp(A.closed3)[ci]);
+      cur = gload(&c.closed3[ci]);
     }
     c.pops++;
     const int cx = key3_x(cur.key), cy = key3_y(cur.key), cbin = key3_bin(cur.key);
@@ -1256,7 +1305,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
       sbin = heading_bin(sh, P.prec);
       scx = trunc_f(sx / P.res);
       scy = trunc_f(sy / P.res);
-      inb = scx > -1 && scx < P.N && scy > -1 && scy < P.N;
+      inb = scx > -1 && scx < c.N && scy > -1 && scy < c.N;
     }
     const bool lead = inb && sub == 0;
     const uint32_t skey = key3(scx, scy, sbin);
@@ -1265,12 +1314,12 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     float occv = 0.0f, pnf = 0.0f;
     uint32_t pvis = 0;
     if (lead) {
-      const size_t cell = (size_t)scx * P.N + scy;
-      occv = gp(P.occ)[cell];
-      sh0 = slot_hash(skey) & A.slots3_mask;
-      slot0 = *(const GAS v2u*)&gp(A.slots3)[sh0];
-      pvis = (gp(P.visited)[cell >> 5] >> (cell & 31)) & 1u;
-      pnf = gp(P.nm_f)[cell];
+      const size_t cell = (size_t)scx * c.N + scy;
+      occv = c.occ[cell];
+      sh0 = slot_hash(skey) & c.smask;
+      slot0 = *(const GAS v2u*)&c.slots3[sh0];
+      pvis = (c.visited[cell >> 5] >> (cell & 31)) & 1u;
+      pnf = c.nm_f[cell];
     }
     STAMP_ADD(16, tx);
     STAMP_T tdub = STAMP_NOW();
@@ -1280,7 +1329,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     const float fc = apf_fused(P, apfs, cur.x, cur.y, sx, sy, sh, __ballot(lead), gs, lane);
     STAMP_ADD(17, tapf);
     STAMP_T tw = STAMP_NOW();
-    const bool kept = lead && occv < P.thr;
+    const bool kept = lead && occv < c.thr;
     const uint64_t km = __ballot(kept);
     c.succ += __popcll(km);
     // closed-set membership (continuing each kept candidate's probe sequence; the closed
@@ -1296,8 +1345,8 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
           isc = true;
           break;
         }
-        hs = (hs + 1) & A.slots3_mask;
-        sv = *(const GAS v2u*)&gp(A.slots3)[hs];
+        hs = (hs + 1) & c.smask;
+        sv = *(const GAS v2u*)&c.slots3[hs];
       }
     }
     const uint64_t closed_m = __ballot(isc);
@@ -1385,6 +1434,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
 template <class CF, bool kWide>
 __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLdsT<CF>& alds, OuterLds* ol,
                                            long long hard_pops, bool resume, int dbg = 0) {
+  bind_hot(c);
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
@@ -1393,7 +1443,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
 #endif
   unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   apf_stage(P, apfs, lane);
-  c.o3.t = gp(A.open3);
+  c.o3.t = c.open3;
   c.o3.lane = lane;
   c.o3.reset_cache();
   closed3_next_gen(c);
@@ -1408,7 +1458,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     c.ps3.next = 1;
     c.ps3.free = NIL;
     // Grid3D::set_start_node soft-resets the start cell's node (Grid3D.cpp:145-148 / 153-154)
-    gp(P.nm_f)[(size_t)P.start_cx * P.N + P.start_cy] = euclid_h(P, P.start_cx, P.start_cy);
+    c.nm_f[(size_t)P.start_cx * c.N + P.start_cy] = euclid_h(P, P.start_cx, P.start_cy);
     Succ s0;
     s0.x = P.start_x;
     s0.y = P.start_y;
@@ -1420,7 +1470,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     s0.cx = P.start_cx;
     s0.cy = P.start_cy;
     if (kWide && !(dbg & 1)) {  // the latency kernel starts in its LDS tree
-      RBT<LdsAcc3> lt = lds_tree(*ol, A);
+      RBT<LdsAcc3> lt = lds_tree(*ol, c);
       lt.clear();
       insert3(c, lt, s0, FLT_MAX, NIL, OUTER_LDS_CAP);
     } else {
@@ -1473,7 +1523,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     // the latency kernel keeps the outer tree in LDS while it fits (a resumed search moves
     // its tree in when it does), then continues in HBM
     if ((!resume || lds_outer_load(c, *ol, lane)) && !(dbg & 1)) {
-      RBT<LdsAcc3> lt = lds_tree(*ol, A);
+      RBT<LdsAcc3> lt = lds_tree(*ol, c);
       code = search_loop<CF, true>(c, lt, apfs, alds, S, hard_pops, closed_lim, open_lim, OUTER_LDS_CAP);
       if (code == LOOP_MIGRATE) lds_outer_store(c, *ol, lane);
     }
@@ -1512,7 +1562,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
       R->ps3_next = c.ps3.next;
       R->ps3_free = c.ps3.free;
       R->parks = parks + 1;
-      R->park_arena = (int)blockIdx.x;
+      R->park_arena = c.slot;
       R->ok = 0;
       R->path_len = 0;
       R->status = SEARCH_PARKED;
@@ -1527,7 +1577,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
   int path_len = 0;
   if (ok) {
     int L = 0;
-    for (int i = terminal; i != NIL; i = gp(A.closed3)[i].prev) {
+    for (int i = terminal; i != NIL; i = c.closed3[i].prev) {
       if (dub_n + L >= P.out_cap || L >= A.chain_cap) { c.status = -28; break; }
       if (lane == 0) gp(A.out_chain)[L] = i;
       ++L;
@@ -1547,7 +1597,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
           kc = gp(A.dub_curv)[q];
         } else {
           const int m = k - dub_n;
-          const Closed3 nd = gload(&gp(A.closed3)[gp(A.out_chain)[m]]);
+          const Closed3 nd = gload(&c.closed3[gp(A.out_chain)[m]]);
           px = nd.x;
           py = nd.y;
           ph = nd.h;
@@ -1573,7 +1623,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
 
   // ---- statistics: closed-set digest (order independent) and counters
   uint64_t cd = 0;
-  for (int i = lane; i < c.n_closed3; i += 64) cd += mix64(digest_key(gp(A.closed3)[i].key));
+  for (int i = lane; i < c.n_closed3; i += 64) cd += mix64(digest_key(c.closed3[i].key));
   cd = wave_sum_u64(cd);
   wave_lds_sync();
   STAMP_ADD(5, trc);
@@ -1598,7 +1648,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     R->astar_pops_hbm = c.apops_g;
     R->t_start = t_start;
     R->t_end = __builtin_amdgcn_s_memrealtime();
-    R->slot = (int)blockIdx.x;
+    R->slot = c.slot;
     R->parks = parks;
 #ifdef HASTAR_STAMPS
     c.cyc[22] = c.o3.n_fill;
@@ -1616,65 +1666,34 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
   return false;
 }
 
-// Persistent work-queue kernel: grid = W resident slots (one wavefront each).  Each slot
-// pulls planner indices (in `order`, longest-expected-first when the host knows) from a
-// device counter until the queue is drained, so early finishers take the next planner.
-// resume = 1: wave b continues parked planner order[b] in arena b (no queue).
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HASTAR_WAVES_PER_EU))) void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners,
-                                                           const SlotArena* __restrict__ arenas,
-                                                           const int* __restrict__ order, int* __restrict__ next,
-                                                           long long hard_pops, int n_prio, int iso, int resume) {
-  __shared__ ApfStage apfs;
-  __shared__ AStarLdsT<NarrowA> alds;
+// Persistent work-queue kernel: one workgroup of 8 independent search wavefronts per CU, each
+// with its own 20 KB slice of the CU's LDS (the workgroup takes the CU's whole LDS, so a
+// latency-kernel workgroup of a split launch can only land on a CU this kernel left free).
+// Wave w of workgroup b is slot s = 8 b + w and runs in arena s (slots >= n_slots take no
+// work); it pulls planner indices (in `order`, longest-expected-first when the host knows)
+// from a device counter until the queue is drained, so early finishers take the next planner.
+constexpr int BATCH_WAVES = 8;
+__global__ __launch_bounds__(64 * BATCH_WAVES) __attribute__((amdgpu_waves_per_eu(HASTAR_WAVES_PER_EU)))
+void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners, const SlotArena* __restrict__ arenas,
+                          int n_slots, const int* __restrict__ order, int* __restrict__ next, long long hard_pops,
+                          int n_prio, int arena_base) {
+  __shared__ ApfStage apfs[BATCH_WAVES];
+  __shared__ AStarLdsT<NarrowA> alds[BATCH_WAVES];
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
+  const int slot = (int)blockIdx.x * BATCH_WAVES + w;
+  if (slot >= n_slots) return;  // a whole wave: no arena for it
   SearchCtx c;
-  c.A = arenas + blockIdx.x;
+  c.A = arenas + slot;
+  c.slot = arena_base + slot;
   const SlotArena& A = *c.A;
-  c.lane = threadIdx.x;
+  c.lane = (int)(threadIdx.x & 63);
   c.cost_only = true;
   c.gen3 = gp(A.gens)[0];
   c.gen2 = gp(A.gens)[1];
-  if (resume) {
-    if ((int)blockIdx.x < n_planners) {
-      c.P = descs + order[blockIdx.x];
-      search_one<NarrowA, false>(c, apfs, alds, nullptr, hard_pops, true);
-    }
-    if (c.lane == 0) {
-      gp(A.gens)[0] = c.gen3;
-      gp(A.gens)[1] = c.gen2;
-    }
-    return;
-  }
-  // Head isolation (iso = 1: SIMD, 2: CU).  Slot 0 runs queue entry 0, the longest expected
-  // search, and publishes its placement (HW_ID bits 4-15: SIMD, CU, SH, SE; XCC_ID); the
-  // other waves wait for that (bounded), and the ones sharing its SIMD / CU take no work,
-  // so the batch's critical search does not share issue slots.
-  bool first = true;
-  if (iso) {
-    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
-    const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
-    const uint32_t key = (((hw >> 4) & 0xfffu) & (iso == 2 ? ~0x3u : ~0u)) | (xcc << 12);
-    if (blockIdx.x == 0) {
-      if (c.lane == 0) __hip_atomic_store(&next[1], (int)(key + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      int head = 0;
-      for (int spin = 0; spin < 20000; ++spin) {
-        head = __hip_atomic_load(&next[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        head = __builtin_amdgcn_readfirstlane(head);
-        if (head != 0) break;
-        __builtin_amdgcn_s_sleep(8);
-      }
-      if (head == (int)(key + 1)) return;  // shares the head's SIMD / CU: no work
-    }
-  }
   for (;;) {
     int q = 0;
-    if (iso && first && blockIdx.x == 0) {
-      q = 0;
-    } else {
-      if (c.lane == 0) q = atomicAdd(next, 1);
-      q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
-    }
-    first = false;
+    if (c.lane == 0) q = atomicAdd(next, 1);
+    q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
     if (q >= n_planners) break;
     // the queue is ordered longest-expected-first; the head of it runs at raised issue
     // priority so the batch's stragglers are not slowed by the waves sharing their SIMD
@@ -1682,7 +1701,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HASTAR_WAVES
     else __builtin_amdgcn_s_setprio(0);
     c.P = descs + order[q];
     // a parked search keeps its state in this wave's arena: the wave takes no more work
-    if (search_one<NarrowA, false>(c, apfs, alds, nullptr, hard_pops, false)) break;
+    if (search_one<NarrowA, false>(c, apfs[w], alds[w], nullptr, hard_pops, false)) break;
   }
   if (c.lane == 0) {
     gp(A.gens)[0] = c.gen3;
@@ -1710,10 +1729,12 @@ template <class CF>
 __global__ __launch_bounds__(64) void hastar_search_wide_kernel(const PlannerDev* __restrict__ descs, int n_planners,
                                                                 const SlotArena* __restrict__ arenas,
                                                                 const int* __restrict__ order, int* __restrict__ next,
-                                                                long long hard_pops, int resume, int dbg) {
+                                                                long long hard_pops, int resume, int dbg,
+                                                                int arena_base, int first_static) {
   __shared__ WideLdsT<CF> W;
   SearchCtx c;
   c.A = arenas + blockIdx.x;
+  c.slot = arena_base + (int)blockIdx.x;
   const SlotArena& A = *c.A;
   c.lane = threadIdx.x;
   c.cost_only = true;
@@ -1725,10 +1746,16 @@ __global__ __launch_bounds__(64) void hastar_search_wide_kernel(const PlannerDev
       search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, true, dbg);
     }
   } else {
-    for (;;) {
+    // first_static: workgroup b runs queue entry b first (the head of a longest-first queue
+    // split over this kernel and the batch kernel, whose counter starts after the head)
+    for (bool first = true;; first = false) {
       int q = 0;
-      if (c.lane == 0) q = atomicAdd(next, 1);
-      q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
+      if (first && first_static) {
+        q = (int)blockIdx.x;
+      } else {
+        if (c.lane == 0) q = atomicAdd(next, 1);
+        q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
+      }
       if (q >= n_planners) break;
       c.P = descs + order[q];
       if (search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, false, dbg)) break;
@@ -1755,6 +1782,7 @@ __global__ __launch_bounds__(64) void k_astar_query(const PlannerDev* __restrict
   c.P = P;
   c.A = arena;
   c.lane = threadIdx.x;
+  bind_hot(c);
   c.cost_only = (mode & 2) != 0;
   c.gen2 = gp(arena->gens)[1];
   c.asearch = c.apops = c.amigr = c.apops_g = 0;
@@ -2365,13 +2393,16 @@ __global__ __launch_bounds__(64) void k_test_dubins_path(PlannerDev P, float sx,
 
 // ------------------------------------------------------------- launch wrappers -------
 hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots, const int* d_order, int n_prio,
-                         int* d_next, long long hard_pops, int iso, hipStream_t st) {
-  // work counter 0 (1 with isolation: slot 0 takes queue entry 0 itself), no head yet
-  const int init[4] = {iso ? 1 : 0, 0, 0, 0};
-  hipError_t e = hipMemcpyAsync(d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(hastar_search_kernel, dim3(n_slots), dim3(64), 0, st, d_descs, n, d_arenas, d_order, d_next,
-                     hard_pops, n_prio, iso, 0);
+                         int* d_next, long long hard_pops, hipStream_t st, int arena_base, int q0) {
+  // work counter q0 (>= 0: reset it; -1: the caller set it)
+  if (q0 >= 0) {
+    const int init[4] = {q0, 0, 0, 0};
+    hipError_t e = hipMemcpyAsync(d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+  }
+  const int groups = (n_slots + BATCH_WAVES - 1) / BATCH_WAVES;
+  hipLaunchKernelGGL(hastar_search_kernel, dim3(groups), dim3(64 * BATCH_WAVES), 0, st, d_descs, n, d_arenas, n_slots,
+                     d_order, d_next, hard_pops, n_prio, arena_base);
   return hipGetLastError();
 }
 // HASTAR_WIDE_DBG (diagnostics): bit 0 keeps the latency kernel's outer tree in HBM
@@ -2380,8 +2411,9 @@ static int wide_dbg() {
   return e ? std::atoi(e) : 0;
 }
 static void launch_wide_cf(dim3 g, hipStream_t st, const PlannerDev* d, int n, const SlotArena* a, const int* o,
-                           int* nx, long long hp, int resume, int dbg) {
-  hipLaunchKernelGGL(hastar_search_wide_kernel<WideA>, g, dim3(64), 0, st, d, n, a, o, nx, hp, resume, dbg);
+                           int* nx, long long hp, int resume, int dbg, int first_static = 0) {
+  hipLaunchKernelGGL(hastar_search_wide_kernel<WideA>, g, dim3(64), 0, st, d, n, a, o, nx, hp, resume, dbg, 0,
+                     first_static);
 }
 hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, const int* d_order,
                          long long hard_pops, hipStream_t st) {
@@ -2391,17 +2423,22 @@ hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_ar
   return hipGetLastError();
 }
 hipError_t launch_search_wide(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots,
-                              const int* d_order, int* d_next, long long hard_pops, hipStream_t st) {
-  const int init[4] = {0, 0, 0, 0};
-  hipError_t e = hipMemcpyAsync(d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
-  if (e != hipSuccess) return e;
-  launch_wide_cf(dim3(n_slots), st, d_descs, n, d_arenas, d_order, d_next, hard_pops, 0, wide_dbg());
+                              const int* d_order, int* d_next, long long hard_pops, hipStream_t st, int head) {
+  // head = 0: the whole queue (counter reset to 0); head = 1: the head of a split queue
+  // (workgroup b takes entry b first; the caller set the counter past the head)
+  if (!head) {
+    const int init[4] = {0, 0, 0, 0};
+    hipError_t e = hipMemcpyAsync(d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+  }
+  launch_wide_cf(dim3(n_slots), st, d_descs, n, d_arenas, d_order, d_next, hard_pops, 0, wide_dbg(), head);
   return hipGetLastError();
 }
 int search_slots_per_cu() {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, hastar_search_kernel, 64, 0) != hipSuccess) return 1;
-  return nb > 0 ? nb : 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, hastar_search_kernel, 64 * BATCH_WAVES, 0) != hipSuccess)
+    return 1;
+  return (nb > 0 ? nb : 1) * BATCH_WAVES;
 }
 hipError_t launch_gather_paths(const PlannerDev* d_descs, const long long* d_off, const int* d_len, int n, float* xyh,
                                float* curv, hipStream_t st) {

@@ -52,6 +52,7 @@ def load_library():
     L.hastar_update_goal.argtypes = [vp, fp, fp]
     L.hastar_reset.argtypes = [vp]
     L.hastar_reset_batch.argtypes = [C.POINTER(C.c_void_p), C.c_int]
+    L.hastar_set_cost_hint.argtypes = [vp, C.c_longlong]
     L.hastar_update_boxes.argtypes = [vp, fp, fp, C.c_int, C.c_float]
     L.hastar_update_lines.argtypes = [vp, fp, fp, C.c_int, C.c_float]
     L.hastar_decay.argtypes = [vp]
@@ -234,6 +235,11 @@ class HybridAStar:
     def reset(self):
         _check(load_library().hastar_reset(self.h))
 
+    def set_cost_hint(self, hint):
+        """Longest-first key of this planner's next batched search (hastar_set_cost_hint; the
+        library sets it to each search's duration; 0 = unknown)."""
+        _check(load_library().hastar_set_cost_hint(self.h, int(hint)))
+
     # the three update_obstacles overloads (HybridAStar.cpp:29-46)
     def update_obstacles(self, items=None, confidence=None, size=None, kind="boxes"):
         if items is None:
@@ -376,9 +382,10 @@ class HybridAStar:
 
     def slots(self):
         """Search-slot pool of this planner's device (after a find_path)."""
-        out = (C.c_longlong * 4)()
+        out = (C.c_longlong * 5)()
         _check(load_library().hastar_debug_slots(self.h, out))
-        return {"resident_slots": out[0], "waves_per_cu": out[1], "arenas": out[2], "arena_mib": out[3]}
+        return {"resident_slots": out[0], "waves_per_cu": out[1], "arenas": out[2], "arena_mib": out[3],
+                "head_cus": out[4]}
 
     def timing(self):
         """(t_start, t_end, slot) of the last search; times in 10 ns ticks."""

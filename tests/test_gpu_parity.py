@@ -250,10 +250,12 @@ def test_reset_batch_equals_reset(gpu, oracle_lib):
         assert (vg == vo).all()
 
 
-def test_batch_with_head_isolation(gpu, oracle_lib, monkeypatch):
-    """HASTAR_ISO=2 (slot 0 runs the queue head; waves sharing its CU take no work) and
-    fewer slots than planners: every result is still the oracle's."""
-    monkeypatch.setenv("HASTAR_ISO", "2")
+@pytest.mark.parametrize("wide", ["1", "0"], ids=["latency_kernel", "batch_kernel"])
+def test_batch_with_fewer_slots(gpu, oracle_lib, monkeypatch, wide):
+    """Fewer slots than planners (3 latency workgroups, or 3 waves of one batch-kernel
+    workgroup whose 5 other waves take no work): the persistent queue hands every planner to
+    a slot, and every result is still the oracle's."""
+    monkeypatch.setenv("HASTAR_WIDE", wide)
     monkeypatch.setenv("HASTAR_SLOTS", "3")
     cases = [synthetic(128, 36, 6, s) for s in (31, 32, 33, 34, 35, 36, 37)]
     gs, os_ = [], []
@@ -265,7 +267,7 @@ def test_batch_with_head_isolation(gpu, oracle_lib, monkeypatch):
         os_.append(o)
     res, _ = gpu.find_path_batch(gs, [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases])
     for i, ((cfg, proto), o) in enumerate(zip(cases, os_)):
-        compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"iso batch {i}")
+        compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"3-slot batch {i}")
 
 
 @pytest.mark.parametrize("wide", ["1", "0"], ids=["latency_kernel", "batch_kernel"])

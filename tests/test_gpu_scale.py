@@ -158,6 +158,26 @@ def test_cfg3_parity_batch(gpu, oracle_lib, monkeypatch, wide):
     assert max(r["stats"]["pops"] for r in res) > 100000  # the long query is in the batch
 
 
+def test_split_launch_head_and_bulk(gpu, oracle_lib, monkeypatch):
+    """A batch split over both kernels at once (HASTAR_SPLIT, as large batches run): the head of
+    the queue on the latency CUs, the rest on the batch kernel beside them, one work counter.
+    Every planner's result is the oracle's, and both kernels took work."""
+    monkeypatch.setenv("HASTAR_WIDE", "0")
+    monkeypatch.setenv("HASTAR_SPLIT", "1")
+    cases = [synthetic(256, 36, 10 + (s % 4) * 10, s) for s in range(1, 25)] + [synthetic(512, 72, 50, 1)]
+    gs, os_ = [], []
+    for cfg, proto in cases:
+        g, o = _pair(gpu, oracle_lib, cfg, proto)
+        gs.append(g)
+        os_.append(o)
+    res, _ = gpu.find_path_batch(gs, [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases], cap=8192)
+    for i, ((cfg, proto), o) in enumerate(zip(cases, os_)):
+        compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"split launch planner {i}")
+    slots = {int(g.timing()[2]) for g in gs}
+    head = gs[0].slots()["head_cus"]
+    assert any(s < head for s in slots) and any(s >= head for s in slots), (slots, head)
+
+
 @pytest.mark.parametrize("wide", KERNELS)
 def test_cfg3_survey_reference_cases(gpu, oracle_lib, monkeypatch, wide):
     """The survey's own cases, 256² to 2048² including cfg3 seeds 1 and 3 (std::mt19937 inputs,
@@ -300,7 +320,8 @@ def test_velocity_last_batch_with_short_caller_buffer(gpu, oracle_lib):
     cap = int(lens[0]) - 1  # planner 0's path does not fit; the others do
     assert (lens[1:] <= cap).all(), lens
     res, _ = gpu.find_path_batch(gs, vels, starts, cap=cap)
-    assert res[0]["stats"]["status"] == gpu.HASTAR_ENOSPC and len(res[0]["path"]) == lens[0]
+    # (find_path_batch fetched the long path with copy_path and cleared its ENOSPC status)
+    assert res[0]["stats"]["status"] == 0 and len(res[0]["path"]) == lens[0]
     prm = (10.0, 3.0, 2.5, 1.5, 3.0)
     v0 = np.asarray(vels, np.float32)
     feas, vel = gpu.VelocityGenerator(*prm).profile_last_batch(lens, v0, np.full(3, 10.0, np.float32),
