@@ -110,6 +110,13 @@ int hastar_reset_batch(const hastar_handle* hs, int n);
  * CUs. */
 int hastar_set_cost_hint(hastar_handle h, long long hint);
 
+/* Device pool reservation (no counterpart in the reference): sizes the device context's search
+ * arenas, batch tables and, when path_points > 0, the packed-path buffers for a batched
+ * find_path of these n planners, so that the batch's first call allocates nothing.  Optional:
+ * find_path grows the pool itself.  Same errors as hastar_find_path_batch (HASTAR_ENOMEM when
+ * the pool cannot be had). */
+int hastar_reserve(const hastar_handle* hs, int n, long long path_points);
+
 /* update_obstacles(obstacles, confidence, apf_added_radius) (HybridAStar.cpp:29-33):
  * boxes = n x {center_x, center_y, dimension_x, dimension_y} (Obstacle.h:16-21). */
 int hastar_update_boxes(hastar_handle h, const float* boxes, const float* confidence, int n,

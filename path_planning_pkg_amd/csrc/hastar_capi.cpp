@@ -1497,6 +1497,59 @@ static int copy_path_out(hastar_handle h, float* xyh, float* curv, int cap, int*
 }
 
 // per-batch device/pinned buffers (descriptors, order, results, path offsets), grown on demand
+// The arena requirement of a batch (every planner's), after checking the handles.
+static int batch_need(const hastar_handle* hs, int n, ArenaReq* need) {
+  const int dev = hs[0] ? hs[0]->device : -1;
+  for (int i = 0; i < n; ++i) {
+    if (!hs[i] || hs[i]->device != dev) return fail(HASTAR_EINVAL, "null handle or handles on different devices");
+    if (!hs[i]->goal_set) return fail(HASTAR_EINVAL, "update_goal must be called before find_path");
+    need->merge(hs[i]->areq);
+  }
+  return 0;
+}
+
+// How a batch of n planners is launched, and the slot arenas it needs (W).
+struct BatchShape {
+  bool wide, split;
+  int head, per_cu, W;
+};
+static BatchShape batch_shape(const DeviceCtx& DC, int n) {
+  BatchShape b{};
+  // A batch no larger than the CU count runs on the latency kernel: one search per CU with the
+  // CU's whole LDS (outer open tree, 2048-node holonomic pool) and its SIMD to itself.  Larger
+  // batches fill every CU with 8 searches (the batch kernel).  HASTAR_WIDE=0/1 forces either.
+  b.wide = n <= DC.n_cu;
+  if (const char* e = std::getenv("HASTAR_WIDE")) b.wide = std::atoi(e) != 0;
+  // A batch many times the CU count splits: its head (the longest expected searches, first in
+  // the queue) on `head_cus` latency CUs, the bulk on the batch kernel beside them.
+  // HASTAR_SPLIT=0/1 forces it off/on.
+  b.split = !b.wide && DC.head_cus > 0 && n > 4 * DC.n_cu;
+  if (const char* e = std::getenv("HASTAR_SPLIT")) b.split = !b.wide && DC.head_cus > 0 && std::atoi(e) != 0;
+  b.head = b.split ? std::min(DC.head_cus, n) : 0;
+  b.per_cu = DC.resident_slots / DC.n_cu;  // batch-kernel waves per CU
+  b.W = std::max(1, std::min(n, b.wide ? DC.n_cu : b.split ? b.head + (DC.n_cu - b.head) * b.per_cu
+                                                           : DC.resident_slots));
+  if (const char* e = std::getenv("HASTAR_SLOTS")) b.W = std::max(1, std::min(b.W, std::atoi(e)));
+  return b;
+}
+
+// Room for `pts` packed path points of a batch (device and pinned host copies).
+static hipError_t points_acquire(DeviceCtx& DC, size_t pts) {
+  if (pts <= DC.pts_cap) return hipSuccess;
+  if (DC.d_pxyh) hipFree(DC.d_pxyh);
+  if (DC.d_pcurv) hipFree(DC.d_pcurv);
+  if (DC.h_pxyh) hipHostFree(DC.h_pxyh);
+  if (DC.h_pcurv) hipHostFree(DC.h_pcurv);
+  DC.d_pxyh = DC.d_pcurv = DC.h_pxyh = DC.h_pcurv = nullptr;
+  DC.pts_cap = 0;
+  hipError_t e = dalloc(&DC.d_pxyh, pts * 3);
+  if (e == hipSuccess) e = dalloc(&DC.d_pcurv, pts);
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&DC.h_pxyh), pts * 3 * sizeof(float));
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&DC.h_pcurv), pts * sizeof(float));
+  if (e == hipSuccess) DC.pts_cap = pts;
+  return e;
+}
+
 static int batch_acquire(DeviceCtx& DC, int n) {
   hipStream_t st = DC.stream;
   if (n <= DC.batch_cap) return 0;
@@ -1584,20 +1637,7 @@ static int finish_batch(DeviceCtx& DC, const hastar_handle* hs, int n, float* xy
   // this batch never reads a previous batch's offsets
   HIPCHK(hipMemcpyAsync(DC.d_off, h_off, ((size_t)n + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
   if (total > 0) {
-    if ((size_t)total > DC.pts_cap) {
-      if (DC.d_pxyh) hipFree(DC.d_pxyh);
-      if (DC.d_pcurv) hipFree(DC.d_pcurv);
-      if (DC.h_pxyh) hipHostFree(DC.h_pxyh);
-      if (DC.h_pcurv) hipHostFree(DC.h_pcurv);
-      DC.d_pxyh = DC.d_pcurv = DC.h_pxyh = DC.h_pcurv = nullptr;
-      DC.pts_cap = 0;
-      const size_t c2 = (size_t)total + (size_t)total / 2 + 1024;
-      HIPCHK(dalloc(&DC.d_pxyh, c2 * 3));
-      HIPCHK(dalloc(&DC.d_pcurv, c2));
-      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_pxyh), c2 * 3 * sizeof(float)));
-      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&DC.h_pcurv), c2 * sizeof(float)));
-      DC.pts_cap = c2;
-    }
+    if ((size_t)total > DC.pts_cap) HIPCHK(points_acquire(DC, (size_t)total + (size_t)total / 2 + 1024));
     HIPCHK(hipMemcpyAsync(DC.d_len, h_len, (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
     HIPCHK(launch_gather_paths(DC.d_descs, DC.d_off, DC.d_len, n, DC.d_pxyh, DC.d_pcurv, st));
     HIPCHK(hipMemcpyAsync(DC.h_pxyh, DC.d_pxyh, (size_t)total * 3 * sizeof(float), hipMemcpyDeviceToHost, st));
@@ -1614,6 +1654,19 @@ static int finish_batch(DeviceCtx& DC, const hastar_handle* hs, int n, float* xy
 
 extern "C" {
 
+int hastar_reserve(const hastar_handle* hs, int n, long long path_points) {
+  if (!hs || n <= 0 || path_points < 0) return fail(HASTAR_EINVAL, "bad argument");
+  ArenaReq need;
+  if (int rc = batch_need(hs, n, &need)) return rc;
+  HIPCHK(hipSetDevice(hs[0]->device));
+  DeviceCtx& DC = *hs[0]->dc;
+  std::lock_guard<std::mutex> lk(DC.mu);
+  if (int rc = arenas_acquire(DC, need, batch_shape(DC, n).W)) return rc;
+  if (int rc = batch_acquire(DC, n)) return rc;
+  if (path_points > 0) HIPCHK(points_acquire(DC, (size_t)path_points));
+  return 0;
+}
+
 int hastar_find_path(hastar_handle h, float vel, const float start[3], float* xyh, float* curv, int cap, int* len,
                      float* cost, int* ok, hastar_stats* stats) {
   return hastar_find_path_batch(&h, 1, &vel, start, xyh, curv, cap, len, cost, ok, stats);
@@ -1623,31 +1676,15 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
                            float* curv, int cap, int* len, float* cost, int* ok, hastar_stats* stats) {
   if (!hs || n <= 0 || !vel || !starts || !len || !cost || !ok || cap < 0 || (cap > 0 && (!xyh || !curv)))
     return fail(HASTAR_EINVAL, "bad argument");
-  const int dev = hs[0] ? hs[0]->device : -1;
   ArenaReq need;
-  for (int i = 0; i < n; ++i) {
-    if (!hs[i] || hs[i]->device != dev) return fail(HASTAR_EINVAL, "null handle or handles on different devices");
-    if (!hs[i]->goal_set) return fail(HASTAR_EINVAL, "update_goal must be called before find_path");
-    need.merge(hs[i]->areq);
-  }
-  HIPCHK(hipSetDevice(dev));
+  if (int rc = batch_need(hs, n, &need)) return rc;
+  HIPCHK(hipSetDevice(hs[0]->device));
   DeviceCtx& DC = *hs[0]->dc;
   std::lock_guard<std::mutex> lk(DC.mu);
   hipStream_t st = DC.stream;
-  // A batch no larger than the CU count runs on the latency kernel: one search per CU with the
-  // CU's whole LDS (outer open tree, 2048-node holonomic pool) and its SIMD to itself.  Larger
-  // batches fill every CU with 8 searches (the batch kernel).  HASTAR_WIDE=0/1 forces either.
-  bool wide = n <= DC.n_cu;
-  if (const char* e = std::getenv("HASTAR_WIDE")) wide = std::atoi(e) != 0;
-  // A batch many times the CU count splits: its head (the longest expected searches, first in
-  // the queue) on `head_cus` latency CUs, the bulk on the batch kernel beside them.
-  // HASTAR_SPLIT=0/1 forces it off/on.
-  bool split = !wide && DC.head_cus > 0 && n > 4 * DC.n_cu;
-  if (const char* e = std::getenv("HASTAR_SPLIT")) split = !wide && DC.head_cus > 0 && std::atoi(e) != 0;
-  const int head = split ? std::min(DC.head_cus, n) : 0;
-  const int per_cu = DC.resident_slots / DC.n_cu;  // batch-kernel waves per CU
-  int W = std::max(1, std::min(n, wide ? DC.n_cu : split ? head + (DC.n_cu - head) * per_cu : DC.resident_slots));
-  if (const char* e = std::getenv("HASTAR_SLOTS")) W = std::max(1, std::min(W, std::atoi(e)));
+  const BatchShape bs = batch_shape(DC, n);
+  const bool wide = bs.wide, split = bs.split;
+  const int head = bs.head, per_cu = bs.per_cu, W = bs.W;
   if (int rc = arenas_acquire(DC, need, W)) return rc;
   const int slots = std::min(W, DC.n_arenas);
   if (int rc = batch_acquire(DC, n)) return rc;

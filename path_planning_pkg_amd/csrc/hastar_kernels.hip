@@ -29,7 +29,8 @@ static_assert(64 / 4 >= MAXS, "4 lanes per candidate action must cover MAXS acti
 // 0 pop+closed insert, 1 successors+APF+Dubins, 2 open/closed bookkeeping, 3 holonomic A*,
 // 4 Dubins shot, 5 reconstruct+stats, 6 whole loop, 7 A* in HBM mode, 8-12 LDS A* pop /
 // find / insert / unlink-hit / memoise, 13-15 outer find / insert / unlink, 16-18 successor
-// generation / APF / Dubins lengths, 19-20 outer insert walk / link.
+// generation / APF / Dubins lengths, 19-20 outer insert walk / link, 24 LDS A* pop unlink,
+// 25 LDS A* insert link, 30 LDS A* ring insert, 31 LDS A* expansion stores.
 #ifdef HASTAR_STAMPS
 #define STAMP_T unsigned long long
 #define STAMP_NOW() __builtin_amdgcn_s_memtime()
@@ -673,8 +674,12 @@ __device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AS
   const int n = tpool_alloc(tr, c.ps2, CF::CAP);
   if (n == NIL) return false;
   tr.payload(n, key, fn, gn, prev);
+  STAMP_T t_l = STAMP_NOW();
   tr.link(left, n, parent);
+  STAMP_ADD(25, t_l);
+  STAMP_T t_r = STAMP_NOW();
   ring_insert(L, rg, rb.r, n, c.lane);
+  STAMP_ADD(30, t_r);
   *node_out = n;
   return true;
 }
@@ -771,7 +776,9 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
     // this lane's hinted open node (the node a find of this cell usually returns); its g came
     // with the probe (hg), and a node's g never changes while it is open
     const int hy = (ohint != 0xffffffffu && !((ohint >> 16) & 1u)) ? (int)(ohint & 0xffffu) : NIL;
+    STAMP_T t_u = STAMP_NOW();
     tr.unlink(b);
+    STAMP_ADD(24, t_u);
     free_lds(c, tr, b);
     ring_erase(L, rg, 0, lane);
     const int ci = (int)tcell;  // closed record = the cell's record
@@ -902,6 +909,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
         }
       }
     }
+    STAMP_T t_e = STAMP_NOW();
     if (st_on) {
       c.nm_f[st_cell] = st_f;
       if (st_node != NIL) {
@@ -910,6 +918,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
       }
     }
     wave_lds_sync();
+    STAMP_ADD(31, t_e);
   }
   *result = FLT_MAX;
   return true;

@@ -53,6 +53,7 @@ def load_library():
     L.hastar_reset.argtypes = [vp]
     L.hastar_reset_batch.argtypes = [C.POINTER(C.c_void_p), C.c_int]
     L.hastar_set_cost_hint.argtypes = [vp, C.c_longlong]
+    L.hastar_reserve.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_longlong]
     L.hastar_update_boxes.argtypes = [vp, fp, fp, C.c_int, C.c_float]
     L.hastar_update_lines.argtypes = [vp, fp, fp, C.c_int, C.c_float]
     L.hastar_decay.argtypes = [vp]
@@ -453,6 +454,14 @@ class BatchBuffers:
         self.cost = np.zeros(n, np.float32)
         self.stats = (HastarStats * n)()
         self.st = np.ctypeslib.as_array(self.stats)
+
+
+def reserve(planners, path_points=0):
+    """hastar_reserve: size the device pool (search arenas, batch tables, packed-path buffers of
+    `path_points` points) for a batched find_path of these planners, ahead of its first call."""
+    n = len(planners)
+    hs = (C.c_void_p * n)(*[p.h.value for p in planners])
+    _check(load_library().hastar_reserve(hs, n, int(path_points)))
 
 
 def reset_batch(planners_or_buffers):

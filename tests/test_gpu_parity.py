@@ -270,6 +270,25 @@ def test_batch_with_fewer_slots(gpu, oracle_lib, monkeypatch, wide):
         compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"3-slot batch {i}")
 
 
+def test_reserve_then_batch(gpu, oracle_lib):
+    """hastar_reserve sizes the device pool ahead of a batch (and rejects bad arguments); the
+    batch that follows still returns the oracle's results."""
+    cases = [synthetic(128, 36, 6, s) for s in (41, 42, 43)]
+    gs, os_ = [], []
+    for cfg, proto in cases:
+        g, o = both(cfg, gpu, oracle_lib)
+        drive(g, proto)
+        drive(o, proto)
+        gs.append(g)
+        os_.append(o)
+    with pytest.raises(gpu.HastarError):
+        gpu.reserve(gs, path_points=-1)
+    gpu.reserve(gs, path_points=4096)
+    res, _ = gpu.find_path_batch(gs, [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases])
+    for i, ((cfg, proto), o) in enumerate(zip(cases, os_)):
+        compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"reserved batch {i}")
+
+
 @pytest.mark.parametrize("wide", ["1", "0"], ids=["latency_kernel", "batch_kernel"])
 def test_batch_equals_single(gpu, oracle_lib, monkeypatch, wide):
     monkeypatch.setenv("HASTAR_WIDE", wide)

@@ -18,7 +18,7 @@ for st in "$@"; do
              || { tail -40 $O/pytest_gpu.txt; exit 1; }; tail -2 $O/pytest_gpu.txt ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { tail -20 $O/smoke.txt; exit 1; }
            tail -1 $O/smoke.txt ;;
-    bench) timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+    bench) timeout -k 10 900 python -u bench.py --dump-timings $O/timings.npz > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
            cut -c1-400 $O/bench.json ;;
     cfg5)  timeout -k 10 600 python -u bench.py --workload cfg5 > $O/bench_cfg5.json 2> $O/bench_cfg5.err || { tail -30 $O/bench_cfg5.err; exit 1; }
            cut -c1-400 $O/bench_cfg5.json ;;

@@ -48,6 +48,9 @@ for s in args.seeds:
                           lds_astar_per_apop={n: round(cyc[8 + i] / max(st["astar_pops"] - modes["astar_pops_hbm"], 1))
                                               for i, n in enumerate(["pop_probe", "find", "insert", "unlink_hit",
                                                                      "memoise"])},
+                          lds_astar_parts_per_apop={n: round(cyc[i] / max(st["astar_pops"] - modes["astar_pops_hbm"], 1))
+                                                    for i, n in ((24, "pop_unlink"), (25, "insert_link"),
+                                                                 (30, "ring_insert"), (31, "expansion_stores"))},
                           outer_per_pop={n: round(cyc[13 + i] / max(st["pops"], 1))
                                          for i, n in enumerate(["find3", "insert3", "unlink3", "succ_gen", "apf",
                                                                 "dubins", "insert_walk", "insert_link",
