@@ -277,6 +277,8 @@ def main():
         achieved = float(np.mean(alg_bytes)) / (avg_kernel_ms * 1e-3) / 1e9
         balance = step_balance(planners)  # before any other find_path overwrites the timings
         balance["pool"] = planners[0].slots()
+        balance["split_launch_ms"] = dict(zip(("head_start", "head_end", "bulk_start", "bulk_end"),
+                                              planners[0].split_ms()))
         timings = {"qids": np.asarray(qids), "pops": last.stats["pops"].copy(),
                    "astar_pops": last.stats["astar_pops"].copy(),
                    "warm": np.array([p.timing() for p in planners], dtype=np.float64)}

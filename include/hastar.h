@@ -188,6 +188,9 @@ typedef struct hastar_relaxed_opts {
                           reference's A* memo persists across replans; map updates in between
                           leave it stale (it only guides: every successor is checked against the
                           current map) [0: recompute per call] */
+  int h_coarse;    /* the Dijkstra field runs over blocks of h_coarse x h_coarse map cells (1, 2 or 4):
+                      a block is passable when any of its cells is, and a cell's heuristic is its
+                      block's distance [2] */
 } hastar_relaxed_opts;
 int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, const float* vel_init, const float* starts,
                                    float* xyh, float* curv, int cap, int* len, float* cost, int* ok,

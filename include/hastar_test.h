@@ -37,6 +37,9 @@ int hastar_debug_timing(hastar_handle h, unsigned long long* out3);
 /* Search-slot pool of the handle's device: {resident wavefronts, search waves per CU, arenas, MiB per arena,
    latency CUs of a split launch (0: none)}. */
 int hastar_debug_slots(hastar_handle h, long long* out5);
+/* the device's last split launch (hastar_find_path_batch of a large batch): ms from the timed
+ * region's start to the head kernel's start and end, and to the bulk kernel's start and end */
+int hastar_debug_split(hastar_handle h, float* out4);
 /* resume arenas carved from idle slot arenas of the pool so far (process-wide count) */
 int hastar_debug_pooled_resumes(long long* out);
 /* The relaxed kernel's per-wave progress words (4 per wave: phase, round, expansion-set size,

@@ -69,6 +69,7 @@ class HastarRelaxedOpts(C.Structure):
         ("max_rounds", C.c_int),
         ("h_weight", C.c_float),
         ("reuse_heuristic", C.c_int),
+        ("h_coarse", C.c_int),
     ]
 
 

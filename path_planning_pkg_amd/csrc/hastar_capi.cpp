@@ -171,7 +171,8 @@ struct DeviceCtx {
   // land on disjoint CUs whichever is dispatched first.
   int head_cus = 0;
   hipStream_t head_st = nullptr, bulk_st = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_head = nullptr, ev_bulk = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_head = nullptr, ev_bulk = nullptr, ev_hs = nullptr, ev_bs = nullptr;
+  float split_ms[4] = {0, 0, 0, 0};  // last split launch: head start / end, bulk start / end after ev0
   // map-update scratch (relocation target + claim table, raster hit counters)
   size_t scratch_cap = 0;
   float* tmp = nullptr;
@@ -262,8 +263,8 @@ int device_ctx(int dev, DeviceCtx** out) {
       if (hipStreamCreateWithFlags(&D.head_st, hipStreamNonBlocking) == hipSuccess &&
           hipStreamCreateWithFlags(&D.bulk_st, hipStreamNonBlocking) == hipSuccess &&
           hipEventCreateWithFlags(&D.ev_fork, hipEventDisableTiming) == hipSuccess &&
-          hipEventCreateWithFlags(&D.ev_head, hipEventDisableTiming) == hipSuccess &&
-          hipEventCreateWithFlags(&D.ev_bulk, hipEventDisableTiming) == hipSuccess)
+          hipEventCreate(&D.ev_head) == hipSuccess && hipEventCreate(&D.ev_bulk) == hipSuccess &&
+          hipEventCreate(&D.ev_hs) == hipSuccess && hipEventCreate(&D.ev_bs) == hipSuccess)
         D.head_cus = hc;
     }
     HIPCHK(dalloc(&D.d_next, 4));  // [0] work counter, [1] head placement, [2] head done
@@ -487,6 +488,7 @@ struct hastar_handle_s {
   bool rvalid = false;
   float rhlim = 0.0f;
   int rstart = 0;
+  int rcoarse = 0;              // the kept field's block side (a call with another one rebuilds it)
 };
 
 // One allocation for the persistent state of a batch of identical planners
@@ -1730,6 +1732,8 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
           if (e == hipSuccess) e = hipEventRecord(DC.ev_fork, st);
           if (e == hipSuccess) e = hipStreamWaitEvent(DC.head_st, DC.ev_fork, 0);
           if (e == hipSuccess) e = hipStreamWaitEvent(DC.bulk_st, DC.ev_fork, 0);
+          if (e == hipSuccess) e = hipEventRecord(DC.ev_hs, DC.head_st);
+          if (e == hipSuccess) e = hipEventRecord(DC.ev_bs, DC.bulk_st);
           if (e == hipSuccess)
             e = launch_search_wide(DC.d_descs, n, DC.d_arenas, head, DC.d_order, DC.d_next, hard_pops, DC.head_st, 1);
           if (e == hipSuccess)
@@ -1745,6 +1749,12 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
                     : launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, hard_pops, st);
       }))
     return r;
+  if (split && slots > head) {
+    hipEventElapsedTime(&DC.split_ms[0], DC.ev0, DC.ev_hs);
+    hipEventElapsedTime(&DC.split_ms[1], DC.ev0, DC.ev_head);
+    hipEventElapsedTime(&DC.split_ms[2], DC.ev0, DC.ev_bs);
+    hipEventElapsedTime(&DC.split_ms[3], DC.ev0, DC.ev_bulk);
+  }
   // Parked searches (their arena could not take one more pop) continue in larger arenas,
   // planners no wave took run in a new queue pass: until every search has ended.
   {
@@ -2016,6 +2026,8 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
   rp.h_stop = opts && opts->h_stop >= 1.0f ? opts->h_stop : 1.5f;
   rp.max_rounds = opts && opts->max_rounds > 0 ? opts->max_rounds : (1 << 20);
   rp.h_weight = opts && opts->h_weight > 0.0f ? opts->h_weight : 1.2f;
+  rp.h_coarse = opts && opts->h_coarse > 0 ? opts->h_coarse : 2;
+  if (rp.h_coarse != 1 && rp.h_coarse != 2 && rp.h_coarse != 4) return fail(HASTAR_EINVAL, "h_coarse must be 1, 2 or 4");
   const int nodes = opts && opts->max_nodes > 0 ? opts->max_nodes : (1 << 18);
   HIPCHK(hipSetDevice(dev));
   DeviceCtx& DC = *hs[0]->dc;
@@ -2046,7 +2058,7 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
         h->rfield = nullptr;
         return fail(HASTAR_ENOMEM, "relaxed heuristic field: hipMalloc failed");
       }
-      fields[i] = RelaxField{h->rfield, h->rhlim, h->rvalid ? 1 : 0, h->rstart};
+      fields[i] = RelaxField{h->rfield, h->rhlim, h->rvalid && h->rcoarse == rp.h_coarse ? 1 : 0, h->rstart};
     }
     if ((size_t)n > DC.rfields_cap) {
       HIPCHK(hipStreamSynchronize(st));
@@ -2071,6 +2083,7 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
     hs[i]->rvalid = fields[i].valid != 0;
     hs[i]->rhlim = fields[i].hlim;
     hs[i]->rstart = fields[i].start_ij;
+    hs[i]->rcoarse = rp.h_coarse;
   }
   float ms = 0.0f;
   hipEventElapsedTime(&ms, DC.ev0, DC.ev1);
@@ -2569,6 +2582,12 @@ int hastar_debug_pooled_resumes(long long* out) {
   if (!out) return fail(HASTAR_EINVAL, "null output");
   *out = g_pooled_resumes.load();
   return HASTAR_OK;
+}
+
+int hastar_debug_split(hastar_handle h, float* out4) {
+  if (!h || !out4) return fail(HASTAR_EINVAL, "bad argument");
+  for (int i = 0; i < 4; ++i) out4[i] = h->dc->split_ms[i];
+  return 0;
 }
 
 int hastar_debug_slots(hastar_handle h, long long* out5) {

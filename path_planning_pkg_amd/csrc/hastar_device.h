@@ -279,31 +279,61 @@ __device__ __forceinline__ int rl_i(int v, int L) { return __builtin_amdgcn_read
 //            sin/cos of the heading, word lanes 0..3 atan2f/acosf, lanes 4..11 the cos/sin
 //            of the RSL and LSR tangent angles — so the dependent chain is 4 calls long;
 //   gs = 4:  lane w of the group evaluates word w alone.
+// Lane L of each row of 16 lanes, to the whole row (DPP row_newbcast, a VALU move: no LDS
+// round trip).  The caller runs it with every lane of the wave active: a DPP move reads
+// `old` (here 0) from a source lane that is off in EXEC, where a ds_bpermute reads 0 too —
+// both only give the row's value under a full mask.
+template <int L>
+__device__ __forceinline__ float row_bcast(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 | L, 0xf, 0xf, false));
+}
+// Lane L or M of each row, per lane (sel): both broadcasts are materialised before the select.
+// Without the empty asm the compiler turns `sel ? bcast<L> : bcast<M>` into an if/else whose
+// arms run the moves under a partial EXEC, where a source lane of the other arm reads as 0
+// (the cause of the round-2 parity failure of this change: ISA inspection).
+template <int L, int M>
+__device__ __forceinline__ float row_bcast_sel(bool sel, float v) {
+  float a = row_bcast<L>(v), b = row_bcast<M>(v);
+  asm volatile("" : "+v"(a), "+v"(b));
+  return sel ? a : b;
+}
+
+// Called with every lane active (the row broadcasts of the 16-lane case read other lanes).
 __device__ __forceinline__ float cand_dubins(float r, const GoalC& GC, float gh, float sx, float sy, float sh, int gs,
                                             int lane) {
   const int base = lane & ~(gs - 1), sub = lane & (gs - 1), w = sub & 3;
-  float len;
-  if (gs == 16) {
+  if (gs == 16) {  // a group is a DPP row
     const float t0 = g_sincosf_sel(sh, (sub & 1) != 0);
-    const Centres C = centres_from(r, sx, sy, shfl_f(t0, base), shfl_f(t0, base + 1), GC);
+    float c0 = row_bcast<0>(t0), s0 = row_bcast<1>(t0);
+    asm volatile("" : "+v"(c0), "+v"(s0));
+    const Centres C = centres_from(r, sx, sy, c0, s0, GC);
     const WordGeo g = word_geo(w, C);
     const float th = g_atan2f(g.dy, g.dx);
     const float ac = g_acosf(word_acos_arg(r, g));  // used by RSL / LSR only
     float t1, q2;
     word_arcs(w == 2 ? 2 : 1, th, ac, &t1, &q2);
     // lanes 4..7: cos t1, sin t1, cos q2, sin q2 of RSL (word lane 1); lanes 8..11: of LSR
-    const int ws = base + ((sub >> 2) == 2 ? 2 : 1), which = sub & 3;
-    const float t1s = shfl_f(t1, ws), q2s = shfl_f(q2, ws);  // both unconditionally (no divergent shuffle)
-    const float at = which < 2 ? t1s : q2s;
-    const float tv = g_sincosf_sel(at, (which & 1) == 0);
-    const int tb = base + (w == 2 ? 8 : 4);
+    // (word lane 2); every broadcast is taken by every lane, then selected
+    const bool lsr = (sub >> 2) == 2;
+    const float t1s = row_bcast_sel<2, 1>(lsr, t1);
+    const float q2s = row_bcast_sel<2, 1>(lsr, q2);
+    const float at = (sub & 3) < 2 ? t1s : q2s;
+    const float tv = g_sincosf_sel(at, (sub & 1) == 0);
+    const bool w2 = w == 2;
+    const float c1 = row_bcast_sel<8, 4>(w2, tv), s1 = row_bcast_sel<9, 5>(w2, tv);
+    const float c2 = row_bcast_sel<10, 6>(w2, tv), s2 = row_bcast_sel<11, 7>(w2, tv);
     float q[4];
-    len = word_len(w, r, g, sh, gh, th, t1, shfl_f(tv, tb), shfl_f(tv, tb + 1), shfl_f(tv, tb + 2),
-                   shfl_f(tv, tb + 3), q);
-  } else {
-    float q[4];
-    len = dubins_word(w, r, dubins_centres_g(r, sx, sy, sh, GC), sh, gh, q);
+    const float len = word_len(w, r, g, sh, gh, th, t1, c1, s1, c2, s2, q);
+    float l0 = row_bcast<0>(len), l1 = row_bcast<1>(len), l2 = row_bcast<2>(len), l3 = row_bcast<3>(len);
+    asm volatile("" : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3));
+    float best = l0;
+    if (l1 < best) best = l1;
+    if (l2 < best) best = l2;
+    if (l3 < best) best = l3;
+    return best;
   }
+  float q[4];
+  const float len = dubins_word(w, r, dubins_centres_g(r, sx, sy, sh, GC), sh, gh, q);
   float best = shfl_f(len, base);
   for (int w2 = 1; w2 < 4; ++w2) {
     const float v = shfl_f(len, base + w2);

@@ -264,7 +264,7 @@ struct RelaxParams {
   float h_stop;     // the Dijkstra covers the ellipse d(c) + |c - start| <= h_stop x |goal - start| + 64 moves
   int max_rounds;
   float h_weight;   // f = g + h_weight x max(h, Dubins length) (1: the reference's f)
-  int pad;
+  int h_coarse;     // the Dijkstra field's block side in map cells (1, 2 or 4)
   unsigned* progress;  // debug (HASTAR_RELAXED_PROGRESS): per-wave phase words in host memory, or null
 };
 

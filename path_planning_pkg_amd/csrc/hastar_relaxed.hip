@@ -174,25 +174,33 @@ struct RelaxShared {
 // iteration starts, and slot (cur-1) & 7 is recycled (reset) long before it is pushed again.
 // The run ends after 3 empty buckets in a row (nothing can be pushed past them) or at the
 // early stop; both decisions use values every thread reads identically.
+// The field is over blocks of K x K map cells (K = rp.h_coarse: 1, 2 or 4): a block is
+// passable when any of its cells is (so no passage of the map closes), its moves cost K x the
+// cell moves, and a cell's heuristic is its block's distance (relaxed_h).  K = 2 settles a
+// quarter of the cells in half the buckets: the bucket loop's dependent round trips, and in a
+// batch the field's scattered traffic, fall with it.
 __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, const RelaxParams& rp,
                                    float* dist_f, BucketEntry* bl) {
   const int tid = threadIdx.x, NT = blockDim.x;
-  const int N = P.N;
-  const float wb = P.act_cost_axis;
-  const float cd = P.act_cost_diag;
+  const int K = rp.h_coarse;
+  const int N = (P.N + K - 1) / K;  // blocks per side
+  const float wb = P.act_cost_axis * (float)K;
+  const float cd = P.act_cost_diag * (float)K;
   const int nact = P.diag ? 8 : 4;
   uint32_t* dist = reinterpret_cast<uint32_t*>(dist_f);
   const size_t NN = (size_t)N * N;
   for (size_t i = tid; i < NN; i += NT) dist[i] = 0x7f800000u;
-  // entries name cells as (i << 16 | j): no integer division per entry
-  const uint32_t goal_ij = ((uint32_t)P.goal_cx << 16) | (uint32_t)P.goal_cy;
+  // entries name blocks as (i << 16 | j): no integer division per entry
+  const int gbx = P.goal_cx / K, gby = P.goal_cy / K, sbx = P.start_cx / K, sby = P.start_cy / K;
+  const uint32_t goal_ij = ((uint32_t)gbx << 16) | (uint32_t)gby;
   const float inv_wb = 1.0f / wb;  // bucket index only: rounding is absorbed by the clamp below
+  const float bres = P.res * (float)K;
   // relax only inside the ellipse d(c) + |c - start| <= bound around the goal-start segment
   const float gsx = (float)(P.goal_cx - P.start_cx), gsy = (float)(P.goal_cy - P.start_cy);
-  const float bound = rp.h_stop * P.res * sqrtf(gsx * gsx + gsy * gsy) + 64.0f * wb;
+  const float bound = rp.h_stop * P.res * sqrtf(gsx * gsx + gsy * gsy) + 64.0f * P.act_cost_axis;
   block_sync();
   if (tid == 0) {
-    dist[(size_t)P.goal_cx * N + P.goal_cy] = 0u;
+    dist[(size_t)gbx * N + gby] = 0u;
     bl[0] = BucketEntry{goal_ij, 0u};
     for (int k = 0; k < 8; ++k) S.cnt[k] = k == 0 ? 1 : 0;
     S.overflow = 0;
@@ -231,9 +239,16 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
         dc[u] = 0u;
         oc[u] = 0.0f;
         if (en[u].cell != 0xffffffffu) {
-          const uint32_t c = (en[u].cell >> 16) * (uint32_t)N + (en[u].cell & 0xffffu);
-          dc[u] = ld_sync(&dist[c]);
-          oc[u] = gp(P.occ)[c];
+          const uint32_t bi = en[u].cell >> 16, bj = en[u].cell & 0xffffu;
+          dc[u] = ld_sync(&dist[bi * (uint32_t)N + bj]);
+          // the block's least occupancy (passable when any of its cells is)
+          float o = FLT_MAX;
+          for (int di = 0; di < K; ++di)
+            for (int dj = 0; dj < K; ++dj) {
+              const uint32_t ci = bi * K + di, cj = bj * K + dj;
+              if (ci < (uint32_t)P.N && cj < (uint32_t)P.N) o = fminf(o, gp(P.occ)[ci * (uint32_t)P.N + cj]);
+            }
+          oc[u] = o;
         }
       }
       RSTAMP(1);
@@ -291,7 +306,7 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
           const int pi = (int)(cij >> 16) + di, pj = (int)(cij & 0xffffu) + dj;
           // the ellipse: a cell whose distance plus its straight-line distance to the start
           // exceeds the bound cannot lie on a path the search needs; it stays unsettled
-          const float es = P.res * sqrtf((float)((pi - P.start_cx) * (pi - P.start_cx) + (pj - P.start_cy) * (pj - P.start_cy)));
+          const float es = bres * sqrtf((float)((pi - sbx) * (pi - sbx) + (pj - sby) * (pj - sby)));
           if (__uint_as_float(nb) + es > bound) continue;
           const uint32_t pij = (uint32_t)pi << 16 | (uint32_t)pj;
           int kb = (int)(__uint_as_float(nb) * inv_wb);
@@ -316,11 +331,12 @@ __device__ float relaxed_heuristic(const PlannerDev& P, const RelaxArena& A, Rel
   return (float)cur * wb;
 }
 
-// The heuristic of cell (i, j): its Dijkstra distance, or for a cell the ellipse left
-// unsettled the bound minus its straight-line distance to the field's start cell.
-__device__ __forceinline__ float relaxed_h(const PlannerDev& P, const float* dist, size_t cell, int i, int j,
-                                          float bound, int sx, int sy) {
-  const float d = ld_dist(dist, cell);
+// The heuristic of cell (i, j): its block's Dijkstra distance, or for a block the ellipse left
+// unsettled the bound minus the cell's straight-line distance to the field's start cell.
+__device__ __forceinline__ float relaxed_h(const PlannerDev& P, const float* dist, int K, int i, int j, float bound,
+                                          int sx, int sy) {
+  const int nb = (P.N + K - 1) / K;
+  const float d = ld_dist(dist, (size_t)(i / K) * nb + (j / K));
   if (d < FLT_MAX) return d;
   const float es = P.res * sqrtf((float)((i - sx) * (i - sx) + (j - sy) * (j - sy)));
   return fmaxf(bound - es, 0.0f);
@@ -331,7 +347,7 @@ __device__ __forceinline__ float relaxed_h(const PlannerDev& P, const float* dis
 // values (g, f and the node's tie), never by the order in which the round's wavefronts run, so
 // a query gives the same path on every run.
 __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, ApfStage& apfs,
-                               const GoalC& GC, const float* dist, float hlim, int hs_x, int hs_y, float hw, int idx,
+                               const GoalC& GC, const float* dist, int hk, float hlim, int hs_x, int hs_y, float hw, int idx,
                                int lane, uint2* list_n) {
   const Node3 cur = gload(&A.nodes[idx]);
   const uint32_t key = ufu(cur.key), tie = ufu((uint32_t)cur.r);
@@ -418,7 +434,7 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
   if (lead) {
     const size_t cell = (size_t)scx * P.N + scy;
     occv = gp(P.occ)[cell];
-    h2 = relaxed_h(P, dist, cell, scx, scy, hlim, hs_x, hs_y);
+    h2 = relaxed_h(P, dist, hk, scx, scy, hlim, hs_x, hs_y);
   }
   const float dub = cand_dubins(P.r_min, GC, P.goal_h, sx, sy, sh, gs, lane);
   const float fc = apf_fused(P, apfs, cxp, cyp, sx, sy, sh, __ballot(lead), gs, lane);
@@ -495,8 +511,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
   if (tid == 0) {
     Node3 s0;
     s0.key = key3(P.start_cx, P.start_cy, P.start_bin);
-    const float h0 = relaxed_h(P, dist, (size_t)P.start_cx * P.N + P.start_cy, P.start_cx, P.start_cy, hlim, hs_x,
-                               hs_y);
+    const float h0 = relaxed_h(P, dist, rp.h_coarse, P.start_cx, P.start_cy, hlim, hs_x, hs_y);
     s0.f = h0;
     s0.l = s0.p = NIL;
     s0.r = 0;
@@ -637,7 +652,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
       if (e >= nE) break;
       RPROG(0, 5);
       RPROG(3, e);
-      relaxed_expand(P, A, S, S.apf[wv], GC, dist, hlim, hs_x, hs_y, rp.h_weight, LE[e], lane, LA);
+      relaxed_expand(P, A, S, S.apf[wv], GC, dist, rp.h_coarse, hlim, hs_x, hs_y, rp.h_weight, LE[e], lane, LA);
     }
     RPROG(0, 6);
     block_sync();

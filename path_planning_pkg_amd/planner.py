@@ -82,6 +82,7 @@ def load_library():
     L.hastar_debug_astar_modes.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_timing.argtypes = [vp, C.POINTER(C.c_ulonglong)]
     L.hastar_debug_slots.argtypes = [vp, C.POINTER(C.c_longlong)]
+    L.hastar_debug_split.argtypes = [vp, fp]
     L.hastar_debug_pooled_resumes.argtypes = [C.POINTER(C.c_longlong)]
     L.hastar_velocity_profile_batch.argtypes = [C.c_int, C.POINTER(HastarVelocityParams), C.c_int,
                                                 C.POINTER(C.c_longlong), fp, fp, fp, fp, C.POINTER(C.c_ubyte), fp,
@@ -387,6 +388,12 @@ class HybridAStar:
         _check(load_library().hastar_debug_slots(self.h, out))
         return {"resident_slots": out[0], "waves_per_cu": out[1], "arenas": out[2], "arena_mib": out[3],
                 "head_cus": out[4]}
+
+    def split_ms(self):
+        """The device's last split launch: ms to head start, head end, bulk start, bulk end."""
+        out = np.zeros(4, np.float32)
+        _check(load_library().hastar_debug_split(self.h, fptr(out)))
+        return [float(v) for v in out]
 
     def timing(self):
         """(t_start, t_end, slot) of the last search; times in 10 ns ticks."""

@@ -54,11 +54,11 @@ def test_rbtree_replica_matches_std_set(tmp_path):
 
 def test_relaxed_entry_point_rejects_bad_arguments():
     """hastar_find_path_relaxed_batch validates its arguments before touching a device, and
-    hastar_relaxed_opts has the C layout the ctypes mirror declares (six 4-byte fields)."""
+    hastar_relaxed_opts has the C layout the ctypes mirror declares (seven 4-byte fields)."""
     from path_planning_pkg_amd.capi import HastarRelaxedOpts
     from path_planning_pkg_amd.planner import load_library
     L = load_library()
-    assert C.sizeof(HastarRelaxedOpts) == 24
+    assert C.sizeof(HastarRelaxedOpts) == 28
     f = (C.c_float * 3)()
     i = (C.c_int * 1)()
     rc = L.hastar_find_path_relaxed_batch(None, 0, f, f, f, f, 1, i, f, i, None, None)

@@ -118,6 +118,23 @@ def test_relaxed_cfg3_queries(gpu, oracle_lib):
     _run_case(gpu, oracle_lib, [synthetic(1024, 72, 200, seed=q + 1) for q in (0, 1, 2, 3, 10226)], "cfg3")
 
 
+@pytest.mark.parametrize("h_coarse", [1, 4])
+def test_relaxed_field_block_sizes(gpu, oracle_lib, h_coarse):
+    """The Dijkstra field over blocks of 1 (every map cell) and 4 x 4 cells (the default is 2):
+    valid paths on cfg3 queries; a field kept with one block size is rebuilt for another; other
+    sizes are rejected."""
+    _run_case(gpu, oracle_lib, [synthetic(1024, 72, 200, seed=q + 1) for q in (0, 3)], f"cfg3 h_coarse={h_coarse}",
+              relaxed=dict(h_coarse=h_coarse))
+    cfg, proto = synthetic(256, 36, 40, 1)
+    g = gpu.HybridAStar(cfg)
+    drive(g, proto)
+    for hc, rebuilt in ((h_coarse, True), (h_coarse, False), (2, True)):
+        gpu.find_path_batch([g], [proto["vel"]], [proto["start"]], relaxed=dict(reuse_heuristic=1, h_coarse=hc))
+        assert (g.cycles()[2] > 0) == rebuilt, (hc, rebuilt)
+    with pytest.raises(gpu.HastarError):
+        gpu.find_path_batch([g], [proto["vel"]], [proto["start"]], relaxed=dict(h_coarse=3))
+
+
 def test_relaxed_cfg5_pairs(gpu, oracle_lib):
     """cfg5 pairs (1024^2, random goal frames): the tick-0 query of pairs 0..7."""
     cases = []

@@ -68,11 +68,12 @@ def pmc(args):
 def counters(args):
     """Every counter of the given rocprofv3 --pmc pass directories, summed over the search
     kernel's dispatch `--dispatch` (per-XCD / per-instance rows are added up)."""
-    out = {"kernel": KERNEL, "batch": args.batch, "grid": args.grid, "dispatch_index": args.dispatch, "counters": {}}
+    kern = args.kernel
+    out = {"kernel": kern, "batch": args.batch, "grid": args.grid, "dispatch_index": args.dispatch, "counters": {}}
     for d in args.dirs:
         per = {}
         for r in rows(d, "counter_collection.csv"):
-            if KERNEL not in r["Kernel_Name"]:
+            if kern not in r["Kernel_Name"]:
                 continue
             key = int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0)
             per.setdefault(r["Counter_Name"], {}).setdefault(key, 0.0)
@@ -121,5 +122,6 @@ c.add_argument("dirs", nargs="+")
 c.add_argument("--batch", type=int, required=True)
 c.add_argument("--grid", type=int, default=1024)
 c.add_argument("--dispatch", type=int, default=1)
+c.add_argument("--kernel", default=KERNEL, help="kernel name substring (default the batch kernel)")
 a = ap.parse_args()
 {"trace": trace, "pmc": pmc, "counters": counters}[a.cmd](a)

@@ -17,7 +17,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from path_planning_pkg_amd import planner as gpu  # noqa: E402
 from tests.scenarios import drive, replan_pairs, synthetic  # noqa: E402
 
-SETTINGS = [(0.5, 1.2, 100.0), (0.5, 1.2, 2.0), (0.5, 1.2, 1.5), (0.5, 1.2, 1.25), (0.25, 1.2, 1.5), (0.5, 1.5, 1.5)]
+# (delta, h_weight, h_stop, h_coarse)
+SETTINGS = [(0.25, 1.2, 1.5, 1), (0.25, 1.2, 1.5, 2), (0.25, 1.2, 1.5, 4), (0.5, 1.2, 1.5, 2), (0.25, 1.2, 2.0, 2)]
 
 
 def groups(names):
@@ -51,12 +52,12 @@ def main():
         ex, ms_ex = gpu.find_path_batch(ps, vels, starts, cap=16384)
         print(json.dumps({"group": name, "mode": "exact", "ms": round(ms_ex, 2),
                           "ok": sum(r["ok"] for r in ex), "pops": [r["stats"]["pops"] for r in ex]}), flush=True)
-        for d, w, hs in SETTINGS:
+        for d, w, hs, hc in SETTINGS:
             t0 = time.perf_counter()
-            rel, ms = gpu.find_path_batch(ps, vels, starts, cap=16384, relaxed=dict(delta=d, h_weight=w, h_stop=hs))
+            rel, ms = gpu.find_path_batch(ps, vels, starts, cap=16384, relaxed=dict(delta=d, h_weight=w, h_stop=hs, h_coarse=hc))
             wall = (time.perf_counter() - t0) * 1e3
             ratios = [r["cost"] / e["cost"] for r, e in zip(rel, ex) if r["ok"] and e["ok"]]
-            row = {"group": name, "delta": d, "h_weight": w, "h_stop": hs, "ms": round(ms, 2), "wall_ms": round(wall, 2),
+            row = {"group": name, "delta": d, "h_weight": w, "h_stop": hs, "h_coarse": hc, "ms": round(ms, 2), "wall_ms": round(wall, 2),
                    "ok": sum(r["ok"] for r in rel), "exact_ok": sum(e["ok"] for e in ex),
                    "status": sorted({r["stats"]["status"] for r in rel}),
                    "cost_ratio_mean": round(float(np.mean(ratios)), 4) if ratios else None,
