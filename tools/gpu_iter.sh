@@ -5,7 +5,8 @@
 #   bench     python bench.py (defaults: cfg3, the headline line)       -> bench.json
 #   cfg5      bench.py --workload cfg5                                  -> bench_cfg5.json
 #   stamps    single-query phase stamps (lib_stamps build) of the bench's longest query and seed 1
-#   prof      tools/prof_r02.sh <tag>: rocprofv3 trace + PMC passes     -> trace_summary.json, pmc_*, counters_*
+#   prof      tools/prof_round.sh <tag>: rocprofv3 trace + PMC passes   -> trace_summary.json, pmc_*, counters_*
+#   single    tools/prof_single.sh <tag> 1 3: SQ instruction mix of single queries on the latency kernel
 set -o pipefail
 TAG=$1; shift
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -24,7 +25,8 @@ for st in "$@"; do
            cut -c1-400 $O/bench_cfg5.json ;;
     stamps) HASTAR_LIB=path_planning_pkg_amd/lib_stamps/libhastar_amd.so timeout -k 10 300 python -u tools/profile_search.py --seeds 2396 1 2 3 > $O/stamps.jsonl 2>&1 \
              || { tail -20 $O/stamps.jsonl; exit 1; }; cut -c1-300 $O/stamps.jsonl ;;
-    prof)  bash tools/prof_r02.sh $TAG || exit 1 ;;
+    prof)  bash tools/prof_round.sh $TAG || exit 1 ;;
+    single) bash tools/prof_single.sh $TAG 1 3 || exit 1 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done

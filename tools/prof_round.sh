@@ -23,3 +23,12 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 python3 tools/prof_summary.py pmc $R/FETCH_SIZE $R/WRITE_SIZE $OUT/pmc_search_summary.json --batch $B --grid 1024 || exit 1
 cat $OUT/pmc_search_summary.json
+# 3. SQ instruction mix / wait states of the batch kernel (one 1-step bench per pass)
+for pass in "SQA SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU" \
+            "SQB SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA"; do
+  set -- $pass
+  name=$1; shift
+  timeout -s KILL 400 rocprofv3 --pmc "$@" --output-format csv --kernel-include-regex hastar_search_kernel -d $R/$name -o pmc \
+    -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --latency-queries 0 > $OUT/pmc_$name.log 2>&1 || { tail -5 $OUT/pmc_$name.log; exit 1; }
+done
+python3 tools/prof_summary.py counters $OUT/counters_search.json $R/SQA $R/SQB --batch $B --dispatch -1 || exit 1
