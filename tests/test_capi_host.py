@@ -63,3 +63,33 @@ def test_relaxed_entry_point_rejects_bad_arguments():
     i = (C.c_int * 1)()
     rc = L.hastar_find_path_relaxed_batch(None, 0, f, f, f, f, 1, i, f, i, None, None)
     assert rc == -22  # HASTAR_EINVAL
+
+
+def test_route_score_cold_order_key():
+    """hastar_test_route_score (the cold-order key of a planner with no history, host only)
+    equals sum 1 / (1 + d)^2 over the boxes, d = box-to-segment distance, on hand cases and on
+    tests/scenarios.py:route_score (the bench's rank deal uses the same score)."""
+    import numpy as np
+    from path_planning_pkg_amd.planner import load_library
+    from tests.scenarios import route_score
+    L = load_library()
+    L.hastar_test_route_score.restype = C.c_double
+    fp = C.POINTER(C.c_float)
+
+    def lib_score(boxes, s, g):
+        b = np.ascontiguousarray(boxes, np.float32).reshape(-1, 4)
+        st, gl = np.asarray(s, np.float32), np.asarray(g, np.float32)
+        return L.hastar_test_route_score(b.ctypes.data_as(fp), len(b), st.ctypes.data_as(fp), gl.ctypes.data_as(fp))
+
+    # a box crossing the route counts 1; one 3 m beside it 1/16; one beyond the goal by 1 m 1/4
+    assert lib_score([[-5, 0, 2, 2]], [-10, 0], [0, 0]) == pytest.approx(1.0)
+    assert lib_score([[-5, 4, 2, 2]], [-10, 0], [0, 0]) == pytest.approx(1 / 16)
+    assert lib_score([[2, 0, 2, 2]], [-10, 0], [0, 0]) == pytest.approx(1 / 4)
+    # a diagonal route passing a box corner at distance sqrt(2)/2
+    assert lib_score([[1.5, -0.5, 1, 1]], [0, 0], [2, 2]) == pytest.approx(1 / (1 + 2 ** -0.5) ** 2)
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        b = np.concatenate([rng.uniform(-60, 20, (30, 2)), rng.uniform(1, 6, (30, 2))], 1).astype(np.float32)
+        s = rng.uniform(-60, 0, 2).astype(np.float32)
+        g = rng.uniform(-10, 10, 2).astype(np.float32)
+        assert lib_score(b, s, g) == pytest.approx(float(route_score(b[None], s, g)[0]), rel=1e-9)

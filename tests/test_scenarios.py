@@ -35,7 +35,7 @@ def test_vectorised_mt19937_generator_matches_per_seed_draws():
     """synthetic_ref_boxes_many (one std::mt19937 stream per seed, vectorised over the seeds)
     draws the same boxes as the per-seed generator; predicted_cost reads those boxes."""
     import numpy as np
-    from tests.scenarios import (_mt19937_words, predicted_cost, synthetic_ref_boxes,
+    from tests.scenarios import (_mt19937_words, predicted_cost, route_score, synthetic_ref_boxes,
                                  synthetic_ref_boxes_many)
     w = _mt19937_words([5, 4357], 1500)
     for i, s in enumerate((5, 4357)):
@@ -47,7 +47,4 @@ def test_vectorised_mt19937_generator_matches_per_seed_draws():
         b, st = synthetic_ref_boxes(1024, 200, s)
         assert np.array_equal(boxes[i], b) and st == stx
     p = predicted_cost(1024, 200, np.array(seeds) - 1)
-    b = boxes.astype(np.float64)
-    r = np.hypot(b[..., 2], b[..., 3]) / 2 + 2.5
-    d = (np.hypot(b[..., 0] - np.clip(b[..., 0], stx, 0.0), b[..., 1]) - r).min(axis=1)
-    assert np.allclose(p, -d)
+    assert np.allclose(p, route_score(boxes, [stx, 0.0], [0.0, 0.0]))
