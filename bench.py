@@ -161,6 +161,8 @@ def parse_args(argv=None):
     ap.add_argument("--relaxed-delta", type=float, default=0.25, help="relaxed mode: frontier width (m)")
     ap.add_argument("--relaxed-weight", type=float, default=1.2, help="relaxed mode: heuristic weight")
     ap.add_argument("--no-relaxed", action="store_true", help="cfg5: skip the relaxed-mode comparison")
+    ap.add_argument("--relaxed-batch-nodes", type=int, default=1 << 16,
+                    help="relaxed batch: node capacity per search (hastar_relaxed_opts.max_nodes)")
     ap.add_argument("--relaxed-batch", type=int, default=4096,
                     help="cfg3/cfg4: queries of the batch also planned in one relaxed call (query rate)")
     ap.add_argument("--dump-timings", default=None,
@@ -364,6 +366,7 @@ def main():
                        "grid": args.grid, "angle_bins": args.bins, "obstacles": args.obstacles,
                        "queries_per_gpu": B, "global_batch": B * world, "parallelism": f"query-sharded x{world}"},
             "kernel_only_value": pops_all / elapsed * ms_per_step / avg_kernel_ms,
+            "kernel_ms_per_step": [float(k) for k in kernel_ms],
             "cold_first_step": {"value": cold_pops_all / cold_s, "ms": cold_s * 1e3,
                                 "note": "first launch of the batch: no longest-first history (the library orders the "
                                         "queue by its cold key: boxes near the start-goal route, hastar.h "
@@ -589,16 +592,22 @@ def relaxed_latency_phase(gpu, planners, vels, starts, last, ids, qids, args, ex
     nb = min(args.relaxed_batch, len(planners))
     batch = None
     if nb > 0:
+        # node capacity 64 k per search (these queries expand < 5 k nodes; the library's default
+        # 256 k sizes an arena at 34 MiB, and beside the exact pool the HBM then holds only a
+        # quarter as many arenas as CUs)
+        bopts = dict(opts, max_nodes=args.relaxed_batch_nodes)
         t0 = time.perf_counter()
-        rb, bms = gpu.find_path_batch(planners[:nb], vels[:nb], starts[:nb], cap=8192, relaxed=opts)
+        rb, bms = gpu.find_path_batch(planners[:nb], vels[:nb], starts[:nb], cap=8192, relaxed=bopts)
         wall = time.perf_counter() - t0
+        groups, arena_mib = planners[0].relaxed_pool()
         br = [float(r["cost"]) / float(last.cost[i]) for i, r in enumerate(rb) if r["ok"] and last.ok[i]]
         batch = {"queries": nb, "kernel_ms": bms, "wall_ms": wall * 1e3, "queries_per_s": nb / (bms * 1e-3),
                  "exact_queries_per_s": exact_qps, "ok": sum(int(r["ok"]) for r in rb),
                  "exact_ok": int(sum(int(last.ok[i]) for i in range(nb))),
                  "status": sorted({int(r["stats"]["status"]) for r in rb}),
                  "cost_ratio_vs_exact_mean": float(np.mean(br)) if br else None,
-                 "cost_ratio_vs_exact_max": float(np.max(br)) if br else None}
+                 "cost_ratio_vs_exact_max": float(np.max(br)) if br else None,
+                 "workgroups": groups, "arena_mib": arena_mib, "max_nodes": args.relaxed_batch_nodes}
     return {"batch": batch, "queries": [qids[i] for i in ids], "gpu_ms": ms, "gpu_median_ms": float(np.median(ms)) if ms else None,
             "exact_gpu_ms_same_queries": exact_ms, "ok": ok, "exact_ok": int(sum(int(last.ok[i]) for i in ids)),
             "cost_ratio_vs_exact": ratios, "expansions": exp, "opts": opts,
@@ -639,6 +648,7 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
     # ticks, as the exact mode keeps its A* memo
     relaxed_opts = dict(delta=args.relaxed_delta, h_weight=args.relaxed_weight, reuse_heuristic=1)
     rx = {"kernel_ms": [], "wall_ms": [], "upkeep_ms": [], "ok": 0, "ratios": []}
+    slowest = []
 
     def step(timed):
         """One tick; returns (stats, kernel ms, successes, seconds of the exact tick).  When
@@ -650,6 +660,11 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
         br = gpu.find_path_batch_arrays(planners, vels, starts, buffers=bufs)
         st = br.stats.copy()
         t_exact = time.perf_counter() - t0
+        if timed:  # the tick's slowest search (it bounds the tick): its pops and inner A* pops
+            tm = np.array([p.timing() for p in planners], dtype=np.float64)
+            j = int(np.argmax(tm[:, 1] - tm[:, 0]))
+            slowest.append({"pair": int(ids[j]), "ms": float((tm[j, 1] - tm[j, 0]) * 1e-5), "pops": int(st["pops"][j]),
+                            "astar_pops": int(st["astar_pops"][j])})
         if timed and not args.no_relaxed and planners:
             t1 = time.perf_counter()
             rel, rms = gpu.find_path_batch(planners, vels, starts, cap=8192, relaxed=relaxed_opts)
@@ -699,7 +714,7 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
                        "grid": args.grid, "angle_bins": args.bins, "obstacles": args.obstacles,
                        "pairs_total": args.pairs, "pairs_rank0": len(ids), "global_batch": args.pairs,
                        "parallelism": f"pair-sharded x{world}"},
-            "replan_latency_ms": avg_k, "tick_ms": elapsed / args.steps * 1e3,
+            "replan_latency_ms": avg_k, "tick_ms": elapsed / args.steps * 1e3, "slowest_search_per_tick": slowest,
             "tick_budget_ms": 50.0, "success_rate": oks / max(len(ids) * args.steps, 1), "setup_s_per_gpu": t_setup,
             "roofline": {"bound": "latency", "roof": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": None,

@@ -42,6 +42,8 @@ int hastar_debug_slots(hastar_handle h, long long* out5);
 int hastar_debug_split(hastar_handle h, float* out4);
 /* resume arenas carved from idle slot arenas of the pool so far (process-wide count) */
 int hastar_debug_pooled_resumes(long long* out);
+/* The device's relaxed-mode arena pool: {arenas (= resident workgroups of a relaxed launch), MiB each}. */
+int hastar_debug_relaxed_pool(hastar_handle h, long long* out2);
 /* The cold-order score of a planner with no history (host only): sum over the boxes {x, y, dx, dy}
  * (world frame) of 1 / (1 + d)^2, d = distance between the box and the start-goal segment. */
 double hastar_test_route_score(const float* boxes, int n, const float start[2], const float goal[2]);

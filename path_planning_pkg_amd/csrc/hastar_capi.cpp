@@ -220,6 +220,7 @@ struct DeviceCtx {
   int n_rarenas = 0;
   size_t r_cells = 0;
   int r_nodes = 0, r_N = 0;
+  int r_asked = 0;  // workgroups the pool was sized for (fewer when HBM capped it)
   RelaxField* d_rfields = nullptr;   // per-planner heuristic fields of a relaxed batch
   size_t rfields_cap = 0;
 };
@@ -2058,15 +2059,16 @@ unsigned* relaxed_progress() {
   return words;
 }
 int relax_acquire(DeviceCtx& D, int N, int nodes, int want) {
-  if (D.n_rarenas >= want && D.r_N >= N && D.r_nodes >= nodes) return 0;
+  // the pool serves a call whose arenas it covers, with as many workgroups as it was sized for
+  // (a pool capped by free HBM is not reallocated by every call that asks for more)
+  if (D.n_rarenas > 0 && D.r_N >= N && D.r_nodes >= nodes && (D.n_rarenas >= want || D.r_asked >= want)) return 0;
   HIPCHK(hipStreamSynchronize(D.stream));
   if (D.rslab) hipFree(D.rslab);
   if (D.d_rarenas) hipFree(D.d_rarenas);
   D.rslab = nullptr;
   D.d_rarenas = nullptr;
   D.n_rarenas = 0;
-  N = std::max(N, D.r_N);
-  nodes = std::max(nodes, D.r_nodes);
+  // sized for this call (a smaller node capacity gives smaller arenas and more workgroups)
   const size_t per = relax_bytes(N, nodes, nullptr, nullptr);
   size_t fr = 0, tot = 0;
   HIPCHK(hipMemGetInfo(&fr, &tot));
@@ -2085,6 +2087,7 @@ int relax_acquire(DeviceCtx& D, int N, int nodes, int want) {
   HIPCHK(hipMemcpyAsync(D.d_rarenas, host.data(), (size_t)n * sizeof(RelaxArena), hipMemcpyHostToDevice, D.stream));
   HIPCHK(hipStreamSynchronize(D.stream));
   D.n_rarenas = n;
+  D.r_asked = want;
   D.r_N = N;
   D.r_nodes = nodes;
   return 0;
@@ -2664,6 +2667,13 @@ int hastar_debug_pooled_resumes(long long* out) {
   if (!out) return fail(HASTAR_EINVAL, "null output");
   *out = g_pooled_resumes.load();
   return HASTAR_OK;
+}
+
+int hastar_debug_relaxed_pool(hastar_handle h, long long* out2) {
+  if (!h || !h->dc || !out2) return fail(HASTAR_EINVAL, "bad argument");
+  out2[0] = h->dc->n_rarenas;
+  out2[1] = h->dc->n_rarenas > 0 ? (long long)(relax_bytes(h->dc->r_N, h->dc->r_nodes, nullptr, nullptr) >> 20) : 0;
+  return 0;
 }
 
 int hastar_debug_split(hastar_handle h, float* out4) {

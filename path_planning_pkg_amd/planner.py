@@ -83,6 +83,7 @@ def load_library():
     L.hastar_debug_timing.argtypes = [vp, C.POINTER(C.c_ulonglong)]
     L.hastar_debug_slots.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_split.argtypes = [vp, fp]
+    L.hastar_debug_relaxed_pool.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_pooled_resumes.argtypes = [C.POINTER(C.c_longlong)]
     L.hastar_velocity_profile_batch.argtypes = [C.c_int, C.POINTER(HastarVelocityParams), C.c_int,
                                                 C.POINTER(C.c_longlong), fp, fp, fp, fp, C.POINTER(C.c_ubyte), fp,
@@ -394,6 +395,12 @@ class HybridAStar:
         out = np.zeros(4, np.float32)
         _check(load_library().hastar_debug_split(self.h, fptr(out)))
         return [float(v) for v in out]
+
+    def relaxed_pool(self):
+        """The device's relaxed-mode arena pool: (arenas, MiB per arena)."""
+        out = (C.c_longlong * 2)()
+        _check(load_library().hastar_debug_relaxed_pool(self.h, out))
+        return int(out[0]), int(out[1])
 
     def timing(self):
         """(t_start, t_end, slot) of the last search; times in 10 ns ticks."""

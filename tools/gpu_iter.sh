@@ -7,6 +7,7 @@
 #   stamps    single-query phase stamps (lib_stamps build) of the bench's longest query and seed 1
 #   prof      tools/prof_round.sh <tag>: rocprofv3 trace + PMC passes   -> trace_summary.json, pmc_*, counters_*
 #   single    tools/prof_single.sh <tag> 1 3: SQ instruction mix of single queries on the latency kernel
+#   relaxed   tools/gpu_relaxed.sh <tag>: relaxed-mode GPU tests + settings sweep  -> pytest.log, sweep.json
 set -o pipefail
 TAG=$1; shift
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -27,6 +28,7 @@ for st in "$@"; do
              || { tail -20 $O/stamps.jsonl; exit 1; }; cut -c1-300 $O/stamps.jsonl ;;
     prof)  bash tools/prof_round.sh $TAG || exit 1 ;;
     single) bash tools/prof_single.sh $TAG 1 3 || exit 1 ;;
+    relaxed) bash tools/gpu_relaxed.sh $TAG || exit 1 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done
