@@ -802,6 +802,11 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
       return true;
     }
     STAMP_ADD(8, t_pop);
+    // every neighbour's key, g and f (AStar.cpp:160-176) in its own lane, in the reference's
+    // float order (g0 + cost, then + h): the loop below reads them instead of computing them
+    const uint32_t key_l = ((uint32_t)ni << 16) | ((uint32_t)nj & 0xffffu);
+    const float gn_l = g0 + acost;
+    const float fn_l = gn_l + euclid_h(P, ni, nj);
     // The expansion's HBM stores (node-map f of inserted cells, prev links of new nodes) are
     // collected in lane k and issued together after the loop: a global store inside the
     // loop would make every later register reuse wait for its completion (vmcnt).
@@ -829,10 +834,10 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
       }
       if ((cmask >> k) & 1ull) continue;
       const int ki = rl_i(ni, k), kj = rl_i(nj, k);
-      const uint32_t key = ((uint32_t)ki << 16) | (uint32_t)kj;
+      const uint32_t key = ufu((uint32_t)__builtin_amdgcn_readlane((int)key_l, k));
       const float fprobe = rl_f(nf, k);  // stale _node_map f, as the reference reads it
-      const float gn = g0 + kcost;
-      const float fn = gn + euclid_h(P, ki, kj);
+      const float gn = rl_f(gn_l, k);    // g0 + kcost
+      const float fn = rl_f(fn_l, k);    // gn + euclid_h(ki, kj)
       STAMP_T t_f = STAMP_NOW();
       // nodes of this cell in the open tree: from the cell's hint (its last inserted node;
       // exact unless a duplicate was ever inserted in this search, then scan the pool)
