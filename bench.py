@@ -67,6 +67,23 @@ def step_balance(planners):
             "longest_search_start_ms": float((t[li, 0] - t[:, 0].min()) * 1e-5)}
 
 
+def step_diag(planners, res):
+    """One step's schedule: span of the searches, the split launch's event times, and the start
+    offset / duration (ms) of the searches on the latency CUs (arenas 0 .. head_cus - 1) and of
+    the step's longest search."""
+    t = np.array([p.timing() for p in planners], dtype=np.float64)
+    t0 = t[:, 0].min()
+    dur = (t[:, 1] - t[:, 0]) * 1e-5
+    head_cus = int(planners[0].slots()["head_cus"])
+    head = np.nonzero(t[:, 2] < head_cus)[0]
+    first = head[np.argsort(t[head, 0])][:16]
+    li = int(np.argmax(dur))
+    return {"kernel_ms": float(res.kernel_ms), "span_ms": float((t[:, 1].max() - t0) * 1e-5),
+            "split_ms": planners[0].split_ms(),
+            "head": [[round(float((t[i, 0] - t0) * 1e-5), 1), round(float(dur[i]), 1), int(t[i, 2])] for i in first],
+            "longest": [round(float((t[li, 0] - t0) * 1e-5), 1), round(float(dur[li]), 1), int(t[li, 2])]}
+
+
 def shard_query_ids(rank, world, batch, pred=None):
     """Queries of one rank: weak scaling, B per GPU, disjoint across ranks, no exchange.  The
     global queries 0 .. world * B - 1 are dealt by predicted cost (`pred`, one value per global
@@ -136,7 +153,7 @@ def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); > 1 without WORLD_SIZE spawns them")
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("HASTAR_BENCH_BATCH", "23552")),
                     help="planners (queries) per GPU")
     ap.add_argument("--grid", type=int, default=None, help="default 1024 (cfg3, cfg5) or 2048 (cfg4)")
@@ -148,6 +165,8 @@ def parse_args(argv=None):
     ap.add_argument("--max-astar-nodes", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--step-diag", action="store_true",
+                    help="per-step schedule diagnostics in the JSON line (reads every search's timing per step)")
     ap.add_argument("--latency-queries", type=int, default=3)
     ap.add_argument("--workload", choices=("cfg3", "cfg4", "cfg5"), default="cfg3",
                     help="cfg3: batch of independent queries (default, the headline line); "
@@ -269,9 +288,12 @@ def main():
     statuses = set()
     oks, parks = 0, 0
     last = None
+    diag = []
     for _ in range(args.steps):
         res = step()
         kernel_ms.append(res.kernel_ms)
+        if args.step_diag:  # per-step schedule diagnostics (inside the timed region: off by default)
+            diag.append(step_diag(planners, res))
         st = res.stats
         pops += int(st["pops"].sum())
         alg_bytes.append(algorithmic_bytes(st, args.obstacles))
@@ -367,6 +389,7 @@ def main():
                        "queries_per_gpu": B, "global_batch": B * world, "parallelism": f"query-sharded x{world}"},
             "kernel_only_value": pops_all / elapsed * ms_per_step / avg_kernel_ms,
             "kernel_ms_per_step": [float(k) for k in kernel_ms],
+            **({"step_diag": diag} if diag else {}),
             "cold_first_step": {"value": cold_pops_all / cold_s, "ms": cold_s * 1e3,
                                 "note": "first launch of the batch: no longest-first history (the library orders the "
                                         "queue by its cold key: boxes near the start-goal route, hastar.h "

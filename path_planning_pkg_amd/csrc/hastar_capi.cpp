@@ -1653,6 +1653,14 @@ static int batch_acquire(DeviceCtx& DC, int n) {
 // Hand a finished batch back: per-planner outcome (stats[i].status), then the paths that fit
 // the caller's buffers packed by one gather kernel and one copy.  lpt: record each search's
 // duration as the planner's longest-first key (exact mode only).
+static bool lpt_work_key() {
+  static const bool on = [] {
+    const char* e = std::getenv("HASTAR_LPT_WORK");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 static int finish_batch(DeviceCtx& DC, const hastar_handle* hs, int n, float* xyh, float* curv, int cap, int* len,
                         float* cost, int* ok, hastar_stats* stats, bool lpt) {
   hipStream_t st = DC.stream;
@@ -1674,8 +1682,12 @@ static int finish_batch(DeviceCtx& DC, const hastar_handle* hs, int n, float* xy
     h->last = R;
     h->have_last = true;
     // longest-first key: the search's own duration (s_memrealtime ticks) — it weighs outer
-    // pops, inner A* pops and shots by what they actually cost, unlike a pop count
-    if (lpt) h->last_pops = R.t_end > R.t_start ? (long long)(R.t_end - R.t_start) : (long long)R.pops + R.astar_pops;
+    // pops, inner A* pops and shots by what they cost where the search ran.  (A schedule-free
+    // work key, 1566 x pops + 1058 x inner pops from a fit of the cfg3 durations, settled the
+    // steps at 3.03 s against 2.74 s: profiles/r03h_bench_long.json; HASTAR_LPT_WORK=1.)
+    if (lpt) h->last_pops = (lpt_work_key() || R.t_end <= R.t_start)
+                                ? 1 + 1566LL * (long long)R.pops + 1058LL * (long long)R.astar_pops
+                                : (long long)(R.t_end - R.t_start);
     ok[i] = R.ok;
     cost[i] = R.ok ? R.cost : FLT_MAX;
     fill_stats(R, stats ? &stats[i] : nullptr);

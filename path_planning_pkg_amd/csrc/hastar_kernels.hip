@@ -415,25 +415,39 @@ __device__ __forceinline__ void rank2(const AStarLdsT<CF>& L, const Ring& rg, fl
 // of a lane's loads (one per 64 entries, at most A_CAP / 2 entries: the shorter side) are
 // issued before its stores, so the shift costs one LDS round trip instead of one per 64
 // entries.  Positions are ring offsets relative to `head` (masked by A_CAP - 1).
+// EXACT: the shift has exactly NCH chunks (chunks 0 .. NCH - 2 are full, only the last may be
+// partial); else at most NCH (each entry tested against cnt).
+template <class CF, int NCH, bool EXACT>
+__device__ __forceinline__ void ring_shift_n(AStarLdsT<CF>& L, int head, int from, int cnt, int dir, int lane) {
+  constexpr int M = CF::CAP - 1;
+  int16_t v[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int i = c * 64 + lane;
+    v[c] = 0;
+    if ((EXACT && c < NCH - 1) || i < cnt) v[c] = L.ring[(head + from + i) & M];
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int i = c * 64 + lane;
+    if ((EXACT && c < NCH - 1) || i < cnt) L.ring[(head + from + i + dir) & M] = v[c];
+  }
+  wave_lds_sync();
+}
 template <class CF>
 __device__ __forceinline__ void ring_shift(AStarLdsT<CF>& L, int head, int from, int cnt, int dir, int lane) {
   constexpr int RING_CH = CF::CAP / 2 / 64;  // chunks of 64 entries in the shorter side
-  constexpr int M = CF::CAP - 1;
-  const int nch = (cnt + 63) >> 6;
-  int16_t v[RING_CH];
-#pragma unroll
-  for (int c = 0; c < RING_CH; ++c) {
-    const int i = c * 64 + lane;
-    v[c] = 0;
-    if (c < nch && i < cnt) v[c] = L.ring[(head + from + i) & M];
+  static_assert(RING_CH >= 4, "ring_shift's specialised chunk counts");
+  // the chunk count is wave-uniform: one straight-line copy per count (the short shifts of a
+  // small open set do not test the chunks they do not have)
+  switch ((cnt + 63) >> 6) {
+    case 1: ring_shift_n<CF, 1, true>(L, head, from, cnt, dir, lane); break;
+    case 2: ring_shift_n<CF, 2, true>(L, head, from, cnt, dir, lane); break;
+    case 3: ring_shift_n<CF, 3, true>(L, head, from, cnt, dir, lane); break;
+    case 4: ring_shift_n<CF, 4, true>(L, head, from, cnt, dir, lane); break;
+    default: ring_shift_n<CF, RING_CH, false>(L, head, from, cnt, dir, lane); break;
   }
-  wave_lds_sync();
-#pragma unroll
-  for (int c = 0; c < RING_CH; ++c) {
-    const int i = c * 64 + lane;
-    if (c < nch && i < cnt) L.ring[(head + from + i + dir) & M] = v[c];
-  }
-  wave_lds_sync();
 }
 
 // ring insert of node x at rank r (shifts the shorter side by one)

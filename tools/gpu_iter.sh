@@ -3,6 +3,7 @@
 #   test      pytest -m gpu (the parity suite, through the C-ABI)      -> gpurun_out/<tag>/pytest_gpu.txt
 #   smoke     __graft_entry__.smoke()                                   -> smoke.txt
 #   bench     python bench.py (defaults: cfg3, the headline line)       -> bench.json
+#   benchlong bench.py --steps 8 --step-diag (per-step kernel times and schedules), no CPU/latency/relaxed legs -> bench_long.json
 #   cfg5      bench.py --workload cfg5                                  -> bench_cfg5.json
 #   stamps    single-query phase stamps (lib_stamps build) of the bench's longest query and seed 1
 #   prof      tools/prof_round.sh <tag>: rocprofv3 trace + PMC passes   -> trace_summary.json, pmc_*, counters_*
@@ -22,6 +23,8 @@ for st in "$@"; do
            tail -1 $O/smoke.txt ;;
     bench) timeout -k 10 900 python -u bench.py --dump-timings $O/timings.npz > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
            cut -c1-400 $O/bench.json ;;
+    benchlong) timeout -k 10 900 python -u bench.py --steps 8 --warmup 1 --step-diag --no-cpu-baseline --latency-queries 0 --relaxed-batch 0 > $O/bench_long.json 2> $O/bench_long.err || { tail -30 $O/bench_long.err; exit 1; }
+           python -c "import json,sys; d=json.load(open('$O/bench_long.json')); print(d['value'], d['kernel_ms_per_step'])" ;;
     cfg5)  timeout -k 10 600 python -u bench.py --workload cfg5 > $O/bench_cfg5.json 2> $O/bench_cfg5.err || { tail -30 $O/bench_cfg5.err; exit 1; }
            cut -c1-400 $O/bench_cfg5.json ;;
     stamps) HASTAR_LIB=path_planning_pkg_amd/lib_stamps/libhastar_amd.so timeout -k 10 300 python -u tools/profile_search.py --seeds 2396 1 2 3 > $O/stamps.jsonl 2>&1 \

@@ -13,13 +13,16 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 R=/tmp/rp_$TAG
 rm -rf $R && mkdir -p $R
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/trace -o run -- python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/trace -o run -- python3 bench.py --warmup 2 --steps 3 > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-python3 tools/prof_summary.py trace $R/trace $OUT/trace_summary.json --warmup 1 --steps 3 || exit 1
+python3 tools/prof_summary.py trace $R/trace $OUT/trace_summary.json --warmup 2 --steps 3 || exit 1
 find $R/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+# the PMC passes run the batch kernel alone (HASTAR_SPLIT=0: under counter collection the
+# profiler serialises the split launch's two kernels, and a 1-step bench then ran > 3 min)
+export HASTAR_SPLIT=0
 B=$(python3 -c "import json;print(json.load(open('$OUT/bench.json'))['config']['queries_per_gpu'])")
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 400 rocprofv3 --pmc $C --output-format csv --kernel-include-regex hastar_search_kernel -d $R/$C -o pmc -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --latency-queries 0 > $OUT/pmc_$C.log 2>&1 || { tail -5 $OUT/pmc_$C.log; exit 1; }
+  timeout -s KILL 400 rocprofv3 --pmc $C --output-format csv --kernel-include-regex hastar_search_kernel -d $R/$C -o pmc -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --latency-queries 0 --relaxed-batch 0 > $OUT/pmc_$C.log 2>&1 || { tail -5 $OUT/pmc_$C.log; exit 1; }
 done
 python3 tools/prof_summary.py pmc $R/FETCH_SIZE $R/WRITE_SIZE $OUT/pmc_search_summary.json --batch $B --grid 1024 || exit 1
 cat $OUT/pmc_search_summary.json
@@ -29,6 +32,6 @@ for pass in "SQA SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_A
   set -- $pass
   name=$1; shift
   timeout -s KILL 400 rocprofv3 --pmc "$@" --output-format csv --kernel-include-regex hastar_search_kernel -d $R/$name -o pmc \
-    -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --latency-queries 0 > $OUT/pmc_$name.log 2>&1 || { tail -5 $OUT/pmc_$name.log; exit 1; }
+    -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --latency-queries 0 --relaxed-batch 0 > $OUT/pmc_$name.log 2>&1 || { tail -5 $OUT/pmc_$name.log; exit 1; }
 done
 python3 tools/prof_summary.py counters $OUT/counters_search.json $R/SQA $R/SQB --batch $B --dispatch -1 || exit 1
