@@ -78,10 +78,13 @@ def step_diag(planners, res):
     head = np.nonzero(t[:, 2] < head_cus)[0]
     first = head[np.argsort(t[head, 0])][:16]
     li = int(np.argmax(dur))
+    st = res.stats
+
+    def row(i):  # start offset ms, duration ms, arena, planner index, pops, inner A* pops
+        return [round(float((t[i, 0] - t0) * 1e-5), 1), round(float(dur[i]), 1), int(t[i, 2]), int(i),
+                int(st["pops"][i]), int(st["astar_pops"][i])]
     return {"kernel_ms": float(res.kernel_ms), "span_ms": float((t[:, 1].max() - t0) * 1e-5),
-            "split_ms": planners[0].split_ms(),
-            "head": [[round(float((t[i, 0] - t0) * 1e-5), 1), round(float(dur[i]), 1), int(t[i, 2])] for i in first],
-            "longest": [round(float((t[li, 0] - t0) * 1e-5), 1), round(float(dur[li]), 1), int(t[li, 2])]}
+            "split_ms": planners[0].split_ms(), "head": [row(i) for i in first], "longest": row(li)}
 
 
 def shard_query_ids(rank, world, batch, pred=None):

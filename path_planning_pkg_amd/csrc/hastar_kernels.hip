@@ -765,24 +765,34 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
     const v2i tpg = pvg_load(c, L, b);  // the popped node's {prev, g}
     const Cell2 tc = gload(&cells[tcell]);
     const int ni = tx + adx, nj = ty + ady;
-    bool valid = false, vis = false, closed = false;
-    float nf = 0.0f;
-    uint32_t ohint = 0xffffffffu;  // this lane's cell: last open node (| dup << 16), or none
-    float hg = 0.0f;               // g of that node (the open cell's record)
-    if (lane < nact && ni > -1 && ni < c.N && nj > -1 && nj < c.N) {
-      const uint32_t cell = (uint32_t)ni * (uint32_t)c.N + (uint32_t)nj;
-      const float occv = c.occ[cell];
-      const uint32_t visw = c.visited[cell >> 5];
+    // the neighbour probes are only issued here; the popped node leaves the LDS tree while they
+    // are in flight (the erase needs none of them), and they are consumed after it
+    const bool inb = lane < nact && ni > -1 && ni < c.N && nj > -1 && nj < c.N;
+    const uint32_t cell = inb ? (uint32_t)ni * (uint32_t)c.N + (uint32_t)nj : 0u;
+    float occv = 0.0f, nf = 0.0f;
+    uint32_t visw = 0u;
+    Cell2 cr{};
+    if (inb) {
+      occv = c.occ[cell];
+      visw = c.visited[cell >> 5];
       nf = c.nm_f[cell];
-      const Cell2 cr = gload(&cells[cell]);
-      valid = occv < c.thr;
-      vis = valid && ((visw >> (cell & 31)) & 1u);
-      closed = valid && cr.cgen == c.gen2;
-      if ((cr.oinfo >> CELL2_OGEN_SHIFT) == (c.gen2 & CELL2_OGEN_MASK)) ohint = cr.oinfo & CELL2_HINT_MASK;
-      hg = cr.g;
+      cr = gload(&cells[cell]);
     }
+    STAMP_T t_u = STAMP_NOW();
+    tr.unlink(b);
+    STAMP_ADD(24, t_u);
+    free_lds(c, tr, b);
+    ring_erase(L, rg, 0, lane);
     // consume every probe before the first store of this pop, so that no later register
     // reuse has to wait on a store (vmcnt counts loads and stores in issue order)
+    const bool valid = inb && occv < c.thr;
+    const bool vis = valid && ((visw >> (cell & 31)) & 1u);
+    const bool closed = valid && cr.cgen == c.gen2;
+    // this lane's cell: last open node (| dup << 16), or none; hg = that node's g (the open
+    // cell's record)
+    const uint32_t ohint = (inb && (cr.oinfo >> CELL2_OGEN_SHIFT) == (c.gen2 & CELL2_OGEN_MASK))
+                               ? (cr.oinfo & CELL2_HINT_MASK) : 0xffffffffu;
+    const float hg = inb ? cr.g : 0.0f;
     const uint64_t vmask = __ballot(valid), vismask = c.cost_only ? __ballot(vis) : 0ull, cmask = __ballot(closed);
     nf = __builtin_amdgcn_readfirstlane(0) + nf;  // keep nf live in a VGPR (no-op)
     const int tprev = ufi(tpg.x);
@@ -790,11 +800,6 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
     // this lane's hinted open node (the node a find of this cell usually returns); its g came
     // with the probe (hg), and a node's g never changes while it is open
     const int hy = (ohint != 0xffffffffu && !((ohint >> 16) & 1u)) ? (int)(ohint & 0xffffu) : NIL;
-    STAMP_T t_u = STAMP_NOW();
-    tr.unlink(b);
-    STAMP_ADD(24, t_u);
-    free_lds(c, tr, b);
-    ring_erase(L, rg, 0, lane);
     const int ci = (int)tcell;  // closed record = the cell's record
     float g0;
     if (ufu(tc.cgen) == c.gen2) {

@@ -267,9 +267,12 @@ struct RBT : Acc {
       sR(p, x);
       if (p == R(0)) sR(0, x);
     }
+    // xp = P(x) throughout; it is p after leaf(x, p), so the usual first iteration (x's new
+    // parent black) reads no link at all.  rootv = P(0) is refreshed after every rotation, so it
+    // is the root at the end.
     int rootv = P(0);
+    int xp = p;
     while (x != rootv) {
-      const int xp = P(x);
       if (C(xp) != RB_RED) break;
       const int xpp = P(xp);
       if (xp == L(xpp)) {
@@ -307,8 +310,9 @@ struct RBT : Acc {
           rootv = P(0);
         }
       }
+      xp = P(x);
     }
-    sC(P(0), RB_BLACK);
+    sC(rootv, RB_BLACK);
   }
 
   RB_HD int minimum(int x) {
