@@ -800,6 +800,17 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
     // this lane's hinted open node (the node a find of this cell usually returns); its g came
     // with the probe (hg), and a node's g never changes while it is open
     const int hy = (ohint != 0xffffffffu && !((ohint >> 16) & 1u)) ? (int)(ohint & 0xffffu) : NIL;
+    // that node's {key, f} for every lane in one LDS round trip (the popped node is already
+    // dead).  A node's key and f do not change while it lives, and no node gets a neighbour's
+    // cell before that neighbour's own insert, so these stay exact for the whole expansion
+    // unless a node is freed in it (a replaced find hit: then `freed` and the loop re-reads)
+    uint32_t hkey = 0xffffffffu;
+    float hf = 0.0f;
+    if (hy != NIL) {
+      hkey = L.kf[hy].key;
+      hf = L.kf[hy].f;
+    }
+    bool freed = false;
     const int ci = (int)tcell;  // closed record = the cell's record
     float g0;
     if (ufu(tc.cgen) == c.gen2) {
@@ -868,8 +879,12 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
         if (dup) {
           sc = same_cell(L, c.ps2.next, key, lane);
         } else {
-          const int y = (int)(hint & 0xffffu);
-          if (ufu(L.kf[y].key) == key) sc = SameCell{1, y, uff(L.kf[y].f)};
+          const int y = (int)(hint & 0xffffu);  // = lane k's hy
+          if (!freed) {
+            if (ufu((uint32_t)__builtin_amdgcn_readlane((int)hkey, k)) == key) sc = SameCell{1, y, rl_f(hf, k)};
+          } else if (ufu(L.kf[y].key) == key) {
+            sc = SameCell{1, y, uff(L.kf[y].f)};
+          }
         }
       }
       RankOut ra, rb;
@@ -913,6 +928,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
         }
         tr.unlink(hit);
         free_lds(c, tr, hit);
+        freed = true;
         ring_erase(L, rg, hit_rank, lane);
         if (st_node == hit) st_pv = false;  // a node inserted earlier in this expansion is gone
         STAMP_ADD(11, t_u);
