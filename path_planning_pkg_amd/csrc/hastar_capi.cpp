@@ -1818,7 +1818,17 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     ms_total += ms;
     return 0;
   };
+  // HASTAR_SPLIT_MODE=2: the head searches run on head workgroups of the batch kernel itself
+  // (wave 0 alone on its CU, the batch kernel's code and LDS layout) instead of the latency kernel
+  static const int split_mode = [] {
+    const char* e = std::getenv("HASTAR_SPLIT_MODE");
+    return e && std::atoi(e) == 2 ? 2 : 1;
+  }();
+  const bool split2 = split && slots > head && split_mode == 2;
   if (int r = timed([&]() -> hipError_t {
+        if (split2)
+          return launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, hard_pops, st, 0, -1,
+                               head);
         if (split && slots > head) {
           // the head's queue entries 0 .. head-1 are taken statically by the latency workgroups
           // (arenas 0 .. head-1); the batch kernel's waves count on from `head` (arenas head ..)
@@ -1844,7 +1854,7 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
                     : launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, hard_pops, st);
       }))
     return r;
-  if (split && slots > head) {
+  if (split && slots > head && !split2) {
     hipEventElapsedTime(&DC.split_ms[0], DC.ev0, DC.ev_hs);
     hipEventElapsedTime(&DC.split_ms[1], DC.ev0, DC.ev_head);
     hipEventElapsedTime(&DC.split_ms[2], DC.ev0, DC.ev_bs);

@@ -6,7 +6,8 @@
 namespace hastar {
 // the batch kernel: 8 search waves per CU (n_slots arenas; slot s runs in d_arenas[s])
 hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots, const int* d_order, int n_prio,
-                         int* d_next, long long hard_pops, hipStream_t st, int arena_base = 0, int q0 = 0);
+                         int* d_next, long long hard_pops, hipStream_t st, int arena_base = 0, int q0 = 0,
+                         int head_wgs = 0);
 hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, const int* d_order,
                          long long hard_pops, hipStream_t st);
 // the latency kernel: one search per CU (batches no larger than the CU count, resumes)

@@ -1725,11 +1725,17 @@ constexpr int BATCH_WAVES = 8;
 __global__ __launch_bounds__(64 * BATCH_WAVES) __attribute__((amdgpu_waves_per_eu(HASTAR_WAVES_PER_EU)))
 void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners, const SlotArena* __restrict__ arenas,
                           int n_slots, const int* __restrict__ order, int* __restrict__ next, long long hard_pops,
-                          int n_prio, int arena_base) {
+                          int n_prio, int arena_base, int head_wgs) {
   __shared__ ApfStage apfs[BATCH_WAVES];
   __shared__ AStarLdsT<NarrowA> alds[BATCH_WAVES];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
-  const int slot = (int)blockIdx.x * BATCH_WAVES + w;
+  // head_wgs > 0: workgroups 0 .. head_wgs - 1 are head workgroups whose wave 0 alone runs
+  // (a CU to itself), starting with queue entry b (the counter starts at head_wgs); slots
+  // 0 .. head_wgs - 1, then 8 per workgroup
+  const int b = (int)blockIdx.x;
+  const bool head = b < head_wgs;
+  if (head && w > 0) return;
+  const int slot = head ? b : head_wgs + (b - head_wgs) * BATCH_WAVES + w;
   if (slot >= n_slots) return;  // a whole wave: no arena for it
   SearchCtx c;
   c.A = arenas + slot;
@@ -1739,10 +1745,14 @@ void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners, 
   c.cost_only = true;
   c.gen3 = gp(A.gens)[0];
   c.gen2 = gp(A.gens)[1];
-  for (;;) {
+  for (bool first = true;; first = false) {
     int q = 0;
-    if (c.lane == 0) q = atomicAdd(next, 1);
-    q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
+    if (first && head) {
+      q = b;
+    } else {
+      if (c.lane == 0) q = atomicAdd(next, 1);
+      q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
+    }
     if (q >= n_planners) break;
     // the queue is ordered longest-expected-first; the head of it runs at raised issue
     // priority so the batch's stragglers are not slowed by the waves sharing their SIMD
@@ -2442,16 +2452,17 @@ __global__ __launch_bounds__(64) void k_test_dubins_path(PlannerDev P, float sx,
 
 // ------------------------------------------------------------- launch wrappers -------
 hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots, const int* d_order, int n_prio,
-                         int* d_next, long long hard_pops, hipStream_t st, int arena_base, int q0) {
+                         int* d_next, long long hard_pops, hipStream_t st, int arena_base, int q0, int head_wgs) {
   // work counter q0 (>= 0: reset it; -1: the caller set it)
+  if (head_wgs > 0) q0 = head_wgs;
   if (q0 >= 0) {
     const int init[4] = {q0, 0, 0, 0};
     hipError_t e = hipMemcpyAsync(d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return e;
   }
-  const int groups = (n_slots + BATCH_WAVES - 1) / BATCH_WAVES;
+  const int groups = head_wgs + (n_slots - head_wgs + BATCH_WAVES - 1) / BATCH_WAVES;
   hipLaunchKernelGGL(hastar_search_kernel, dim3(groups), dim3(64 * BATCH_WAVES), 0, st, d_descs, n, d_arenas, n_slots,
-                     d_order, d_next, hard_pops, n_prio, arena_base);
+                     d_order, d_next, hard_pops, n_prio, arena_base, head_wgs);
   return hipGetLastError();
 }
 // HASTAR_WIDE_DBG (diagnostics): bit 0 keeps the latency kernel's outer tree in HBM
