@@ -28,7 +28,7 @@ int hastar_debug_motion(hastar_handle h, float* off, float* dth, float* cost, fl
                         float* r_min);
 int hastar_debug_closed_keys(hastar_handle h, int* out, int cap);
 /* Cycles per search phase of the last search (all zero unless built with -DHASTAR_STAMPS). */
-int hastar_debug_cycles(hastar_handle h, unsigned long long* out32);
+int hastar_debug_cycles(hastar_handle h, unsigned long long* out40);
 /* {inner A* searches migrated from LDS to HBM, inner A* pops done in HBM mode} of the last search. */
 int hastar_debug_astar_modes(hastar_handle h, long long* out2);
 /* Timing of the last search: {t_start, t_end} in s_memrealtime ticks (100 MHz, chip-wide

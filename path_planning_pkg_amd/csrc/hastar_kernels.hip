@@ -832,6 +832,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
       return true;
     }
     STAMP_ADD(8, t_pop);
+    STAMP_T t_pre = STAMP_NOW();
     // every neighbour's key, g and f (AStar.cpp:160-176) in its own lane, in the reference's
     // float order (g0 + cost, then + h): the loop below reads them instead of computing them
     const uint32_t key_l = ((uint32_t)ni << 16) | ((uint32_t)nj & 0xffffu);
@@ -844,6 +845,8 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
     float st_f = 0.0f, st_g = 0.0f;
     int st_node = NIL;
     bool st_on = false, st_pv = false;  // st_pv: pvg[st_node] = {ci, st_g} is still due
+    STAMP_ADD(33, t_pre);
+    STAMP_T t_nl = STAMP_NOW();
     for (int k = 0; k < nact; ++k) {
       if (!((vmask >> k) & 1ull)) continue;
       const float kcost = rl_f(acost, k);
@@ -918,7 +921,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
           st_hint = nn == NIL ? ohint : ((uint32_t)nn | (uint32_t)(dup || sc.cnt > 0) << 16);
         }
         STAMP_ADD(10, t_i);
-      } else if (gn < hit_g(c, L, hit, k, hy, hg, sc.cnt == 1 && sc.idx == hit, st_pv, st_node, st_g)) {
+      } else if (STAMP_T t_rp = STAMP_NOW(); gn < hit_g(c, L, hit, k, hy, hg, sc.cnt == 1 && sc.idx == hit, st_pv, st_node, st_g)) {
         STAMP_T t_u = STAMP_NOW();
         if (hit_rank < 0) {
           const float hf = tr.F(hit);
@@ -947,8 +950,10 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
           st_pv = nn != NIL;
           st_hint = nn == NIL ? ohint : ((uint32_t)nn | (uint32_t)(dup || sc.cnt > 0) << 16);
         }
+        STAMP_ADD(34, t_rp);
       }
     }
+    STAMP_ADD(32, t_nl);
     STAMP_T t_e = STAMP_NOW();
     if (st_on) {
       c.nm_f[st_cell] = st_f;
@@ -972,6 +977,7 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLdsT<CF>& L, int s
   const SlotArena& A = *c.A;
   const int lane = c.lane;
   const size_t s_cell = (size_t)si * c.N + sj;
+  STAMP_T t_hs = STAMP_NOW();
   if (check_start && ((c.visited[s_cell >> 5] >> (s_cell & 31)) & 1u)) return c.nm_f[s_cell];
   const float h0 = euclid_h(P, si, sj);
   c.nm_f[s_cell] = h0;  // Grid2D::set_start_node_grid -> Node2D::soft_reset
@@ -1006,6 +1012,7 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLdsT<CF>& L, int s
     acost = (adx != 0 && ady != 0) ? P.act_cost_diag : P.act_cost_axis;
   }
   float result = FLT_MAX;
+  STAMP_ADD(35, t_hs);
   if (astar_loop_lds(c, tl, L, rg, adx, ady, acost, &result)) return result;
   // migrate the LDS tree to HBM nodes (identical indices) and continue there
   c.amigr++;

@@ -89,7 +89,7 @@ constexpr uint32_t SLOT3_IDX_MASK = (1u << SLOT3_IDX_BITS) - 1;
 constexpr uint32_t SLOT3_GEN_MASK = 0xffu;
 
 // diagnostic phase counters of the search kernel (-DHASTAR_STAMPS)
-constexpr int NSTAMP = 32;
+constexpr int NSTAMP = 40;
 
 // Search status codes of SearchResult::status besides 0 / HASTAR_E* (host-side only).
 constexpr int SEARCH_NOT_RUN = -1;  // the host's sentinel: no wave took this planner

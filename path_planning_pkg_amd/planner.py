@@ -367,7 +367,7 @@ class HybridAStar:
         return out[:min(n, cap)].copy()
 
     def cycles(self):
-        out = (C.c_ulonglong * 32)()
+        out = (C.c_ulonglong * 40)()
         _check(load_library().hastar_debug_cycles(self.h, out))
         return list(out)
 

@@ -50,7 +50,10 @@ for s in args.seeds:
                                                                      "memoise"])},
                           lds_astar_parts_per_apop={n: round(cyc[i] / max(st["astar_pops"] - modes["astar_pops_hbm"], 1))
                                                     for i, n in ((24, "pop_unlink"), (25, "insert_link"),
-                                                                 (30, "ring_insert"), (31, "expansion_stores"))},
+                                                                 (30, "ring_insert"), (31, "expansion_stores"),
+                                                                 (32, "neighbour_loop"), (33, "lane_precompute"),
+                                                                 (34, "replace_path"))},
+                          astar_setup_per_search=round(cyc[35] / max(st["astar_searches"], 1)),
                           outer_per_pop={n: round(cyc[13 + i] / max(st["pops"], 1))
                                          for i, n in enumerate(["find3", "insert3", "unlink3", "succ_gen", "apf",
                                                                 "dubins", "insert_walk", "insert_link",
