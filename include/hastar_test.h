@@ -45,7 +45,8 @@ int hastar_debug_pooled_resumes(long long* out);
 /* The device's relaxed-mode arena pool: {arenas (= resident workgroups of a relaxed launch), MiB each}. */
 int hastar_debug_relaxed_pool(hastar_handle h, long long* out2);
 /* The cold-order score of a planner with no history (host only): sum over the boxes {x, y, dx, dy}
- * (world frame) of 1 / (1 + d)^2, d = distance between the box and the start-goal segment. */
+ * (world frame) of (1 + t) / (1 + d)^3, d = distance between the box and the start-goal segment,
+ * t = the box centre's position along it (0 at the start, 1 at the goal). */
 double hastar_test_route_score(const float* boxes, int n, const float start[2], const float goal[2]);
 /* The relaxed kernel's per-wave progress words (4 per wave: phase, round, expansion-set size,
  * expansion index; workgroup b, wave w at [(b * 8 + w) * 4]) in pinned host memory, readable

@@ -234,7 +234,7 @@ def synthetic_ref_boxes_many(N, K, seeds, res=0.5, clear=8.0):
 def route_score(boxes, start, goal):
     """The library's cold-order key (hastar_capi.cpp:route_score) for many box sets at once:
     boxes (Q, K, 4) {x, y, dx, dy} in the world frame, start/goal (2,) or (Q, 2): sum over a
-    row's boxes of 1 / (1 + d)^2, d = distance between the axis-aligned box and the start-goal
+    row's boxes of (1 + t) / (1 + d)^3, d = distance between the axis-aligned box and the start-goal
     segment (0 when the segment crosses it)."""
     b = np.asarray(boxes, np.float64)
     s = np.broadcast_to(np.asarray(start, np.float64), (b.shape[0], 2))[:, None, :]
@@ -267,7 +267,10 @@ def route_score(boxes, start, goal):
     for px, py in ((x0, y0), (x1, y0), (x0, y1), (x1, y1)):
         m = np.minimum(m, pt_seg(px, py))
     d = np.where(hit, 0.0, m)
-    return (1.0 / (1.0 + d) ** 2).sum(axis=-1)
+    cx, cy = b[..., 0], b[..., 1]
+    L2 = dx * dx + dy * dy
+    t = np.clip(np.where(L2 > 0, ((cx - ax) * dx + (cy - ay) * dy) / np.where(L2 > 0, L2, 1.0), 0.0), 0, 1)
+    return ((1.0 + t) / (1.0 + d) ** 3).sum(axis=-1)
 
 
 def predicted_cost(N, K, query_ids, res=0.5, apf_r=2.5, chunk=8192):
