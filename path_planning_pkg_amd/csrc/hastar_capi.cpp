@@ -1826,10 +1826,8 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   };
   // HASTAR_SPLIT_MODE=2: the head searches run on head workgroups of the batch kernel itself
   // (wave 0 alone on its CU, the batch kernel's code and LDS layout) instead of the latency kernel
-  static const int split_mode = [] {
-    const char* e = std::getenv("HASTAR_SPLIT_MODE");
-    return e && std::atoi(e) == 2 ? 2 : 1;
-  }();
+  const char* sm_env = std::getenv("HASTAR_SPLIT_MODE");
+  const int split_mode = sm_env && std::atoi(sm_env) == 2 ? 2 : 1;
   const bool split2 = split && slots > head && split_mode == 2;
   if (int r = timed([&]() -> hipError_t {
         if (split2)

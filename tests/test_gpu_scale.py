@@ -158,12 +158,15 @@ def test_cfg3_parity_batch(gpu, oracle_lib, monkeypatch, wide):
     assert max(r["stats"]["pops"] for r in res) > 100000  # the long query is in the batch
 
 
-def test_split_launch_head_and_bulk(gpu, oracle_lib, monkeypatch):
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_split_launch_head_and_bulk(gpu, oracle_lib, monkeypatch, mode):
     """A batch split over both kernels at once (HASTAR_SPLIT, as large batches run): the head of
-    the queue on the latency CUs, the rest on the batch kernel beside them, one work counter.
-    Every planner's result is the oracle's, and both kernels took work."""
+    the queue on the latency CUs, the rest on the batch kernel beside them, one work counter
+    (mode 2: the head on single-wave head workgroups of the batch kernel itself).  Every
+    planner's result is the oracle's, and both the head and the bulk took work."""
     monkeypatch.setenv("HASTAR_WIDE", "0")
     monkeypatch.setenv("HASTAR_SPLIT", "1")
+    monkeypatch.setenv("HASTAR_SPLIT_MODE", mode)
     cases = [synthetic(256, 36, 10 + (s % 4) * 10, s) for s in range(1, 25)] + [synthetic(512, 72, 50, 1)]
     gs, os_ = [], []
     for cfg, proto in cases:
