@@ -277,6 +277,10 @@ def main():
     t0 = time.perf_counter()
     r0 = step()
     progress("cold first step done")
+    # the first step's outcome of a stratified sample (every 64th query and the 8 with the most
+    # pops), paths included, for the bit-exact check against the oracle after the timed region
+    strat = sorted(set(range(0, B, 64)) | set(np.argsort(-r0.stats["pops"], kind="stable")[:8].tolist()))
+    cold_sample = {i: r0.result(i) for i in strat} if (rank == 0 and not args.no_cpu_baseline) else None
     cold_s = time.perf_counter() - t0
     cold_pops = int(r0.stats["pops"].sum())
     cold_s, cold_pops_all = reduce_over_ranks(dist, cold_s, cold_pops, f"cuda:{device}")
@@ -427,6 +431,8 @@ def main():
             # the CPU sample runs the rank's queries in query-id order (a representative sample,
             # not the predicted-costliest head of the GPU batch), latency queries first
             sample = lat_ids + [i for i in np.argsort(qids, kind="stable") if i not in lat_ids]
+            progress("parity sample")
+            out["parity_sample"] = parity_sample(cfgs, cold_sample, [qids[i] for i in sorted(cold_sample)])
             progress("cpu baseline")
             cb = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps, lat_ids, sample)
             out["cpu_baseline"] = cb
@@ -806,6 +812,44 @@ def cpu_baseline_cfg5(pairs, budget_s, ticks):
             "sample": f"first {n} pairs of rank 0 x {ticks} ticks (same call sequence as the GPU run), find_path only, "
                       f"{T} threads with one private planner each (oracle/hastar_oracle.cpp, -O3)",
             "tick_ms_one_core_per_pair": float(tick_max.mean()) if n else None}
+
+
+def parity_sample(cfgs, gpu, qids):
+    """Bit-exact check at the bench's own size, outside the timed region: the first (cold) step's
+    result of a stratified sample of the batch (`gpu`: planner index -> result, every 64th query
+    plus the 8 longest) against the oracle's reset + find_path on the same maps, on the host's
+    threads: success, cost bits, the search statistics and digests, path and curvature bits."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle.pyoracle import OraclePlanner
+    from tests.scenarios import drive
+    idx = sorted(gpu)
+
+    def run(i):
+        o = OraclePlanner(cfgs[i][0])
+        drive(o, cfgs[i][1])
+        o.reset()
+        r = o.find_path(cfgs[i][1]["vel"], cfgs[i][1]["start"])
+        o.close()
+        return r
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cpu_threads()) as ex:
+        res = list(ex.map(run, idx))
+    keys = ("pops", "successors", "astar_pops", "astar_searches", "shots", "closed_size", "pop_digest",
+            "closed_digest", "via_shot")
+    bad = []
+    for i, q, o in zip(idx, qids, res):
+        g = gpu[i]
+        same = (g["ok"] == o["ok"] and np.float32(g["cost"]).tobytes() == np.float32(o["cost"]).tobytes()
+                and all(g["stats"][k] == o["stats"][k] for k in keys)
+                and g["path"].tobytes() == o["path"].tobytes() and g["curvature"].tobytes() == o["curvature"].tobytes())
+        if not same:
+            bad.append(int(q))
+    return {"queries": len(idx), "bit_exact": not bad, "mismatched_queries": bad[:16],
+            "pops_checked": int(sum(int(gpu[i]["stats"]["pops"]) for i in idx)),
+            "path_poses_checked": int(sum(len(gpu[i]["path"]) for i in idx)), "oracle_s": time.perf_counter() - t0,
+            "note": "first (cold) step of every 64th query and the 8 longest, against the oracle's reset + "
+                    "find_path: success, cost, statistics, pop/closed digests, path and curvature bits"}
 
 
 def cpu_baseline(cfgs, gpu_results, budget_s, replans, lat_ids, sample=None):

@@ -45,3 +45,32 @@ def test_step_balance():
     assert abs(b["slot_busy_mean_ms"] - 3.0) < 1e-9
     assert abs(b["busy_frac"] - 0.75) < 1e-9
     assert abs(b["longest_search_under_load_ms"] - 3.0) < 1e-9 and b["longest_search_start_ms"] == 0.0
+
+
+def test_parity_sample_compares_every_field():
+    """bench.parity_sample (the bench's bit-exact check of a stratified sample of its own batch):
+    results equal to the oracle's pass, a one-bit difference in a path or a digest fails."""
+    import numpy as np
+    import bench
+    from oracle.pyoracle import OraclePlanner
+    from tests.scenarios import drive, synthetic_ref
+    cfgs = [synthetic_ref(256, 36, 20, s) for s in (1, 2, 3)]
+    ref = {}
+    for i, (cfg, proto) in enumerate(cfgs):
+        o = OraclePlanner(cfg)
+        drive(o, proto)
+        o.reset()
+        ref[i] = o.find_path(proto["vel"], proto["start"])
+        o.close()
+    r = bench.parity_sample(cfgs, ref, [0, 1, 2])
+    assert r["bit_exact"] and r["queries"] == 3 and r["path_poses_checked"] > 0, r
+    bent = dict(ref)
+    p = ref[1]["path"].copy()
+    p.view(np.uint32)[0, 0] ^= 1
+    bent[1] = dict(ref[1], path=p)
+    r = bench.parity_sample(cfgs, bent, [10, 11, 12])
+    assert not r["bit_exact"] and r["mismatched_queries"] == [11], r
+    st = dict(ref[2]["stats"], closed_digest=ref[2]["stats"]["closed_digest"] ^ 1)
+    bent = dict(ref)
+    bent[2] = dict(ref[2], stats=st)
+    assert bench.parity_sample(cfgs, bent, [0, 1, 2])["mismatched_queries"] == [2]
