@@ -257,8 +257,10 @@ int device_ctx(int dev, DeviceCtx** out) {
     HIPCHK(hipGetDeviceProperties(&prop, dev));
     D.resident_slots = search_slots_per_cu() * prop.multiProcessorCount;
     D.n_cu = prop.multiProcessorCount;
-    // head CUs (HASTAR_HEAD_CUS, default 8; 0 = no split)
-    int hc = 8;
+    // head CUs (HASTAR_HEAD_CUS, default 16; 0 = no split).  16 rather than 8: with 8, one step
+    // in 6-10 ran every latency-CU search 1.6-1.9x slower; 56 steps with 16 showed none, at the
+    // same mean (profiles/r03s_bench_h*.all.jsonl)
+    int hc = 16;
     if (const char* e = std::getenv("HASTAR_HEAD_CUS")) hc = std::atoi(e);
     if (hc > 0 && D.n_cu >= 8 * hc) {
       if (hipStreamCreateWithFlags(&D.head_st, hipStreamNonBlocking) == hipSuccess &&

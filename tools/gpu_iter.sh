@@ -7,6 +7,7 @@
 #   benchlong0 the same with HASTAR_SPLIT=0 (no latency CUs)   -> bench_long_nosplit.json
 #   benchdrv  bench.py --steps 20 --warmup 5 (the driver's command line)  -> bench_drv.json
 #   headcus   16-step benches: split mode 1 / 2 with 8 head CUs, mode 1 with 16 -> bench_mode*_head*.json
+#   head20    20-step benches alternating 8 and 16 latency CUs (x2)  -> bench_h{8,16}.all.jsonl
 #   cfg4      bench.py --workload cfg4                              -> bench_cfg4.json
 #   cfg5      bench.py --workload cfg5                                  -> bench_cfg5.json
 #   stamps    single-query phase stamps (lib_stamps build) of the bench's longest query and seed 1
@@ -36,6 +37,8 @@ for st in "$@"; do
     headcus) for cfg in "1 8" "2 8" "1 16"; do set -- $cfg
              HASTAR_SPLIT_MODE=$1 HASTAR_HEAD_CUS=$2 timeout -k 10 600 python -u bench.py --steps 16 --warmup 2 --step-diag --no-cpu-baseline --latency-queries 0 --relaxed-batch 0 > $O/bench_mode$1_head$2.json 2> $O/bench_mode$1_head$2.err || { tail -30 $O/bench_mode$1_head$2.err; exit 1; }
              python -c "import json; d=json.load(open('$O/bench_mode$1_head$2.json')); print('mode $1 head $2', d['value'], [round(k) for k in d['kernel_ms_per_step']])"; done ;;
+    head20) for hc in 8 16 8 16; do HASTAR_HEAD_CUS=$hc timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --step-diag --no-cpu-baseline --latency-queries 0 --relaxed-batch 0 > $O/bench_h$hc.json 2> $O/bench_h$hc.err || { tail -30 $O/bench_h$hc.err; exit 1; }
+             python -c "import json; d=json.load(open('$O/bench_h$hc.json')); print($hc, d['value'], [round(k) for k in d['kernel_ms_per_step']])"; cat $O/bench_h$hc.json >> $O/bench_h$hc.all.jsonl; done ;;
     cfg4)  timeout -k 10 900 python -u bench.py --workload cfg4 > $O/bench_cfg4.json 2> $O/bench_cfg4.err || { tail -30 $O/bench_cfg4.err; exit 1; }
            cut -c1-400 $O/bench_cfg4.json ;;
     cfg5)  timeout -k 10 600 python -u bench.py --workload cfg5 > $O/bench_cfg5.json 2> $O/bench_cfg5.err || { tail -30 $O/bench_cfg5.err; exit 1; }
