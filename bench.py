@@ -181,7 +181,7 @@ def parse_args(argv=None):
                     help="cfg3/cfg4 inputs: SURVEY.md §8d's std::mt19937 draws (the survey's reference runs) or "
                          "round 1's numpy PCG64 draws")
     ap.add_argument("--relaxed-delta", type=float, default=0.25, help="relaxed mode: frontier width (m)")
-    ap.add_argument("--relaxed-weight", type=float, default=1.2, help="relaxed mode: heuristic weight")
+    ap.add_argument("--relaxed-weight", type=float, default=1.35, help="relaxed mode: heuristic weight (the library default)")
     ap.add_argument("--no-relaxed", action="store_true", help="cfg5: skip the relaxed-mode comparison")
     ap.add_argument("--relaxed-batch-nodes", type=int, default=1 << 16,
                     help="relaxed batch: node capacity per search (hastar_relaxed_opts.max_nodes)")

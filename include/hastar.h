@@ -178,12 +178,12 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel_init
 typedef struct hastar_relaxed_opts {
   float delta;     /* frontier width in metres [0.25] */
   float h_stop;    /* the Dijkstra covers the ellipse d(c) + |c - start| <= h_stop x |goal - start| + 64 moves;
-                      cells outside get bound - |c - start| [1.5] */
+                      cells outside get bound - |c - start| [1.2] */
   int max_nodes;   /* node capacity per search; beyond it the search ends with HASTAR_EOVERFLOW [1 << 18] */
   int max_rounds;  /* [1 << 20] */
-  float h_weight;  /* f = g + h_weight x max(h, Dubins length); > 1 trades cost for speed [1.2]
-                      (at the defaults the measured costs were 0.92-1.00 x the exact mode's,
-                      profiles/relaxed_sweep_r02.json) */
+  float h_weight;  /* f = g + h_weight x max(h, Dubins length); > 1 trades cost for speed [1.35]
+                      (defaults from profiles/r03t_relaxed_sweep.json: costs 0.92-1.01 x the exact
+                      mode's, the cfg3 and cfg5 groups in 10.3 and 8.4 ms) */
   int reuse_heuristic; /* 1: the planner keeps its heuristic field (N*N floats of device memory)
                           and later relaxed calls reuse it until reset() or update_goal(), as the
                           reference's A* memo persists across replans; map updates in between

@@ -2136,9 +2136,9 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
   }
   RelaxParams rp{};
   rp.delta = opts && opts->delta > 0.0f ? opts->delta : 0.25f;
-  rp.h_stop = opts && opts->h_stop >= 1.0f ? opts->h_stop : 1.5f;
+  rp.h_stop = opts && opts->h_stop >= 1.0f ? opts->h_stop : 1.2f;
   rp.max_rounds = opts && opts->max_rounds > 0 ? opts->max_rounds : (1 << 20);
-  rp.h_weight = opts && opts->h_weight > 0.0f ? opts->h_weight : 1.2f;
+  rp.h_weight = opts && opts->h_weight > 0.0f ? opts->h_weight : 1.35f;
   rp.h_coarse = opts && opts->h_coarse > 0 ? opts->h_coarse : 2;
   if (rp.h_coarse != 1 && rp.h_coarse != 2 && rp.h_coarse != 4) return fail(HASTAR_EINVAL, "h_coarse must be 1, 2 or 4");
   const int nodes = opts && opts->max_nodes > 0 ? opts->max_nodes : (1 << 18);

@@ -18,7 +18,7 @@ from path_planning_pkg_amd import planner as gpu  # noqa: E402
 from tests.scenarios import drive, replan_pairs, synthetic  # noqa: E402
 
 # (delta, h_weight, h_stop, h_coarse)
-SETTINGS = [(0.25, 1.2, 1.5, 1), (0.25, 1.2, 1.5, 2), (0.25, 1.2, 1.5, 4), (0.5, 1.2, 1.5, 2), (0.25, 1.2, 2.0, 2)]
+SETTINGS = [(0.25, 1.2, 1.5, 2), (0.25, 1.2, 1.3, 2), (0.25, 1.2, 1.2, 2), (0.25, 1.35, 1.5, 2), (0.25, 1.35, 1.3, 2), (0.35, 1.2, 1.5, 2)]
 
 
 def groups(names):
