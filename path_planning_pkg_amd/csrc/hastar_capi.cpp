@@ -189,6 +189,7 @@ struct DeviceCtx {
   PlannerDev* d_descs = nullptr;
   int* d_order = nullptr;
   int* d_next = nullptr;
+  bool kernels_warm = false;  // the search kernels' code objects are loaded (hastar_reserve)
   SearchResult* d_results = nullptr;
   SearchResult* h_results = nullptr;   // pinned
   long long* d_off = nullptr;          // path point offsets of the packed hand-back
@@ -1756,6 +1757,14 @@ int hastar_reserve(const hastar_handle* hs, int n, long long path_points) {
   if (int rc = arenas_acquire(DC, need, batch_shape(DC, n).W)) return rc;
   if (int rc = batch_acquire(DC, n)) return rc;
   if (path_points > 0) HIPCHK(points_acquire(DC, (size_t)path_points));
+  // both search kernels once on an empty queue (every wave exits at its first queue read), so
+  // that their code objects are loaded here and not in the batch's first call
+  if (!DC.kernels_warm) {
+    HIPCHK(launch_search(DC.d_descs, 0, DC.d_arenas, 1, DC.d_order, 0, DC.d_next, 0, DC.stream));
+    HIPCHK(launch_search_wide(DC.d_descs, 0, DC.d_arenas, 1, DC.d_order, DC.d_next, 0, DC.stream, 0));
+    HIPCHK(hipStreamSynchronize(DC.stream));
+    DC.kernels_warm = true;
+  }
   return 0;
 }
 
