@@ -4,8 +4,9 @@
 // hastar_velocity_profile_batch).
 //
 // Same constructor and generate_velocity_profile signature, so local_planner.cpp:164-165,
-// 323, 332, 451, 460 compile unchanged against this header.  Differences a caller can observe:
-//   * only T = float exists (the ROS node instantiates float);
+// 323, 332, 451, 460 compile unchanged against this header.  Both instantiations of the
+// reference exist (VelocityGenerator.cpp:88-89): float (bit-exact) and double (device f64
+// libm: within 1e-12 relative of the reference).  Differences a caller can observe:
 //   * an empty path (undefined behaviour in the reference) or a device failure throws
 //     std::runtime_error;
 //   * generate_velocity_profiles (not in the reference) profiles many paths in one launch;
@@ -19,12 +20,13 @@
 #include <vector>
 
 #include "../hastar.h"
+#include "../hastar_f64.h"
 #include "common.h"
 
 namespace planning {
 
 template <typename T>
-class VelocityGenerator;  // only the float specialisation below is provided
+class VelocityGenerator;  // float and double specialisations below
 
 template <>
 class VelocityGenerator<float> {
@@ -62,6 +64,41 @@ class VelocityGenerator<float> {
 
  private:
   hastar_velocity_params _p;
+  int _device;
+};
+
+template <>
+class VelocityGenerator<double> {
+ public:
+  VelocityGenerator(double max_velocity, double coast_velocity, double max_lat_acc, double max_long_acc,
+                    double max_long_dec)
+      : _p{max_velocity, coast_velocity, max_lat_acc, max_long_acc, max_long_dec} {
+    const char* d = std::getenv("HASTAR_DEVICE");
+    _device = d ? std::atoi(d) : 0;
+  }
+  bool generate_velocity_profile(const double vel_init, const double max_velocity_curr,
+                                 const std::vector<Vector3D<double>>& path, const std::vector<double>& curvature,
+                                 std::vector<double>& velocity, bool coast_to_goal, bool stop_at_goal = false) const {
+    if (path.empty() || curvature.size() < path.size())
+      throw std::runtime_error("VelocityGenerator: empty path or short curvature vector");
+    const long long off[2] = {0, (long long)path.size()};
+    std::vector<double> xyh(3 * path.size());
+    for (size_t i = 0; i < path.size(); ++i) {
+      xyh[3 * i] = path[i]._x;
+      xyh[3 * i + 1] = path[i]._y;
+      xyh[3 * i + 2] = path[i]._heading;
+    }
+    velocity.resize(path.size());
+    const unsigned char flags = (unsigned char)((coast_to_goal ? 1 : 0) | (stop_at_goal ? 2 : 0));
+    unsigned char feasible = 0;
+    const int rc = hastar_velocity_profile_batch_f64(_device, &_p, 1, off, xyh.data(), curvature.data(), &vel_init,
+                                                     &max_velocity_curr, &flags, velocity.data(), &feasible);
+    if (rc != 0) throw std::runtime_error(std::string("hastar_velocity_profile_batch_f64: ") + hastar_last_error());
+    return feasible != 0;
+  }
+
+ private:
+  hastar_velocity_params_f64 _p;
   int _device;
 };
 

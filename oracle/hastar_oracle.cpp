@@ -41,6 +41,7 @@
 #include <thread>
 
 #include "../include/hastar.h"
+#include "../include/hastar_f64.h"
 
 namespace orc {
 // Optional pop limit for census tools (0 = none, the reference's behaviour): a search that
@@ -88,6 +89,9 @@ static inline uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 static inline uint32_t f32bits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+// the pop digest's g term: the float bit pattern, or the double's 64 bits (HybridAStar<double>)
+static inline uint64_t gbits(float g) { return f32bits(g); }
+static inline uint64_t gbits(double g) { uint64_t u; std::memcpy(&u, &g, 8); return u; }
 
 // ------------------------------------------------------------------ Dubins (Dubins.cpp)
 enum Word { RSR = 0, RSL = 1, LSR = 2, LSL = 3 };
@@ -353,9 +357,10 @@ template <class T> struct Planner {
   // statistics
   hastar_stats st{};
 
-  static std::vector<T> tovec(const float* p, int n) { return std::vector<T>(p, p + n); }
+  template <class In> static std::vector<T> tovec(const In* p, int n) { return std::vector<T>(p, p + n); }
 
-  explicit Planner(const hastar_params& p)
+  // PR = hastar_params (float inputs) or hastar_params_f64 (HybridAStar<double>)
+  template <class PR> explicit Planner(const PR& p)
       : shot_interval(p.dubins_shot_interval), shot_decay(p.dubins_shot_interval_decay),
         res(p.grid_resolution),
         thr(std::log(static_cast<T>(p.obstacle_threshold) / (1.0 - static_cast<T>(p.obstacle_threshold)))),
@@ -392,7 +397,7 @@ template <class T> struct Planner {
     visited.assign((size_t)N * N, 0);
   }
   // HybridAStar.cpp:22-24 (tan_max over steering, HybridAStar.h:20-25)
-  static T min_radius(const hastar_params& p) {
+  template <class PR> static T min_radius(const PR& p) {
     T mx = *std::max_element(p.steering, p.steering + p.num_steering);
     T tm = std::tan(mx);
     return static_cast<T>(p.wheelbase) / (std::cos(std::atan2(static_cast<T>(p.rear_to_cg) * tm,
@@ -416,7 +421,7 @@ template <class T> struct Planner {
     }
   }
   // Grid3D::update_obstacles(boxes) (Grid3D.cpp:22-44) + Grid2D boxes (Grid2D.cpp:99-139)
-  void boxes(const float* b, const float* conf, int n, T apf_r) {
+  template <class In> void boxes(const In* b, const In* conf, int n, T apf_r) {
     apf.clear();
     for (int k = 0; k < n; ++k) {
       T ox = b[4 * k], oy = b[4 * k + 1], dx = b[4 * k + 2], dy = b[4 * k + 3];
@@ -442,7 +447,7 @@ template <class T> struct Planner {
     }
   }
   // Grid2D::update_obstacles(lines) (Grid2D.cpp:142-194)
-  void lines(const float* L, const float* conf, int n, T width) {
+  template <class In> void lines(const In* L, const In* conf, int n, T width) {
     for (int k = 0; k < n; ++k) {
       P2<T> a = rot2<T>(static_cast<T>(L[4 * k]) - goal2.x, static_cast<T>(L[4 * k + 1]) - goal2.y, grid_heading);
       P2<T> b = rot2<T>(static_cast<T>(L[4 * k + 2]) - goal2.x, static_cast<T>(L[4 * k + 3]) - goal2.y, grid_heading);
@@ -728,7 +733,7 @@ template <class T> struct Planner {
       op3.erase(it);
       st.pops++;
       dig = mix64(dig ^ (((uint64_t)(uint32_t)cur->cx << 40) | ((uint64_t)(uint32_t)cur->cy << 16) |
-                         (uint64_t)(uint32_t)cur->bin)) + f32bits((float)cur->g);
+                         (uint64_t)(uint32_t)cur->bin)) + gbits(cur->g);
       if (cur->cx == goal_node.cx && cur->cy == goal_node.cy) {
         terminal = *cur;
         out = {terminal.g, true};
@@ -1224,3 +1229,115 @@ extern "C" void orc_shape_stats(long long* out) {
   for (int q = 0; q < 16; ++q) out[q] = orc::g_shape[q], orc::g_shape[q] = 0;
 }
 #endif
+
+// =========================================== HybridAStar<double> / VelocityGenerator<double>
+// The reference's second instantiation (HybridAStar.cpp:285-286, VelocityGenerator.cpp:88-89),
+// the checker of the device double planner (include/hastar_f64.h): the same templated
+// restatement as above with T = double, glibc double libm.
+using OP64 = orc::Planner<double>;
+
+extern "C" {
+
+void* orc64_create(const hastar_params_f64* p) { return new OP64(*p); }
+void orc64_destroy(void* h) { delete static_cast<OP64*>(h); }
+void orc64_update_goal(void* h, const double g[3], const double s[3]) {
+  static_cast<OP64*>(h)->update_goal({g[0], g[1], g[2]}, {s[0], s[1], s[2]});
+}
+void orc64_reset(void* h) { static_cast<OP64*>(h)->reset(); }
+void orc64_update_boxes(void* h, const double* b, const double* c, int n, double r) { static_cast<OP64*>(h)->boxes(b, c, n, r); }
+void orc64_update_lines(void* h, const double* l, const double* c, int n, double w) { static_cast<OP64*>(h)->lines(l, c, n, w); }
+void orc64_decay(void* h) { static_cast<OP64*>(h)->decay(); }
+void orc64_get_obstacles(void* h, double* out) {
+  auto* P = static_cast<OP64*>(h);
+  std::memcpy(out, P->occ.data(), P->occ.size() * sizeof(double));
+}
+void orc64_get_memo(void* h, double* f_out, unsigned char* visited_out) {
+  auto* P = static_cast<OP64*>(h);
+  std::memcpy(f_out, P->nm_f.data(), P->nm_f.size() * sizeof(double));
+  std::memcpy(visited_out, P->visited.data(), P->visited.size());
+}
+int orc64_find_path(void* h, double vel, const double start[3], double* xyh, double* curv, int cap, int* len,
+                    double* cost, int* ok, hastar_stats* stats, double* wall_ms) {
+  auto* P = static_cast<OP64*>(h);
+  std::vector<orc::P3<double>> path;
+  std::vector<double> cv;
+  auto t0 = std::chrono::steady_clock::now();
+  auto r = P->find_path(vel, {start[0], start[1], start[2]}, path, cv);
+  auto t1 = std::chrono::steady_clock::now();
+  if (wall_ms) *wall_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  *cost = r.first;
+  *ok = r.second ? 1 : 0;
+  if (stats) *stats = P->st;
+  *len = (int)path.size();
+  if ((int)path.size() > cap) return HASTAR_ENOSPC;
+  for (size_t k = 0; k < path.size(); ++k) {
+    xyh[3 * k] = path[k].x;
+    xyh[3 * k + 1] = path[k].y;
+    xyh[3 * k + 2] = path[k].h;
+    curv[k] = cv[k];
+  }
+  return 0;
+}
+int orc64_closed_keys(void* h, int* out, int cap) {
+  auto* P = static_cast<OP64*>(h);
+  std::vector<long long> k;
+  for (const auto& n : P->cl3) k.push_back(((long long)n.cx << 40) | ((long long)n.cy << 16) | n.bin);
+  std::sort(k.begin(), k.end());
+  int n = (int)k.size();
+  for (int i = 0; i < n && i < cap; ++i) {
+    out[3 * i] = (int)(k[i] >> 40);
+    out[3 * i + 1] = (int)((k[i] >> 16) & 0xffffff);
+    out[3 * i + 2] = (int)(k[i] & 0xffff);
+  }
+  return n;
+}
+
+// VelocityGenerator<double>::generate_velocity_profile (VelocityGenerator.cpp:19-84), T = double
+int orc64_velocity_profile(const double prm[5], double vel_init, double max_velocity_curr, const double* xyh,
+                           const double* curv, int n, int coast_to_goal, int stop_at_goal, double* out) {
+  using T = double;
+  const T vmax_param = prm[0], vcoast = prm[1], a_lat = prm[2], a_lat2 = prm[2] * prm[2], a_acc = prm[3],
+          a_dec = prm[4];
+  struct P3 { T _x, _y, _h; };
+  std::vector<P3> path((size_t)n);
+  for (int i = 0; i < n; ++i) path[i] = {xyh[3 * i], xyh[3 * i + 1], xyh[3 * i + 2]};
+  std::vector<T> curvature(curv, curv + n);
+  T max_velocity = coast_to_goal ? vcoast : vmax_param;
+  max_velocity = std::min(max_velocity, max_velocity_curr);
+  const T max_velocity_sqr = max_velocity * max_velocity;
+  const std::size_t path_size = path.size();
+  std::vector<T> velocity(path_size), velocity_sqr(path_size);
+  velocity_sqr[0] = vel_init * vel_init;
+  T max_velocity_sqr_curr = velocity_sqr[0];
+  for (std::size_t i = 0; i + 1 < path_size; i++) {
+    const std::size_t pi = path_size - i - 1;
+    T step = std::hypot(path[pi - 1]._x - path[pi]._x, path[pi - 1]._y - path[pi]._y);
+    T lat = velocity_sqr[i] * curvature[pi];
+    T rem = a_dec * std::sqrt(1.0 - (lat * lat) / a_lat2);
+    max_velocity_sqr_curr = std::max(max_velocity_sqr_curr - 2 * rem * step, max_velocity_sqr);
+    velocity_sqr[i + 1] = (curvature[pi - 1] != 0) ? std::min(a_lat / curvature[pi - 1], max_velocity_sqr_curr)
+                                                   : max_velocity_sqr_curr;
+  }
+  velocity_sqr[path_size - 1] = stop_at_goal ? 0 : velocity_sqr[path_size - 1];
+  for (std::size_t i = 0; i + 1 < path_size; i++) {
+    const std::size_t pi = path_size - i - 1;
+    T step = std::hypot(path[pi - 1]._x - path[pi]._x, path[pi - 1]._y - path[pi]._y);
+    T lat = velocity_sqr[i] * curvature[pi];
+    T rem = a_acc * std::sqrt(1.0 - (lat * lat) / a_lat2);
+    velocity_sqr[i + 1] = std::min(velocity_sqr[i] + 2 * rem * step, velocity_sqr[i + 1]);
+  }
+  for (std::size_t i = path_size - 1; i > 0; i--) {
+    const std::size_t pi = path_size - i - 1;
+    T step = std::hypot(path[pi + 1]._x - path[pi]._x, path[pi + 1]._y - path[pi]._y);
+    T lat = velocity_sqr[i] * curvature[pi];
+    T rem = a_dec * std::sqrt(1.0 - (lat * lat) / a_lat2);
+    velocity_sqr[i - 1] = std::min(velocity_sqr[i] + 2 * rem * step, velocity_sqr[i - 1]);
+    velocity[i - 1] = std::sqrt(velocity_sqr[i - 1]);
+  }
+  velocity[path_size - 1] = std::sqrt(velocity_sqr[path_size - 1]);
+  for (int i = 0; i < n; ++i) out[i] = velocity[i];
+  constexpr T tol = static_cast<T>(0.25);
+  return vel_init < (velocity[0] + tol) ? 1 : 0;
+}
+
+}  // extern "C"

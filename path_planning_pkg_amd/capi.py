@@ -40,6 +40,14 @@ class HastarParams(C.Structure):
     ]
 
 
+class HastarParamsF64(C.Structure):
+    """hastar_params_f64 (include/hastar_f64.h) == HybridAStar<double> ctor args."""
+
+    _fields_ = [(name, C.c_double if t is C.c_float else (C.POINTER(C.c_double) if name in ("steering", "curvature_weights")
+                                                           else t))
+                for name, t in HastarParams._fields_]
+
+
 class HastarStats(C.Structure):
     _fields_ = [
         ("pops", C.c_longlong),
@@ -92,6 +100,9 @@ class PlannerConfig:
             raise ValueError("curvature_weights must have one entry per steering angle")
         self.steering = np.ascontiguousarray(steering, dtype=np.float32)
         self.curvature_weights = np.ascontiguousarray(curvature_weights, dtype=np.float32)
+        # the same arguments as doubles, unrounded (HybridAStar<double>, include/hastar_f64.h)
+        self.steering64 = np.ascontiguousarray(steering, dtype=np.float64)
+        self.curvature_weights64 = np.ascontiguousarray(curvature_weights, dtype=np.float64)
         self.values = dict(
             dubins_shot_interval=int(dubins_shot_interval),
             dubins_shot_interval_decay=int(dubins_shot_interval_decay),
@@ -117,13 +128,31 @@ class PlannerConfig:
         return p
 
 
+    def struct_f64(self):
+        """hastar_params_f64 of the same arguments (the Python floats as doubles)."""
+        p = HastarParamsF64(**{k: v for k, v in self.values.items()})
+        p.num_steering = len(self.steering64)
+        p.steering = self.steering64.ctypes.data_as(C.POINTER(C.c_double))
+        p.curvature_weights = self.curvature_weights64.ctypes.data_as(C.POINTER(C.c_double))
+        return p
+
+
 def steering_from_degrees(deg):
     """`angle = angle * M_PI/180.0f` on a float (test_hybrid_astar.cpp:36-39)."""
     return [float(np.float32(float(np.float32(d)) * math.pi / 180.0)) for d in deg]
 
 
+def steering_from_degrees_f64(deg):
+    """`angle * deg_to_rad` with T = double (local_planner.cpp:143-146)."""
+    return [float(d) * (math.pi / 180.0) for d in deg]
+
+
 def fptr(a):
     return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def dptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
 
 
 def iptr(a):

@@ -53,6 +53,14 @@ int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+}  // namespace
+
+// the other host modules (hastar_f64.cpp) report through the same hastar_last_error()
+namespace hastar {
+int set_last_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace hastar
+
+namespace {
 
 #define HIPCHK(expr)                                                                          \
   do {                                                                                        \
@@ -268,8 +276,17 @@ int device_ctx(int dev, DeviceCtx** out) {
           hipStreamCreateWithFlags(&D.bulk_st, hipStreamNonBlocking) == hipSuccess &&
           hipEventCreateWithFlags(&D.ev_fork, hipEventDisableTiming) == hipSuccess &&
           hipEventCreate(&D.ev_head) == hipSuccess && hipEventCreate(&D.ev_bulk) == hipSuccess &&
-          hipEventCreate(&D.ev_hs) == hipSuccess && hipEventCreate(&D.ev_bs) == hipSuccess)
+          hipEventCreate(&D.ev_hs) == hipSuccess && hipEventCreate(&D.ev_bs) == hipSuccess) {
         D.head_cus = hc;
+      } else {
+        // a partial set is released and the split launch stays off (visible as head_cus = 0 in
+        // hastar_debug_slots); said once, since results are unaffected
+        for (hipStream_t* s : {&D.head_st, &D.bulk_st})
+          if (*s) hipStreamDestroy(*s), *s = nullptr;
+        for (hipEvent_t* e : {&D.ev_fork, &D.ev_head, &D.ev_bulk, &D.ev_hs, &D.ev_bs})
+          if (*e) hipEventDestroy(*e), *e = nullptr;
+        std::fprintf(stderr, "hastar: split launch disabled (stream/event creation failed)\n");
+      }
     }
     HIPCHK(dalloc(&D.d_next, 4));  // [0] work counter, [1] head placement, [2] head done
     D.init = true;
@@ -913,14 +930,15 @@ int hastar_reset(hastar_handle h) {
   return HASTAR_OK;
 }
 
-// reset() of n planners: one kernel clears every bitmap of a device (planners grouped by
-// device and grid size)
+// the caller's longest-first key of the planner's next batched search (include/hastar.h)
 int hastar_set_cost_hint(hastar_handle h, long long hint) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");
   h->last_pops = hint;
   return HASTAR_OK;
 }
 
+// reset() of n planners: one kernel clears every bitmap of a device (planners grouped by
+// device and grid size)
 int hastar_reset_batch(const hastar_handle* hs, int n) {
   if (!hs || n < 0) return fail(HASTAR_EINVAL, "bad argument");
   for (int i = 0; i < n; ++i)
@@ -1017,9 +1035,22 @@ static void boxes_prep(hastar_handle h, const float* boxes, const float* conf, i
 // update_obstacles(boxes) of n planners of one device (planner i's counts[i] boxes follow
 // planner i-1's in `boxes` / `conf`): one staged upload, one copy launch for the APF lists,
 // and one raster launch per layer index over every planner's boxes of that layer.
+static int update_boxes_run(const hastar_handle* hs, int n, const float* boxes, const float* conf, const int* counts,
+                            float apf_added_radius, const std::vector<long long>& first);
 static int update_boxes_impl(const hastar_handle* hs, int n, const float* boxes, const float* conf, const int* counts,
                              float apf_added_radius) {
   if (n <= 0) return HASTAR_OK;
+  std::vector<long long> first(n + 1, 0);
+  for (int i = 0; i < n; ++i) first[i + 1] = first[i] + (counts[i] > 0 ? counts[i] : 0);
+  const int rc = update_boxes_run(hs, n, boxes, conf, counts, apf_added_radius, first);
+  // the cold-order key's input (route_score): the boxes of the last update that went through.
+  // Line obstacles do not enter the key (it only orders a batch's searches, never their results).
+  if (rc == HASTAR_OK)
+    for (int i = 0; i < n; ++i) hs[i]->boxes_w.assign(boxes + 4 * first[i], boxes + 4 * first[i + 1]);
+  return rc;
+}
+static int update_boxes_run(const hastar_handle* hs, int n, const float* boxes, const float* conf, const int* counts,
+                            float apf_added_radius, const std::vector<long long>& first) {
   const int dev = hs[0]->device;
   for (int i = 0; i < n; ++i) {
     if (!hs[i] || hs[i]->device != dev) return fail(HASTAR_EINVAL, "null handle or handles on different devices");
@@ -1028,9 +1059,6 @@ static int update_boxes_impl(const hastar_handle* hs, int n, const float* boxes,
   HIPCHK(hipSetDevice(dev));
   DeviceCtx& DC = *hs[0]->dc;
   std::vector<BoxPrep> prep(n);
-  std::vector<long long> first(n + 1, 0);
-  for (int i = 0; i < n; ++i) first[i + 1] = first[i] + counts[i];
-  for (int i = 0; i < n; ++i) hs[i]->boxes_w.assign(boxes + 4 * first[i], boxes + 4 * first[i + 1]);
   // host preparation of every planner (rotations, raster origins, layers: O(boxes^2) each),
   // spread over host threads for large batches
   {
@@ -1659,8 +1687,9 @@ static int batch_acquire(DeviceCtx& DC, int n) {
   return 0;
 }
 
-// Hand a finished batch back: per-planner outcome (stats[i].status), then the paths that fit
-// the caller's buffers packed by one gather kernel and one copy.  lpt: record each search's
+// Hand a finished batch back: per-planner outcome (stats[i].status), then every path packed on
+// the device by one gather kernel (kept there for hastar_velocity_profile_last_batch) and one
+// copy to the caller's buffers of the paths that fit its cap.  lpt: record each search's
 // duration as the planner's longest-first key (exact mode only).
 static bool lpt_work_key() {
   static const bool on = [] {
@@ -2714,7 +2743,7 @@ int hastar_debug_relaxed_pool(hastar_handle h, long long* out2) {
 }
 
 int hastar_debug_split(hastar_handle h, float* out4) {
-  if (!h || !out4) return fail(HASTAR_EINVAL, "bad argument");
+  if (!h || !h->dc || !out4) return fail(HASTAR_EINVAL, "bad argument");
   for (int i = 0; i < 4; ++i) out4[i] = h->dc->split_ms[i];
   return 0;
 }

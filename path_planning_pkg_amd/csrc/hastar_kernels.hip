@@ -755,8 +755,12 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
   // an open (not closed) cell's record holds its hinted node's g and prev link, written with
   // the hint; cgen = any value but this search's generation
   const uint32_t open_cgen = c.gen2 - 1u;
+  // migrate before a pop that could take the pool past the LDS capacity or the arena's HBM
+  // tree (the migration copies every index in use into A.open2, and max_astar_nodes bounds the
+  // inner search in both modes and on both kernels alike)
+  const int lim = CF::CAP < c.A->open2_cap ? CF::CAP : c.A->open2_cap;
   while (rg.n > 0) {
-    if (c.ps2.next + 8 > CF::CAP) return false;
+    if (c.ps2.next + 8 > lim) return false;
     STAMP_T t_pop = STAMP_NOW();
     const int b = tr.begin();
     const Quad top = tr.quad(b);

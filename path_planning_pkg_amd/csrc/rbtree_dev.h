@@ -12,7 +12,8 @@
 //   _Rb_tree_insert_and_rebalance, _Rb_tree_rebalance_for_erase, _Rb_tree_decrement.
 // They are restated below on pool indices: node 0 is the header (p = root,
 // l = leftmost, r = rightmost, color red), NIL (-1) is the null link.
-// Tested against std::set on random operation streams: tests/test_rbtree_host.py.
+// Tested against std::set on random operation streams: tools/rbtree_check.cpp, run by
+// tests/test_capi_host.py.
 #pragma once
 #include <type_traits>
 #include "hastar_layout.h"
@@ -43,14 +44,28 @@ inline uint32_t rb_uu(uint32_t v) { return v; }
 inline float rb_uf(float v) { return v; }
 #endif
 
-// comparator of the reference: (ka != kb) && (fa < fb)
-RB_HD bool rb_less(uint32_t ka, float fa, uint32_t kb, float fb) { return (ka != kb) && (fa < fb); }
+// comparator of the reference: (ka != kb) && (fa < fb); FT = the planner's T (float, or
+// double for HybridAStar<double>, hastar_f64.hip)
+template <class FT>
+RB_HD bool rb_less(uint32_t ka, FT fa, uint32_t kb, FT fb) { return (ka != kb) && (fa < fb); }
 
-// {key, f, l, r} of one node in one 16-byte load (the first 16 bytes of every node type)
-struct Quad {
+// {key, f, l, r} of one node (for float: one 16-byte load, the first 16 bytes of every node type)
+template <class FT>
+struct QuadT {
   uint32_t key;
-  float f;
+  FT f;
   int l, r;
+};
+using Quad = QuadT<float>;
+
+// the f type of a tree layout: Acc::FT when the accessor declares one, else float
+template <class A, class = void>
+struct rb_acc_ft {
+  using type = float;
+};
+template <class A>
+struct rb_acc_ft<A, std::void_t<typename A::FT>> {
+  using type = typename A::FT;
 };
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef int rb_v4i __attribute__((ext_vector_type(4)));
@@ -112,6 +127,8 @@ struct RBT : Acc {
   using Acc::sC;
   using Acc::K;
   using Acc::F;
+  using FT = typename rb_acc_ft<Acc>::type;
+  using Q = QuadT<FT>;
 
   RB_HD int root() { return P(0); }
   RB_HD int begin() { return L(0); }  // == 0 (header) when empty
@@ -169,20 +186,20 @@ struct RBT : Acc {
 
   // std::set::find (stl_tree.h _M_lower_bound + key_compare check).  Returns 0 (= end)
   // when not "found".
-  RB_HD int find(uint32_t k, float f) {
+  RB_HD int find(uint32_t k, FT f) {
     int y = 0, x = P(0), depth = 0;
     uint32_t yk = 0;
-    float yf = 0.0f;
+    FT yf = 0;
     if constexpr (Acc::kPathWalk) {
       bool unused;
       int rj;
       uint32_t rk;
-      float rf;
+      FT rf;
       this->path_walk(k, f, false, &y, &yk, &yf, &unused, &rj, &rk, &rf);
       x = NIL;
     }
     while (x != NIL) {
-      const Quad q = this->quad_at(x, depth++);
+      const Q q = this->quad_at(x, depth++);
       if (!rb_less(q.key, q.f, k, f)) {
         y = x;
         yk = q.key;
@@ -198,11 +215,11 @@ struct RBT : Acc {
 
   // _M_get_insert_unique_pos: returns the parent for the new node (>= 0) or -2 when an
   // "equivalent" element exists (insert dropped).  *left = insert_left of _M_insert_.
-  RB_HD int insert_pos(uint32_t k, float f, bool* left) {
+  RB_HD int insert_pos(uint32_t k, FT f, bool* left) {
     int x = P(0), y = 0, depth = 0;
     bool comp = true;
     uint32_t yk = 0;
-    float yf = 0.0f;
+    FT yf = 0;
     if constexpr (Acc::kPathWalk) {
       // The walk also reports the deepest node where it turned right (rj; -1 if none).
       // That node is decrement(y) when the walk ended by going left, and y is the
@@ -210,7 +227,7 @@ struct RBT : Acc {
       // further tree access.
       int rj;
       uint32_t rk;
-      float rf;
+      FT rf;
       this->path_walk(k, f, true, &y, &yk, &yf, &comp, &rj, &rk, &rf);
       if (comp) {
         if (rj < 0) {
@@ -230,7 +247,7 @@ struct RBT : Acc {
       return -2;
     }
     while (x != NIL) {
-      const Quad q = this->quad_at(x, depth++);
+      const Q q = this->quad_at(x, depth++);
       y = x;
       yk = q.key;
       yf = q.f;

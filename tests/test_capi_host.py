@@ -1,5 +1,5 @@
 """CPU-side checks of the drop-in boundary: the C-ABI library loads, exports every
-symbol include/hastar.h, include/hastar_units.h and include/hastar_test.h declare, and refuses to run without a
+symbol include/hastar.h, hastar_f64.h, hastar_units.h and hastar_test.h declare, and refuses to run without a
 GPU (no CPU fallback).  Also the libstdc++ red-black-tree replica used by the search
 kernel vs std::set (tools/rbtree_check.cpp)."""
 import ctypes as C
@@ -14,10 +14,10 @@ ROOT = Path(__file__).resolve().parents[1]
 
 def declared_symbols():
     names = []
-    for hdr in ("hastar.h", "hastar_test.h", "hastar_units.h"):
+    for hdr in ("hastar.h", "hastar_f64.h", "hastar_test.h", "hastar_units.h"):
         text = (ROOT / "include" / hdr).read_text()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-        names += re.findall(r"\b(hastar_[a-z0-9_]+)\s*\(", text)
+        names += re.findall(r"\b(hastar(?:64)?_[a-z0-9_]+)\s*\(", text)
     return sorted(set(names))
 
 
@@ -26,7 +26,7 @@ def test_library_exports_declared_symbols():
     assert LIB_PATH.exists(), "build first (__graft_entry__.build())"
     lib = C.CDLL(str(LIB_PATH))
     syms = declared_symbols()
-    assert "hastar_create_f32" in syms and "hastar_find_path_batch" in syms
+    assert "hastar_create_f32" in syms and "hastar_find_path_batch" in syms and "hastar64_find_path" in syms
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
 
@@ -40,6 +40,10 @@ def test_no_cpu_fallback_without_gpu():
     cfg, _, _ = harness()
     with pytest.raises(HastarError) as e:
         HybridAStar(cfg)
+    assert e.value.rc == -5
+    from path_planning_pkg_amd.planner64 import HybridAStar64
+    with pytest.raises(HastarError) as e:
+        HybridAStar64(cfg)
     assert e.value.rc == -5
 
 

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from tests.parity_util import assert_bits_equal, bits  # noqa: F401 (re-exported)
-from tests.scenarios import drive, harness, synthetic
+from tests.scenarios import drive, harness, synthetic, synthetic_ref
 
 pytestmark = pytest.mark.gpu
 
@@ -268,6 +268,31 @@ def test_batch_with_fewer_slots(gpu, oracle_lib, monkeypatch, wide):
     res, _ = gpu.find_path_batch(gs, [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases])
     for i, ((cfg, proto), o) in enumerate(zip(cases, os_)):
         compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"3-slot batch {i}")
+
+
+@pytest.mark.parametrize("wide", ["1", "0"], ids=["latency_kernel", "batch_kernel"])
+def test_small_inner_arena_bounds_both_kernels_alike(gpu, oracle_lib, monkeypatch, wide):
+    """max_astar_nodes below the LDS pool (1024 / 2048 nodes): the LDS tree migrates before the
+    pool could outgrow the arena's HBM tree, so a search either ends like the oracle's or, when
+    an inner search needs more nodes than the arena holds, with HASTAR_EOVERFLOW on both kernels
+    alike (the latency kernel copied up to 2048 nodes into a 601-node open2)."""
+    monkeypatch.setenv("HASTAR_WIDE", wide)
+    from path_planning_pkg_amd.capi import PlannerConfig
+    outs = []
+    for cap in (600, 1500):
+        cfg, proto = synthetic_ref(1024, 72, 200, 1)
+        cfg = PlannerConfig(**{**cfg.values, "max_astar_nodes": cap}, steering=cfg.steering)
+        g, o = both(cfg, gpu, oracle_lib)
+        drive(g, proto)
+        drive(o, proto)
+        r = g.find_path(proto["vel"], proto["start"])
+        outs.append(r["stats"]["status"])
+        if r["stats"]["status"] == 0:
+            compare_results(r, o.find_path(proto["vel"], proto["start"]), f"max_astar_nodes={cap}")
+        else:
+            assert r["stats"]["status"] == -75 and not r["ok"]
+    # seed 1's inner searches need more than 600 nodes but not more than 1500 (tools/astar_shape_stats.py)
+    assert outs == [-75, 0], outs
 
 
 def test_reserve_then_batch(gpu, oracle_lib):
