@@ -21,6 +21,7 @@ roofline (SURVEY.md §8d algorithmic bytes / kernel time from HIP events on its 
 the CPU oracle timed on `cores` host threads, one private planner per thread (rank 0).
 """
 import argparse
+import hashlib
 import json
 import os
 import socket
@@ -79,10 +80,17 @@ def step_diag(planners, res):
     first = head[np.argsort(t[head, 0])][:16]
     li = int(np.argmax(dur))
     st = res.stats
+    # where each search ran: (XCC, SE, SH, CU) of its wavefront; a CU pair (CU, CU ^ 1) shares
+    # an instruction cache, so the partner CU's searches (other kernel or not) are counted
+    hw = [p.hw_id() for p in planners]
+    cu_key = [(x, se, sh, cu) for x, cu, se, sh, _ in hw]
+    from collections import Counter
+    on_cu = Counter(cu_key)
 
-    def row(i):  # start offset ms, duration ms, arena, planner index, pops, inner A* pops
+    def row(i):  # start offset ms, duration ms, arena, planner index, pops, inner A* pops, XCC, SE, SH, CU,
+        x, se, sh, cu = cu_key[i]  # searches on the instruction-cache partner CU in this step
         return [round(float((t[i, 0] - t0) * 1e-5), 1), round(float(dur[i]), 1), int(t[i, 2]), int(i),
-                int(st["pops"][i]), int(st["astar_pops"][i])]
+                int(st["pops"][i]), int(st["astar_pops"][i]), x, se, sh, cu, on_cu[(x, se, sh, cu ^ 1)]]
     return {"kernel_ms": float(res.kernel_ms), "span_ms": float((t[:, 1].max() - t0) * 1e-5),
             "split_ms": planners[0].split_ms(), "head": [row(i) for i in first], "longest": row(li)}
 
@@ -681,6 +689,9 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
     relaxed_opts = dict(delta=args.relaxed_delta, h_weight=args.relaxed_weight, reuse_heuristic=1)
     rx = {"kernel_ms": [], "wall_ms": [], "upkeep_ms": [], "ok": 0, "ratios": []}
     slowest = []
+    # every (pair, tick) outcome of the exact loop, warm-up ticks included, for the parity
+    # readout against the oracle's replay of the same loop (cpu_baseline_cfg5)
+    gpu_ticks = [[] for _ in pairs]
 
     def step(timed):
         """One tick; returns (stats, kernel ms, successes, seconds of the exact tick).  When
@@ -692,6 +703,8 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
         br = gpu.find_path_batch_arrays(planners, vels, starts, buffers=bufs)
         st = br.stats.copy()
         t_exact = time.perf_counter() - t0
+        for i in range(len(planners)):
+            gpu_ticks[i].append(tick_key(br.result(i)))
         if timed:  # the tick's slowest search (it bounds the tick): its pops and inner A* pops
             tm = np.array([p.timing() for p in planners], dtype=np.float64)
             j = int(np.argmax(tm[:, 1] - tm[:, 0]))
@@ -764,7 +777,8 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
                 "note": "non-parity mode (hastar_find_path_relaxed_batch) on the same ticks' maps and starts as the "
                         "exact loop (rank 0); tick_ms = its find_path wall + the same batched upkeep"}
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_cfg5(pairs, args.cpu_seconds, args.warmup + args.steps)
+            out["cpu_baseline"], replay = cpu_baseline_cfg5(pairs, args.cpu_seconds, args.warmup + args.steps)
+            out["parity_sample"] = cfg5_parity(gpu_ticks, replay, ids)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
@@ -772,13 +786,42 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
         print(json.dumps(out))
 
 
+def tick_key(r):
+    """What parity compares for one (pair, tick) search: success, cost bits, pops, pop and closed
+    digests, and a hash of the path and curvature bits."""
+    h = hashlib.blake2b(np.ascontiguousarray(r["path"], np.float32).tobytes(), digest_size=8)
+    h.update(np.ascontiguousarray(r["curvature"], np.float32).tobytes())
+    st = r["stats"]
+    return (bool(r["ok"]), np.float32(r["cost"]).tobytes().hex(), int(st["pops"]), int(st["pop_digest"]),
+            int(st["closed_digest"]), h.hexdigest())
+
+
+def cfg5_parity(gpu_ticks, replay, ids):
+    """Every (pair, tick) of the GPU loop against the oracle's replay of the same loop (the
+    pairs cpu_baseline_cfg5 replayed: all of them unless its budget ran out first)."""
+    bad, checked, pops = [], 0, 0
+    for i, ticks in replay.items():
+        for t, (g, o) in enumerate(zip(gpu_ticks[i], ticks)):
+            checked += 1
+            pops += o[2]
+            if g != o:
+                bad.append([int(ids[i]), t])
+    return {"pairs": len(replay), "ticks_per_pair": len(gpu_ticks[0]) if gpu_ticks else 0, "searches": checked,
+            "bit_exact": not bad and checked == sum(len(t) for t in gpu_ticks), "mismatched_pair_ticks": bad[:16],
+            "pops_checked": int(pops),
+            "note": "every pair x every tick (warm-up included) of the exact replan loop, without reset, against the "
+                    "oracle's replay of the same call sequence: success, cost bits, pops, pop/closed digests, "
+                    "path+curvature bits (hash)"}
+
+
 def cpu_baseline_cfg5(pairs, budget_s, ticks):
     """The oracle replaying the same pairs' replan loops on `cpu_threads()` host threads, one
     private planner per thread (find_path timed only; ctypes calls release the GIL).  Pairs are
-    taken in order, one thread per pair, in rounds of T pairs until the rounds' parallel wall time
-    reaches the budget.  value = pops / parallel find_path wall.  A tick's pairs are independent,
-    so with a core per pair the CPU's tick takes as long as its slowest pair
-    (tick_ms_one_core_per_pair)."""
+    taken in order, one thread per pair, in rounds of T pairs until every pair is replayed (the
+    parity readout needs them all) or the rounds' parallel wall time reaches 4x the budget.
+    value = pops / parallel find_path wall.  A tick's pairs are independent, so with a core per
+    pair the CPU's tick takes as long as its slowest pair (tick_ms_one_core_per_pair).  Also
+    returns {pair index: [tick_key per tick]} of the replayed pairs."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle.pyoracle import OraclePlanner
     from tests.scenarios import drive, replan_tick, replan_tick_inputs
@@ -788,30 +831,33 @@ def cpu_baseline_cfg5(pairs, budget_s, ticks):
         cfg, proto, v = pv
         o = OraclePlanner(cfg)
         drive(o, proto)
-        ms, pops = [], 0
+        ms, pops, keys = [], 0, []
         for t in range(ticks):
             r = o.find_path(proto["vel"], replan_tick_inputs(proto, v, t)[0])
             pops += r["stats"]["pops"]
             ms.append(r["wall_ms"])
+            keys.append(tick_key(r))
             replan_tick(o, proto, v, t)
         o.close()
-        return pops, ms
+        return pops, ms, keys
 
     pops, wall, n = 0, 0.0, 0
     tick_max = np.zeros(ticks)
+    replay = {}
     with ThreadPoolExecutor(T) as ex:
-        while n < len(pairs) and wall < budget_s:
+        while n < len(pairs) and wall < 4 * budget_s:
             rnd = list(ex.map(run_pair, pairs[n:n + T]))
             # the round's find_path time on T cores: its slowest pair's summed find_path time
-            wall += max(sum(ms) for _, ms in rnd) * 1e-3
-            for p, ms in rnd:
+            wall += max(sum(ms) for _, ms, _ in rnd) * 1e-3
+            for j, (p, ms, keys) in enumerate(rnd):
                 pops += p
                 tick_max = np.maximum(tick_max, ms)
+                replay[n + j] = keys
             n += len(rnd)
-    return {"value": pops / wall if wall > 0 else None, "unit": "expansions/s", "cores": T, "kind": "port",
-            "sample": f"first {n} pairs of rank 0 x {ticks} ticks (same call sequence as the GPU run), find_path only, "
-                      f"{T} threads with one private planner each (oracle/hastar_oracle.cpp, -O3)",
-            "tick_ms_one_core_per_pair": float(tick_max.mean()) if n else None}
+    return ({"value": pops / wall if wall > 0 else None, "unit": "expansions/s", "cores": T, "kind": "port",
+             "sample": f"first {n} pairs of rank 0 x {ticks} ticks (same call sequence as the GPU run), find_path "
+                       f"only, {T} threads with one private planner each (oracle/hastar_oracle.cpp, -O3)",
+             "tick_ms_one_core_per_pair": float(tick_max.mean()) if n else None}, replay)
 
 
 def parity_sample(cfgs, gpu, qids):

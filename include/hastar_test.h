@@ -34,6 +34,9 @@ int hastar_debug_astar_modes(hastar_handle h, long long* out2);
 /* Timing of the last search: {t_start, t_end} in s_memrealtime ticks (100 MHz, chip-wide
  * clock) and the slot (persistent wavefront) that ran it. */
 int hastar_debug_timing(hastar_handle h, unsigned long long* out3);
+/* Where the last search ran: XCC_ID << 16 | HW_ID[15:0] (wave, SIMD, pipe, CU, SH, SE fields) of
+ * its wavefront at the end of the search. */
+int hastar_debug_hw_id(hastar_handle h, int* out);
 /* Search-slot pool of the handle's device: {resident wavefronts, search waves per CU, arenas, MiB per arena,
    latency CUs of a split launch (0: none)}. */
 int hastar_debug_slots(hastar_handle h, long long* out5);

@@ -667,6 +667,7 @@ static hastar_handle new_planner(const hastar_params* p, int device, DeviceCtx* 
   const int astar_cap =
       p->max_astar_nodes > 0 ? p->max_astar_nodes : (int)std::min<size_t>(NN + 16, (size_t)65536);
   R.open2 = astar_cap + 1;
+  D.astar_cap = astar_cap + 1;  // the planner's own bound: an arena of the pool may hold more
   R.cells = NN;
   int dub_cap = p->max_dubins_samples;
   if (dub_cap <= 0) {
@@ -2724,6 +2725,12 @@ int hastar_debug_timing(hastar_handle h, unsigned long long* out3) {
   out3[0] = h->last.t_start;
   out3[1] = h->last.t_end;
   out3[2] = (unsigned long long)h->last.slot;
+  return HASTAR_OK;
+}
+
+int hastar_debug_hw_id(hastar_handle h, int* out) {
+  if (!h || !out || !h->have_last) return fail(HASTAR_EINVAL, "no search result");
+  *out = h->last.hw_id;
   return HASTAR_OK;
 }
 

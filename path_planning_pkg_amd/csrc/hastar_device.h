@@ -420,9 +420,8 @@ __device__ __forceinline__ float apf_field(const PlannerDev& P, const ApfStage& 
 // half-width r + apf_reach around it misses (cx, cy) cannot pass the exact pre-test of any
 // successor: the obstacle list is culled once, then lanes run over (candidate, kept
 // obstacle) pairs, and every successor's in-radius terms are summed in obstacle order.
-__device__ __forceinline__ float apf_fused(const PlannerDev& P, ApfStage& S, float cx, float cy, float sx,
-                                           float sy, float sh, uint64_t cmask, int gs, int lane) {
-  ApfCand* __restrict__ kept = S.kept;
+__device__ __forceinline__ float apf_fused_k(const PlannerDev& P, const ApfStage& S, ApfCand* __restrict__ kept, float cx,
+                                             float cy, float sx, float sy, float sh, uint64_t cmask, int gs, int lane) {
   float fc = 0.0f;
   if (cmask == 0) return fc;
   int C = APF_MAXC + 1;
@@ -486,6 +485,11 @@ __device__ __forceinline__ float apf_fused(const PlannerDev& P, ApfStage& S, flo
   }
   wave_lds_sync();
   return fc;
+}
+// the same with the stage's own cull buffer (a helper wave of the latency kernel brings its own)
+__device__ __forceinline__ float apf_fused(const PlannerDev& P, ApfStage& S, float cx, float cy, float sx, float sy,
+                                           float sh, uint64_t cmask, int gs, int lane) {
+  return apf_fused_k(P, S, S.kept, cx, cy, sx, sy, sh, cmask, gs, lane);
 }
 
 // Dubins.cpp:326-563 sampling of the chosen word, wave-parallel (64 samples per step).

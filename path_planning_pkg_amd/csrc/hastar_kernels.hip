@@ -95,6 +95,7 @@ struct SearchCtx {
   long long pops, succ, apops, asearch, shots, amigr, apops_g;
   int status;
   bool cost_only;   // AStar::a_star_search(get_cost_only): memo exits + memoise (always, inside the search)
+  uint32_t prep_epoch;  // latency kernel: the search's epoch in the helper waves' prep table
 #ifdef HASTAR_STAMPS
   unsigned long long cyc[NSTAMP];
 #endif
@@ -564,7 +565,7 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
   const int nact = P.diag ? 8 : 4;
   GAS Cell2* cells = c.cell2;
   static_assert(G, "the LDS mode is astar_loop_lds");
-  const int cap = A.open2_cap;
+  const int cap = A.open2_cap < P.astar_cap ? A.open2_cap : P.astar_cap;  // the planner's max_astar_nodes
   while (!tr.empty()) {
     STAMP_T t_pop = STAMP_NOW();
     const int b = tr.begin();
@@ -758,7 +759,8 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
   // migrate before a pop that could take the pool past the LDS capacity or the arena's HBM
   // tree (the migration copies every index in use into A.open2, and max_astar_nodes bounds the
   // inner search in both modes and on both kernels alike)
-  const int lim = CF::CAP < c.A->open2_cap ? CF::CAP : c.A->open2_cap;
+  const int acap = c.A->open2_cap < P.astar_cap ? c.A->open2_cap : P.astar_cap;
+  const int lim = CF::CAP < acap ? CF::CAP : acap;
   while (rg.n > 0) {
     if (c.ps2.next + 8 > lim) return false;
     STAMP_T t_pop = STAMP_NOW();
@@ -1093,7 +1095,7 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, OT& o3, const Succ& s, flo
 // of the batch's longest at 9,414; when the pool cannot take one more pop the tree moves to
 // the HBM records (same indices: only links and colours are copied) and the search continues
 // behind the register cache (RBT<CachedAcc3>).
-constexpr int OUTER_LDS_CAP = 5504;
+constexpr int OUTER_LDS_CAP = 5056;  // (5504 before round 4: the helper waves' prep table took the rest)
 struct alignas(16) Q3L {
   uint32_t key;
   float f;
@@ -1212,6 +1214,206 @@ __device__ __forceinline__ bool lds_outer_load(SearchCtx& c, OuterLds& ol, int l
   return true;
 }
 
+
+// ---- expansion prep: helper waves of the latency kernel ------------------------------------
+// The latency kernel runs one search per CU with one wavefront, so three SIMDs of its CU idle.
+// Its workgroup has three more waves that PRE-compute expansions: a node's successors
+// (VehicleModel.cpp:63-105: poses, speed limits, bins, cells, the occupancy filter of
+// Grid3D.cpp:54-59), their APF fields (Grid3D.cpp:206-227) and Dubins lengths (Dubins.cpp:19-69)
+// are pure functions of the node's pose, speed, curvature index and the search's map, not of the
+// search state.  The main wave posts every successor it may insert; a helper computes that
+// successor's own expansion while the main wave goes on (finds, inner A*, inserts); when the main
+// wave later pops a node whose inputs match a finished entry bit for bit, it takes the entry
+// instead of computing it.  Entries are tagged with the search's epoch and hold their inputs, so a
+// result can only be used for exactly the inputs it was computed from: results are identical
+// by construction (tests/test_gpu_*: every latency-kernel case).
+//
+// A ring of PREP_E entries in LDS (request seq s lives in entry s % PREP_E); state word per entry:
+// seq << 2 | phase, phase 0 = empty / being written by the main wave, 1 = posted, 2 = a helper
+// computes it, 3 = done.  The main wave overwrites only entries that no helper holds (a CAS to
+// phase 0); a helper claims a posted entry by CAS 1 -> 2 and alone moves it 2 -> 3.
+constexpr int PREP_E = 32;   // entries (the latest requests; cfg5 pops: 78 % of nodes were inserted within the last 32)
+constexpr int PREP_C = 4;    // candidates per entry: action windows of at most 4 (16-lane groups)
+constexpr int PREP_HELPERS = 3;
+struct alignas(16) PrepIn {  // the inputs of one expansion
+  uint32_t key;
+  float x, y, h, vmin;
+  int ci;
+  uint32_t epoch, pad;
+};
+struct alignas(16) PrepCand {  // one candidate successor of that expansion
+  float sx, sy, sh, vm, fc, dub, oact;
+  uint32_t skey;
+  uint32_t flags;  // bit 0: feasible (speed limit), bit 1: cell in the grid, bit 2: kept (bit 1 and occ < thr)
+  uint32_t pad0, pad1, pad2;
+};
+struct PrepShared {
+  PrepIn in[PREP_E];
+  PrepCand out[PREP_E][PREP_C];
+  uint32_t state[PREP_E];
+  uint32_t tail;                    // requests posted so far (main wave)
+  uint32_t epoch;                   // the current search (main wave)
+  uint32_t stop;                    // the kernel is done (main wave)
+  uint32_t pad;
+  int pidx;                         // the planner of `epoch` (its index in the kernel's descriptors)
+  int pad1;
+  ApfCand kept[PREP_HELPERS][APF_MAXC];  // the helpers' APF cull buffers
+};
+
+typedef LAS PrepShared PrepL;
+__device__ __forceinline__ uint32_t prep_ld(LAS uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void prep_st(LAS uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool prep_cas(LAS uint32_t* p, uint32_t expect, uint32_t v) {
+  return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// main wave: the entry holding the expansion of `cur` (a closed record: the popped node, or the
+// old record of its key), waiting for a helper still computing it; -1 if there is none
+__device__ __forceinline__ int prep_find(PrepL& pr, uint32_t key, float x, float y, float h, float vmin, int ci,
+                                         uint32_t epoch, int lane) {
+  const int e = lane & (PREP_E - 1);
+  const uint32_t st = prep_ld(&pr.state[e]);
+  PrepIn in;
+  __builtin_memcpy(&in, (const PrepIn*)&pr.in[e], sizeof(in));
+  const bool match = lane < PREP_E && (st & 3u) >= 2u && in.epoch == epoch && in.key == key &&
+                     __float_as_uint(in.x) == __float_as_uint(x) && __float_as_uint(in.y) == __float_as_uint(y) &&
+                     __float_as_uint(in.h) == __float_as_uint(h) && __float_as_uint(in.vmin) == __float_as_uint(vmin) &&
+                     in.ci == ci;
+  const uint64_t m = __ballot(match);
+  if (!m) return -1;
+  const int e0 = (int)__ffsll((unsigned long long)m) - 1;
+  uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)st, e0);
+  // a helper holds it: it finishes this one expansion (about the main wave's own cost of it)
+  while ((s0 & 3u) == 2u) {
+    __builtin_amdgcn_s_sleep(1);
+    s0 = ufu(prep_ld(&pr.state[e0]));
+  }
+  return (s0 & 3u) == 3u ? e0 : -1;
+}
+
+// main wave: post the kept successors of this expansion (candidate a of the window in lanes
+// [16 a, 16 a + 16), lead lane 16 a), newest last
+__device__ __forceinline__ void prep_post(PrepL& pr, bool post, uint32_t skey, float sx, float sy, float sh,
+                                          float vm, int ci, uint32_t epoch, int lane) {
+  const uint64_t m = __ballot(post);
+  if (!m) return;
+  const uint32_t tail = ufu(pr.tail);
+  if (post) {
+    const uint32_t k = (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    const uint32_t seq = tail + k + 1u;  // >= 1
+    const int e = (int)(seq & (PREP_E - 1));
+    const uint32_t old = prep_ld(&pr.state[e]);
+    if ((old & 3u) != 2u && prep_cas(&pr.state[e], old, seq << 2)) {
+      PrepIn in;
+      in.key = skey;
+      in.x = sx;
+      in.y = sy;
+      in.h = sh;
+      in.vmin = vm;
+      in.ci = ci;
+      in.epoch = epoch;
+      in.pad = 0;
+      __builtin_memcpy((PrepIn*)&pr.in[e], &in, sizeof(in));
+      prep_st(&pr.state[e], (seq << 2) | 1u);
+    }
+  }
+  if (lane == 0) pr.tail = tail + (uint32_t)__popcll(m);
+  wave_lds_sync();
+}
+
+// helper wave h (1..3): claim the newest posted expansion, compute it, publish it; returns when
+// the main wave has set `stop`
+__device__ void prep_helper(PrepL& pr, const ApfStage& apfs, const PlannerDev* __restrict__ descs, int h, int lane) {
+  ApfCand* kept_buf = (ApfCand*)pr.kept[h - 1];
+  for (;;) {
+    const int e = lane & (PREP_E - 1);
+    const uint32_t st = prep_ld(&pr.state[e]);
+    const bool posted = lane < PREP_E && (st & 3u) == 1u;
+    // the newest posted request (largest seq)
+    uint32_t best = posted ? (st >> 2) : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) best = max(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    best = ufu(best);
+    if (best == 0u) {
+      if (ufu(prep_ld(&pr.stop))) return;
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    const int be = (int)(best & (PREP_E - 1));
+    bool won = false;
+    if (lane == 0) won = prep_cas(&pr.state[be], (best << 2) | 1u, (best << 2) | 2u);
+    if (!__builtin_amdgcn_readfirstlane((int)won)) continue;
+    PrepIn in;
+    __builtin_memcpy(&in, (const PrepIn*)&pr.in[be], sizeof(in));
+    const PlannerDev* Pp = descs + ufi(pr.pidx);
+    const uint32_t epoch = ufu(prep_ld(&pr.epoch));
+    if (ufu(in.epoch) == epoch) {
+      const PlannerDev& P = *Pp;
+      const uint32_t key = ufu(in.key);
+      const float cx = uff(in.x), cy = uff(in.y), ch = uff(in.h), cvm = uff(in.vmin);
+      const int cci = ufi(in.ci), cbin = key3_bin(key);
+      const bool slow = cvm < 1.0f;
+      int lo = cci - P.na;
+      lo = lo < 0 ? 0 : lo;
+      const int span = 2 * P.na + 1;
+      const int ca = lane >> 4, sub = lane & 15;
+      const int ai = lo + ca;
+      bool cand = ca < span && ai < P.nsteer;
+      const int ia = cand ? ai : lo;
+      const float cabs = gp(P.curv_abs)[ia];
+      const GAS float* ofs = &gp(P.off)[2 * ((size_t)ia * (P.bins + 1) + cbin)];
+      const float ofx = ofs[0], ofy = ofs[1], odth = gp(P.dth)[ia], oact = gp(P.act_cost)[ia];
+      float vm = 0.0f;
+      if (cand && !slow) {
+        const float lat = cvm * cabs;
+        if (lat > P.a_lat) cand = false;
+        const float al = (float)sqrt(1.0 - (double)((lat * lat) / P.a_lat2));
+        vm = cvm - 2.0f * al * P.ts;
+      }
+      float sx = 0.0f, sy = 0.0f, sh = 0.0f;
+      int sbin = 0, scx = 0, scy = 0;
+      bool inb = false;
+      if (cand) {
+        sx = cx + ofx;
+        sy = cy + ofy;
+        sh = wrap_pi_f(ch + odth);
+        sbin = heading_bin(sh, P.prec);
+        scx = trunc_f(sx / P.res);
+        scy = trunc_f(sy / P.res);
+        inb = scx > -1 && scx < P.N && scy > -1 && scy < P.N;
+      }
+      const bool lead = inb && sub == 0;
+      float occv = 0.0f;
+      if (lead) occv = gp(P.occ)[(size_t)scx * P.N + scy];
+      const GoalC GC = goal_centres(P.r_min, P.goal_x, P.goal_y, P.goal_h);
+      const float dub = cand_dubins(P.r_min, GC, P.goal_h, sx, sy, sh, 16, lane);
+      const float fc = apf_fused_k(P, apfs, kept_buf, cx, cy, sx, sy, sh, __ballot(lead), 16, lane);
+      const bool kept = lead && occv < P.thr;
+      if (sub == 0 && ca < PREP_C) {
+        PrepCand o;
+        o.sx = sx;
+        o.sy = sy;
+        o.sh = sh;
+        o.vm = vm;
+        o.fc = fc;
+        o.dub = dub;
+        o.oact = oact;
+        o.skey = key3(scx, scy, sbin);
+        o.flags = (cand ? 1u : 0u) | (inb ? 2u : 0u) | (kept ? 4u : 0u);
+        o.pad0 = o.pad1 = o.pad2 = 0u;
+        __builtin_memcpy((PrepCand*)&pr.out[be][ca], &o, sizeof(o));
+      }
+    }
+    wave_lds_sync();
+    if (lane == 0) prep_st(&pr.state[be], (best << 2) | 3u);
+  }
+}
+
 // The loop of hybrid_a_star_search (HybridAStar.cpp:107-194) over outer open tree OT: the
 // HBM tree behind the register cache (RBT<CachedAcc3>) or the latency kernel's LDS tree
 // (RBT<LdsAcc3>).  Returns LOOP_DONE (the search ended: goal, shot, empty open set or a
@@ -1226,9 +1428,10 @@ struct LoopState {
   int ok, via_shot, terminal, dub_n;
   float cost;
 };
-template <class CF, bool kLdsOuter, class OT>
+template <class CF, bool kLdsOuter, bool kPrep, class OT>
 __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs, AStarLdsT<CF>& alds, LoopState& S,
-                                           long long hard_pops, int closed_lim, int open_lim, int open_cap) {
+                                           long long hard_pops, int closed_lim, int open_lim, int open_cap,
+                                           PrepL* pr = nullptr) {
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
@@ -1344,28 +1547,53 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     const int ai = lo + ca;
     bool cand = ca < span && ai < P.nsteer;
     const int ia = cand ? ai : lo;  // in-range index: the table loads are unconditional
-    const float cabs = gp(P.curv_abs)[ia];
-    const GAS float* ofs = &gp(P.off)[2 * ((size_t)ia * (P.bins + 1) + cbin)];
-    const float ofx = ofs[0], ofy = ofs[1], odth = gp(P.dth)[ia], oact = gp(P.act_cost)[ia];
-    float vm = 0.0f;
-    if (cand && !shot_allowed) {
-      const float lat = cur.vmin * cabs;
-      if (lat > P.a_lat) cand = false;
-      const float al = (float)sqrt(1.0 - (double)((lat * lat) / P.a_lat2));
-      vm = cur.vmin - 2.0f * al * P.ts;
+    // latency kernel: a helper wave may have computed this expansion already (bit for bit the
+    // values below: the same code on the same inputs, prep_helper)
+    int pe = -1;
+    if constexpr (kPrep) {
+      if (gs == 16) pe = prep_find(*pr, cur.key, cur.x, cur.y, cur.h, cur.vmin, cur.ci, c.prep_epoch, lane);
     }
-    float sx = 0.0f, sy = 0.0f, sh = 0.0f, sg = 0.0f;
+    float vm = 0.0f, sx = 0.0f, sy = 0.0f, sh = 0.0f, sg = 0.0f, dub = 0.0f, fc = 0.0f;
     int sbin = 0, scx = 0, scy = 0;
-    bool inb = false;
-    if (cand) {
-      sx = cur.x + ofx;
-      sy = cur.y + ofy;
-      sh = wrap_pi_f(cur.h + odth);
-      sg = cur.g + oact;
-      sbin = heading_bin(sh, P.prec);
-      scx = trunc_f(sx / P.res);
-      scy = trunc_f(sy / P.res);
-      inb = scx > -1 && scx < c.N && scy > -1 && scy < c.N;
+    bool inb = false, pkept = false;
+    if (kPrep && pe >= 0) {
+      PrepCand pc;
+      __builtin_memcpy(&pc, (const PrepCand*)&pr->out[pe][ca & (PREP_C - 1)], sizeof(pc));
+      cand = cand && ca < PREP_C && (pc.flags & 1u);
+      if (cand) {
+        sx = pc.sx;
+        sy = pc.sy;
+        sh = pc.sh;
+        vm = pc.vm;
+        sg = cur.g + pc.oact;
+        sbin = key3_bin(pc.skey);
+        scx = key3_x(pc.skey);
+        scy = key3_y(pc.skey);
+        inb = (pc.flags & 2u) != 0u;
+        pkept = (pc.flags & 4u) != 0u;
+        dub = pc.dub;
+        fc = pc.fc;
+      }
+    } else {
+      const float cabs = gp(P.curv_abs)[ia];
+      const GAS float* ofs = &gp(P.off)[2 * ((size_t)ia * (P.bins + 1) + cbin)];
+      const float ofx = ofs[0], ofy = ofs[1], odth = gp(P.dth)[ia], oact = gp(P.act_cost)[ia];
+      if (cand && !shot_allowed) {
+        const float lat = cur.vmin * cabs;
+        if (lat > P.a_lat) cand = false;
+        const float al = (float)sqrt(1.0 - (double)((lat * lat) / P.a_lat2));
+        vm = cur.vmin - 2.0f * al * P.ts;
+      }
+      if (cand) {
+        sx = cur.x + ofx;
+        sy = cur.y + ofy;
+        sh = wrap_pi_f(cur.h + odth);
+        sg = cur.g + oact;
+        sbin = heading_bin(sh, P.prec);
+        scx = trunc_f(sx / P.res);
+        scy = trunc_f(sy / P.res);
+        inb = scx > -1 && scx < c.N && scy > -1 && scy < c.N;
+      }
     }
     const bool lead = inb && sub == 0;
     const uint32_t skey = key3(scx, scy, sbin);
@@ -1375,21 +1603,27 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     uint32_t pvis = 0;
     if (lead) {
       const size_t cell = (size_t)scx * c.N + scy;
-      occv = c.occ[cell];
+      if (!kPrep || pe < 0) occv = c.occ[cell];
       sh0 = slot_hash(skey) & c.smask;
       slot0 = *(const GAS v2u*)&c.slots3[sh0];
       pvis = (c.visited[cell >> 5] >> (cell & 31)) & 1u;
       pnf = c.nm_f[cell];
     }
     STAMP_ADD(16, tx);
-    STAMP_T tdub = STAMP_NOW();
-    const float dub = cand_dubins(r, GC, P.goal_h, sx, sy, sh, gs, lane);
-    STAMP_ADD(18, tdub);
-    STAMP_T tapf = STAMP_NOW();
-    const float fc = apf_fused(P, apfs, cur.x, cur.y, sx, sy, sh, __ballot(lead), gs, lane);
-    STAMP_ADD(17, tapf);
+    if (!kPrep || pe < 0) {
+      STAMP_T tdub = STAMP_NOW();
+      dub = cand_dubins(r, GC, P.goal_h, sx, sy, sh, gs, lane);
+      STAMP_ADD(18, tdub);
+      STAMP_T tapf = STAMP_NOW();
+      fc = apf_fused(P, apfs, cur.x, cur.y, sx, sy, sh, __ballot(lead), gs, lane);
+      STAMP_ADD(17, tapf);
+    }
     STAMP_T tw = STAMP_NOW();
-    const bool kept = lead && occv < c.thr;
+    const bool kept = lead && ((kPrep && pe >= 0) ? pkept : occv < c.thr);
+    // hand the kept successors to the helper waves: the next pops are mostly among them
+    if constexpr (kPrep) {
+      if (gs == 16) prep_post(*pr, kept, skey, sx, sy, sh, vm, lo + ca, c.prep_epoch, lane);
+    }
     const uint64_t km = __ballot(kept);
     c.succ += __popcll(km);
     // closed-set membership (continuing each kept candidate's probe sequence; the closed
@@ -1493,7 +1727,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
 // pops with HASTAR_EOVERFLOW (an explicit budget; 0 = none, the reference's behaviour).
 template <class CF, bool kWide>
 __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLdsT<CF>& alds, OuterLds* ol,
-                                           long long hard_pops, bool resume, int dbg = 0) {
+                                           long long hard_pops, bool resume, int dbg = 0, PrepL* pr = nullptr) {
   bind_hot(c);
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
@@ -1503,6 +1737,13 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
 #endif
   unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   apf_stage(P, apfs, lane);
+  if constexpr (kWide) {  // a new epoch of the helper waves' prep table: this planner, its map and APF list
+    c.prep_epoch += 1u;  // the main wave alone writes the epoch (and pidx, before the call): it counts its searches
+    if (lane == 0) {
+      prep_st(&pr->epoch, c.prep_epoch);
+    }
+    wave_lds_sync();
+  }
   c.o3.t = c.open3;
   c.o3.lane = lane;
   c.o3.reset_cache();
@@ -1584,13 +1825,13 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     // its tree in when it does), then continues in HBM
     if ((!resume || lds_outer_load(c, *ol, lane)) && !(dbg & 1)) {
       RBT<LdsAcc3> lt = lds_tree(*ol, c);
-      code = search_loop<CF, true>(c, lt, apfs, alds, S, hard_pops, closed_lim, open_lim, OUTER_LDS_CAP);
+      code = search_loop<CF, true, kWide>(c, lt, apfs, alds, S, hard_pops, closed_lim, open_lim, OUTER_LDS_CAP, pr);
       if (code == LOOP_MIGRATE) lds_outer_store(c, *ol, lane);
     }
   }
   if (code == LOOP_MIGRATE) {
     c.o3.reset_cache();
-    code = search_loop<CF, false>(c, c.o3, apfs, alds, S, hard_pops, closed_lim, open_lim, A.open3_cap);
+    code = search_loop<CF, false, kWide>(c, c.o3, apfs, alds, S, hard_pops, closed_lim, open_lim, A.open3_cap, pr);
   }
   const bool parked = code == LOOP_PARKED;
   counter = S.counter;
@@ -1709,6 +1950,10 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     R->t_start = t_start;
     R->t_end = __builtin_amdgcn_s_memrealtime();
     R->slot = c.slot;
+    // placement of the wave that ran it (diagnostics of the split launch):
+    // s_getreg of HW_REG_XCC_ID (hwreg 20) and HW_REG_HW_ID (hwreg 4), full 32-bit fields
+    R->hw_id = (int)(((uint32_t)__builtin_amdgcn_s_getreg(0xF814) & 0xfu) << 16 |
+                     ((uint32_t)__builtin_amdgcn_s_getreg(0xF804) & 0xffffu));
     R->parks = parks;
 #ifdef HASTAR_STAMPS
     c.cyc[22] = c.o3.n_fill;
@@ -1792,28 +2037,49 @@ struct WideLdsT {
   ApfStage apfs;
   AStarLdsT<CF> alds;
   OuterLds ol;
+  PrepShared prep;
 };
 using WideLds = WideLdsT<WideA>;
 static_assert(sizeof(WideLds) <= 163840, "the latency kernel's LDS must fit one CU");
+// Wave 0 runs the searches; waves 1 .. PREP_HELPERS precompute expansions for it (prep_helper).
+constexpr int WIDE_WAVES = 1 + PREP_HELPERS;
 template <class CF>
-__global__ __launch_bounds__(64) void hastar_search_wide_kernel(const PlannerDev* __restrict__ descs, int n_planners,
-                                                                const SlotArena* __restrict__ arenas,
-                                                                const int* __restrict__ order, int* __restrict__ next,
-                                                                long long hard_pops, int resume, int dbg,
-                                                                int arena_base, int first_static) {
+__global__ __launch_bounds__(64 * WIDE_WAVES) void hastar_search_wide_kernel(
+    const PlannerDev* __restrict__ descs, int n_planners, const SlotArena* __restrict__ arenas,
+    const int* __restrict__ order, int* __restrict__ next, long long hard_pops, int resume, int dbg, int arena_base,
+    int first_static) {
   __shared__ WideLdsT<CF> W;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = (int)(threadIdx.x & 63);
+  PrepL* pr = lp(&W.prep);
+  if (wv == 0) {
+    for (int e = lane; e < PREP_E; e += 64) pr->state[e] = 0u;
+    if (lane == 0) {
+      pr->tail = 0u;
+      pr->epoch = 0u;
+      pr->stop = 0u;
+    }
+  }
+  __syncthreads();  // the only workgroup barrier: helpers start on an initialised table
+  if (wv > 0) {
+    prep_helper(*pr, W.apfs, descs, wv, lane);
+    return;
+  }
   SearchCtx c;
   c.A = arenas + blockIdx.x;
   c.slot = arena_base + (int)blockIdx.x;
   const SlotArena& A = *c.A;
-  c.lane = threadIdx.x;
+  c.lane = lane;
   c.cost_only = true;
+  c.prep_epoch = 0u;
   c.gen3 = gp(A.gens)[0];
   c.gen2 = gp(A.gens)[1];
   if (resume) {
     if ((int)blockIdx.x < n_planners) {
-      c.P = descs + order[blockIdx.x];
-      search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, true, dbg);
+      const int pi = order[blockIdx.x];
+      c.P = descs + pi;
+      if (lane == 0) pr->pidx = pi;
+      search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, true, dbg, pr);
     }
   } else {
     // first_static: workgroup b runs queue entry b first (the head of a longest-first queue
@@ -1827,13 +2093,16 @@ __global__ __launch_bounds__(64) void hastar_search_wide_kernel(const PlannerDev
         q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
       }
       if (q >= n_planners) break;
-      c.P = descs + order[q];
-      if (search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, false, dbg)) break;
+      const int pi = order[q];
+      c.P = descs + pi;
+      if (lane == 0) pr->pidx = pi;
+      if (search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, false, dbg, pr)) break;
     }
   }
   if (c.lane == 0) {
     gp(A.gens)[0] = c.gen3;
     gp(A.gens)[1] = c.gen2;
+    prep_st(&pr->stop, 1u);  // the helpers leave their loop
   }
 }
 
@@ -2483,7 +2752,7 @@ static int wide_dbg() {
 }
 static void launch_wide_cf(dim3 g, hipStream_t st, const PlannerDev* d, int n, const SlotArena* a, const int* o,
                            int* nx, long long hp, int resume, int dbg, int first_static = 0) {
-  hipLaunchKernelGGL(hastar_search_wide_kernel<WideA>, g, dim3(64), 0, st, d, n, a, o, nx, hp, resume, dbg, 0,
+  hipLaunchKernelGGL(hastar_search_wide_kernel<WideA>, g, dim3(64 * WIDE_WAVES), 0, st, d, n, a, o, nx, hp, resume, dbg, 0,
                      first_static);
 }
 hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, const int* d_order,

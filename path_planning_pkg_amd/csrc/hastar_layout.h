@@ -112,7 +112,8 @@ struct SearchResult {
   int astar_migrations;   // inner A* searches that outgrew LDS
   unsigned long long cycles[NSTAMP]; // diagnostic build (-DHASTAR_STAMPS): s_memtime per phase
   unsigned long long t_start, t_end;  // s_memrealtime (100 MHz, chip-wide) around the search
-  int slot, pad_r;                    // slot (wavefront) that ran it
+  int slot;                           // slot (wavefront) that ran it
+  int hw_id;                          // where: XCC_ID << 16 | HW_ID bits 15:0 (SE, SH, CU, SIMD, wave) at the end
   // park state (status == SEARCH_PARKED)
   int park_arena;                     // arena index (in the launch's arena array) holding the state
   int counter, interval, shot_allowed;  // Dubins-shot schedule (HybridAStar.cpp:96-154)
@@ -151,7 +152,7 @@ struct PlannerDev {
   float* out_xyh;        // reconstructed path (out_cap x 3) and curvature (out_cap)
   float* out_curv;
   int out_cap;
-  int pad_o0;
+  int astar_cap;         // max_astar_nodes + 1: the inner open tree's pool, whatever arena runs the search
   SearchResult* result;
 };
 

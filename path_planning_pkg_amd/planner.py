@@ -82,6 +82,7 @@ def load_library():
     L.hastar_debug_astar_modes.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_timing.argtypes = [vp, C.POINTER(C.c_ulonglong)]
     L.hastar_debug_slots.argtypes = [vp, C.POINTER(C.c_longlong)]
+    L.hastar_debug_hw_id.argtypes = [vp, ip]
     L.hastar_debug_split.argtypes = [vp, fp]
     L.hastar_debug_relaxed_pool.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_pooled_resumes.argtypes = [C.POINTER(C.c_longlong)]
@@ -407,6 +408,14 @@ class HybridAStar:
         out = (C.c_ulonglong * 3)()
         _check(load_library().hastar_debug_timing(self.h, out))
         return out[0], out[1], int(out[2])
+
+    def hw_id(self):
+        """(XCC, CU, SE, SH, SIMD) of the wavefront that ran the last search (HW_REG_XCC_ID /
+        HW_REG_HW_ID: wave 3:0, SIMD 5:4, pipe 7:6, CU 11:8, SH 12, SE 15:13)."""
+        v = C.c_int(0)
+        _check(load_library().hastar_debug_hw_id(self.h, C.byref(v)))
+        x = v.value
+        return (x >> 16) & 0xF, (x >> 8) & 0xF, (x >> 13) & 0x7, (x >> 12) & 1, (x >> 4) & 3
 
     def field(self, poses):
         p = _f32(poses, (-1, 3))

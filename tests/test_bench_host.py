@@ -74,3 +74,20 @@ def test_parity_sample_compares_every_field():
     bent = dict(ref)
     bent[2] = dict(ref[2], stats=st)
     assert bench.parity_sample(cfgs, bent, [0, 1, 2])["mismatched_queries"] == [2]
+
+
+def test_cfg5_parity_compares_every_pair_and_tick():
+    import numpy as np
+    import bench
+    r = dict(ok=True, cost=1.5, path=np.ones((3, 3), np.float32), curvature=np.zeros(3, np.float32),
+             stats=dict(pops=7, pop_digest=11, closed_digest=13))
+    k = bench.tick_key(r)
+    g = [[k, k], [k, k]]
+    out = bench.cfg5_parity(g, {0: [k, k], 1: [k, k]}, [5, 6])
+    assert out["bit_exact"] and out["searches"] == 4 and out["pops_checked"] == 28
+    r2 = dict(r, path=r["path"].copy())
+    r2["path"][1, 2] = np.nextafter(np.float32(1), np.float32(2))
+    out = bench.cfg5_parity(g, {0: [k, k], 1: [k, bench.tick_key(r2)]}, [5, 6])
+    assert not out["bit_exact"] and out["mismatched_pair_ticks"] == [[6, 1]]
+    # a pair the oracle did not replay (budget) leaves the readout partial, never "bit_exact"
+    assert not bench.cfg5_parity(g, {0: [k, k]}, [5, 6])["bit_exact"]

@@ -22,19 +22,52 @@ ap.add_argument("--obstacles", type=int, default=200)
 ap.add_argument("--seeds", type=int, nargs="+", default=[1])
 ap.add_argument("--generator", choices=["pcg64", "mt19937"], default="mt19937")
 ap.add_argument("--replan", action="store_true", help="profile the bench step: find_path, reset, find_path")
+ap.add_argument("--cfg5-pairs", type=int, nargs="*", default=None,
+                help="profile cfg5 replan loops instead (pair ids, bench.py --workload cfg5): every tick's search, "
+                     "summed over --ticks ticks (the latency kernel)")
+ap.add_argument("--ticks", type=int, default=6)
 args = ap.parse_args()
 names = ["pop", "expand", "open_bookkeeping", "astar", "shot", "reconstruct", "loop", "astar_hbm_mode"]
-for s in args.seeds:
-    gen = synthetic_ref if args.generator == "mt19937" else synthetic
-    cfg, proto = gen(args.grid, args.bins, args.obstacles, s)
+def cfg5_runs(pair):
+    """one cfg5 pair's replan loop (no reset between ticks); yields per tick (planner, stats, ms)"""
+    from tests.scenarios import replan_pairs, replan_tick_inputs
+    cfg, proto, v = replan_pairs(args.grid, args.bins, args.obstacles, 1, seed=1000 + pair)[0]
     p = gpu.HybridAStar(cfg)
     drive(p, proto)
-    if args.replan:
-        gpu.find_path_batch([p], [proto["vel"]], [proto["start"]])
-        p.reset()
-    res, ms = gpu.find_path_batch([p], [proto["vel"]], [proto["start"]])
-    cyc = p.cycles()
-    st = res[0]["stats"]
+    for t in range(args.ticks):
+        start, _ = replan_tick_inputs(proto, v, t)
+        res, ms = gpu.find_path_batch([p], [proto["vel"]], [start])
+        yield p, res[0]["stats"], ms
+        _, boxes = replan_tick_inputs(proto, v, t + 1)
+        p.decay()
+        p.update_boxes(boxes, [proto["box_conf"]] * len(boxes), proto["apf_r"])
+
+
+def runs():
+    if args.cfg5_pairs is not None:
+        for pair in args.cfg5_pairs:
+            tot, stt, mss = None, None, 0.0
+            for p, st, ms in cfg5_runs(pair):
+                cyc = p.cycles()
+                tot = list(cyc) if tot is None else [a + b for a, b in zip(tot, cyc)]
+                stt = dict(st) if stt is None else {k: stt[k] + st[k] if isinstance(st[k], int) and k not in
+                                                    ("pop_digest", "closed_digest", "status") else st[k] for k in st}
+                mss += ms
+            yield f"cfg5 pair {pair} x {args.ticks} ticks", p, tot, stt, mss
+        return
+    for s in args.seeds:
+        gen = synthetic_ref if args.generator == "mt19937" else synthetic
+        cfg, proto = gen(args.grid, args.bins, args.obstacles, s)
+        p = gpu.HybridAStar(cfg)
+        drive(p, proto)
+        if args.replan:
+            gpu.find_path_batch([p], [proto["vel"]], [proto["start"]])
+            p.reset()
+        res, ms = gpu.find_path_batch([p], [proto["vel"]], [proto["start"]])
+        yield s, p, p.cycles(), res[0]["stats"], ms
+
+
+for s, p, cyc, st, ms in runs():
     loop = max(cyc[6], 1)
     share = {names[i]: round(cyc[i] / loop, 4) for i in range(6)}
     share["open_bookkeeping"] = round((cyc[2] - cyc[3]) / loop, 4)
