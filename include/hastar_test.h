@@ -40,6 +40,9 @@ int hastar_debug_hw_id(hastar_handle h, int* out);
 /* Search-slot pool of the handle's device: {resident wavefronts, search waves per CU, arenas, MiB per arena,
    latency CUs of a split launch (0: none)}. */
 int hastar_debug_slots(hastar_handle h, long long* out5);
+/* head arenas of the device's split launches: {count, pool arenas per head arena (0 = own
+ * allocation), outer capacity in pops} (hastar_capi.cpp head_acquire) */
+int hastar_debug_head_arenas(hastar_handle h, long long* out3);
 /* the device's last split launch (hastar_find_path_batch of a large batch): ms from the timed
  * region's start to the head kernel's start and end, and to the bulk kernel's start and end */
 int hastar_debug_split(hastar_handle h, float* out4);

@@ -220,6 +220,17 @@ struct DeviceCtx {
   long long last_total = 0;
   char* vel_slab = nullptr;       // velocity-profile staging (grown, reused)
   size_t vel_cap = 0;
+  // Head arenas of a split launch: after a search parked in a split launch, the latency CUs of
+  // the next ones get arenas sized for it (so the head's longest searches run through without
+  // waiting for the launch's end to resume): an allocation of their own when the HBM has room,
+  // else carved from the pool's first head_n * head_k arenas (the bulk keeps the rest).
+  // head_n = 0: none (the head uses plain pool arenas).
+  int head_k = 0, head_n = 0;     // head_k: pool arenas per carved head arena (0: own allocation)
+  void* head_slab = nullptr;      // the own allocation
+  long long head_grant = 0;       // their outer capacity in pops (SlotArena::pops_grant)
+  long long head_want = 0;        // pops of the longest search that parked in a split launch
+  SlotArena* d_head = nullptr;    // their descriptors (head_n); the head kernel's slot ids start at n_arenas
+  std::vector<SlotArena> h_head;
   SlotArena* d_resume = nullptr;  // arena descriptors of a resume launch
   int* d_resume_order = nullptr;
   size_t resume_cap = 0;
@@ -434,6 +445,10 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
   D.slab = nullptr;
   D.d_arenas = nullptr;
   D.n_arenas = 0;
+  if (D.head_k > 0) {  // head arenas carved from the old slab
+    D.head_k = D.head_n = 0;
+    D.head_grant = 0;
+  }
   const ArenaLayout lay = arena_layout(r);
   const size_t per = lay.total();
   // memory budget of the pool: HASTAR_ARENA_MB, else HASTAR_ARENA_FRAC (default 0.8) of
@@ -467,6 +482,70 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
   D.n_arenas = n;
   D.arena_bytes = per;
   D.fit_arenas = n < n_want ? n : (1 << 30);
+  return 0;
+}
+
+// Head arenas released: the pool arenas a head carve took get their plain layout back (fresh
+// generation-stamped tables; the descriptors in d_arenas never changed), an own allocation is
+// freed.
+int head_release(DeviceCtx& D) {
+  if (D.head_n == 0) return 0;
+  if (D.head_k > 0) {
+    const ArenaLayout lay = arena_layout(D.areq);
+    for (int q = 0; q < D.head_n * D.head_k; ++q) {
+      SlotArena tmp;
+      HIPCHK(carve_arena(static_cast<char*>(D.slab) + D.arena_bytes * (size_t)q, D.areq, lay, &tmp, D.stream));
+    }
+  }
+  HIPCHK(hipStreamSynchronize(D.stream));
+  if (D.head_slab) hipFree(D.head_slab);
+  D.head_slab = nullptr;
+  D.head_k = D.head_n = 0;
+  D.head_grant = 0;
+  return 0;
+}
+
+// Head arenas for a split launch with `head` latency CUs, each holding a search of head_want
+// pops (+25 %): an own allocation when the HBM keeps kHeadroom beside it, else k consecutive
+// pool arenas each, while at most a quarter of the launch's `slots` arenas go to them.  None
+// when no search needs them or neither way has the room.
+int head_acquire(DeviceCtx& D, int head, int span, int slots) {
+  // (a parked search outgrew its planner's capacity rule, P.arena_pops << 2 parks, whatever
+  // the pool arena's size: the grant lifts that rule in the head arenas, hastar_kernels.hip)
+  if (D.head_want <= 0 || D.arena_bytes == 0) return head_release(D);
+  const long long grant = std::min(D.head_want + D.head_want / 4, (long long)SLOT3_IDX_MASK - 1);
+  if (D.head_n == head && D.head_grant == grant) return 0;
+  if (int rc = head_release(D)) return rc;
+  ArenaReq r = D.areq;
+  size_outer(r, grant, span);
+  r.merge(D.areq);
+  const ArenaLayout lay = arena_layout(r);
+  const size_t each = lay.total();
+  size_t fr = 0, tot = 0;
+  int k = 0;
+  if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > each * (size_t)head + kHeadroom &&
+      hipMalloc(&D.head_slab, each * (size_t)head) == hipSuccess) {
+    k = 0;
+  } else {
+    D.head_slab = nullptr;
+    k = (int)((each + D.arena_bytes - 1) / D.arena_bytes);
+    if ((long long)head * k > slots / 4) return 0;  // the bulk would lose too many arenas
+  }
+  D.h_head.assign((size_t)head, SlotArena{});
+  for (int b = 0; b < head; ++b) {
+    char* at = D.head_slab ? static_cast<char*>(D.head_slab) + each * (size_t)b
+                           : static_cast<char*>(D.slab) + D.arena_bytes * (size_t)b * k;
+    HIPCHK(carve_arena(at, r, lay, &D.h_head[(size_t)b], D.stream));
+    D.h_head[(size_t)b].pops_grant = (int)grant;
+  }
+  if (D.d_head) hipFree(D.d_head);
+  D.d_head = nullptr;
+  HIPCHK(dalloc(&D.d_head, (size_t)head));
+  HIPCHK(hipMemcpyAsync(D.d_head, D.h_head.data(), (size_t)head * sizeof(SlotArena), hipMemcpyHostToDevice, D.stream));
+  HIPCHK(hipStreamSynchronize(D.stream));
+  D.head_k = k;
+  D.head_n = head;
+  D.head_grant = grant;
   return 0;
 }
 
@@ -1819,6 +1898,20 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   if (int rc = arenas_acquire(DC, need, W)) return rc;
   const int slots = std::min(W, DC.n_arenas);
   if (int rc = batch_acquire(DC, n)) return rc;
+  // HASTAR_SPLIT_MODE=2: the head searches run on head workgroups of the batch kernel itself
+  // (wave 0 alone on its CU, the batch kernel's code and LDS layout) instead of the latency kernel
+  const char* sm_env = std::getenv("HASTAR_SPLIT_MODE");
+  const int split_mode = sm_env && std::atoi(sm_env) == 2 ? 2 : 1;
+  const bool split2 = split && slots > head && split_mode == 2;
+  const bool split1 = split && slots > head && !split2;
+  {
+    // head arenas (DeviceCtx::head_k) only for the latency kernel's head of a split launch
+    int span = 2;
+    for (int i = 0; i < n; ++i) span = std::max(span, hs[i]->span);
+    if (int rc = split1 ? head_acquire(DC, head, span, slots) : head_release(DC)) return rc;
+  }
+  // pool arenas [0, hoff) carved into head arenas
+  const int hoff = DC.head_k > 0 ? DC.head_n * DC.head_k : 0;
   std::vector<PlannerDev> descs(n);
   for (int i = 0; i < n; ++i) {
     prepare_start(hs[i], vel[i], starts + 3 * i);
@@ -1865,18 +1958,14 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     ms_total += ms;
     return 0;
   };
-  // HASTAR_SPLIT_MODE=2: the head searches run on head workgroups of the batch kernel itself
-  // (wave 0 alone on its CU, the batch kernel's code and LDS layout) instead of the latency kernel
-  const char* sm_env = std::getenv("HASTAR_SPLIT_MODE");
-  const int split_mode = sm_env && std::atoi(sm_env) == 2 ? 2 : 1;
-  const bool split2 = split && slots > head && split_mode == 2;
   if (int r = timed([&]() -> hipError_t {
         if (split2)
           return launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, hard_pops, st, 0, -1,
                                head);
-        if (split && slots > head) {
+        if (split1) {
           // the head's queue entries 0 .. head-1 are taken statically by the latency workgroups
-          // (arenas 0 .. head-1); the batch kernel's waves count on from `head` (arenas head ..)
+          // (arenas 0 .. head-1, or the head arenas); the batch kernel's waves count on from
+          // `head` (pool arenas from max(head, hoff))
           const int init[4] = {head, 0, 0, 0};
           hipError_t e = hipMemcpyAsync(DC.d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
           if (e == hipSuccess) e = hipEventRecord(DC.ev_fork, st);
@@ -1884,11 +1973,15 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
           if (e == hipSuccess) e = hipStreamWaitEvent(DC.bulk_st, DC.ev_fork, 0);
           if (e == hipSuccess) e = hipEventRecord(DC.ev_hs, DC.head_st);
           if (e == hipSuccess) e = hipEventRecord(DC.ev_bs, DC.bulk_st);
+          const int boff = std::max(head, hoff);
           if (e == hipSuccess)
-            e = launch_search_wide(DC.d_descs, n, DC.d_arenas, head, DC.d_order, DC.d_next, hard_pops, DC.head_st, 1);
+            e = DC.head_n > 0 ? launch_search_wide(DC.d_descs, n, DC.d_head, head, DC.d_order, DC.d_next, hard_pops,
+                                                   DC.head_st, 1, DC.n_arenas)
+                              : launch_search_wide(DC.d_descs, n, DC.d_arenas, head, DC.d_order, DC.d_next, hard_pops,
+                                                   DC.head_st, 1);
           if (e == hipSuccess)
-            e = launch_search(DC.d_descs, n, DC.d_arenas + head, std::min(slots - head, (DC.n_cu - head) * per_cu),
-                              DC.d_order, n_prio, DC.d_next, hard_pops, DC.bulk_st, head, -1);
+            e = launch_search(DC.d_descs, n, DC.d_arenas + boff, std::min(slots - boff, (DC.n_cu - head) * per_cu),
+                              DC.d_order, n_prio, DC.d_next, hard_pops, DC.bulk_st, boff, -1);
           if (e == hipSuccess) e = hipEventRecord(DC.ev_head, DC.head_st);
           if (e == hipSuccess) e = hipEventRecord(DC.ev_bulk, DC.bulk_st);
           if (e == hipSuccess) e = hipStreamWaitEvent(st, DC.ev_head, 0);
@@ -1899,7 +1992,7 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
                     : launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, hard_pops, st);
       }))
     return r;
-  if (split && slots > head && !split2) {
+  if (split1) {
     hipEventElapsedTime(&DC.split_ms[0], DC.ev0, DC.ev_hs);
     hipEventElapsedTime(&DC.split_ms[1], DC.ev0, DC.ev_head);
     hipEventElapsedTime(&DC.split_ms[2], DC.ev0, DC.ev_bs);
@@ -1930,8 +2023,8 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
       // resume arena.
       nxt.clear();
       std::vector<char> pool_busy((size_t)DC.n_arenas, 0);
-      const int wq = notrun.empty() ? 0 : std::min<int>(slots, (int)notrun.size());
-      for (int q = 0; q < wq && q < DC.n_arenas; ++q) pool_busy[(size_t)q] = 1;
+      const int wq = notrun.empty() ? 0 : std::min<int>(slots - hoff, (int)notrun.size());
+      for (int q = 0; q < hoff + wq && q < DC.n_arenas; ++q) pool_busy[(size_t)q] = 1;
       for (int i : parked)
         if (!in_resume[i] && DC.h_results[i].park_arena >= 0 && DC.h_results[i].park_arena < DC.n_arenas)
           pool_busy[(size_t)DC.h_results[i].park_arena] = 1;
@@ -1960,6 +2053,8 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
         SlotArena host_from;
         if (in_resume[i]) {
           from = &cur[(size_t)R.park_arena].desc;
+        } else if (R.park_arena >= DC.n_arenas) {  // a head arena (slot ids n_arenas + b)
+          from = &DC.h_head[(size_t)(R.park_arena - DC.n_arenas)];
         } else {
           HIPCHK(hipMemcpy(&host_from, DC.d_arenas + R.park_arena, sizeof(SlotArena), hipMemcpyDeviceToHost));
           from = &host_from;
@@ -2012,12 +2107,12 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
       if (!notrun.empty()) {
         HIPCHK(hipMemcpyAsync(DC.d_order, notrun.data(), notrun.size() * sizeof(int), hipMemcpyHostToDevice, st));
         for (int i : notrun) in_resume[i] = 0;
-        const int w = std::min<int>(slots, (int)notrun.size());
+        const int w = std::min<int>(slots - hoff, (int)notrun.size());
         if (int r = timed([&] {
-              return wide ? launch_search_wide(DC.d_descs, (int)notrun.size(), DC.d_arenas, w, DC.d_order, DC.d_next,
-                                               hard_pops, st)
-                          : launch_search(DC.d_descs, (int)notrun.size(), DC.d_arenas, w, DC.d_order, 0, DC.d_next,
-                                          hard_pops, st);
+              return wide ? launch_search_wide(DC.d_descs, (int)notrun.size(), DC.d_arenas + hoff, w, DC.d_order,
+                                               DC.d_next, hard_pops, st, 0, hoff)
+                          : launch_search(DC.d_descs, (int)notrun.size(), DC.d_arenas + hoff, w, DC.d_order, 0,
+                                          DC.d_next, hard_pops, st, hoff);
             }))
           return r;
       }
@@ -2063,6 +2158,10 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
       HIPCHK(hipStreamSynchronize(st));
     }
   }
+  // a search that parked in a split launch sizes the next split launches' head arenas
+  if (split1)
+    for (int i = 0; i < n; ++i)
+      if (DC.h_results[i].parks > 0) DC.head_want = std::max(DC.head_want, DC.h_results[i].pops);
   g_last_ms = ms_total;
   return finish_batch(DC, hs, n, xyh, curv, cap, len, cost, ok, stats, true);
 }
@@ -2553,6 +2652,7 @@ static int astar_run(hastar_handle h, int si, int sj, int mode, const float goal
   DeviceCtx& DC = *h->dc;
   std::lock_guard<std::mutex> lk(DC.mu);
   if (int rc = arenas_acquire(DC, h->areq, 1)) return rc;
+  if (int rc = head_release(DC)) return rc;
   const int pcap = std::max(cap, 1);
   const size_t bytes = align256(sizeof(PlannerDev)) + 256 + align256((size_t)pcap * 2 * sizeof(float)) + 256;
   if (int rc = stage_acquire(DC, bytes)) return rc;
@@ -2763,6 +2863,15 @@ int hastar_debug_slots(hastar_handle h, long long* out5) {
   out5[2] = D.n_arenas;
   out5[3] = (long long)(D.arena_bytes >> 20);
   out5[4] = D.head_cus;
+  return HASTAR_OK;
+}
+
+int hastar_debug_head_arenas(hastar_handle h, long long* out3) {
+  if (!h || !h->dc || !out3) return fail(HASTAR_EINVAL, "bad handle");
+  const DeviceCtx& D = *h->dc;
+  out3[0] = D.head_n;
+  out3[1] = D.head_k;
+  out3[2] = D.head_grant;
   return HASTAR_OK;
 }
 

@@ -12,7 +12,8 @@ hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_ar
                          long long hard_pops, hipStream_t st);
 // the latency kernel: one search per CU (batches no larger than the CU count, resumes)
 hipError_t launch_search_wide(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots,
-                              const int* d_order, int* d_next, long long hard_pops, hipStream_t st, int head = 0);
+                              const int* d_order, int* d_next, long long hard_pops, hipStream_t st, int head = 0,
+                              int arena_base = 0);
 int search_slots_per_cu();
 hipError_t launch_relaxed(const PlannerDev* d_descs, int n, const RelaxArena* d_arenas, int n_arenas, int* d_next,
                           const RelaxParams& rp, RelaxField* d_fields, hipStream_t st);

@@ -1804,7 +1804,9 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
   float cost = FLT_MAX;
   // the planner's outer capacity after `parks` resumes (4x each), bounded by this arena: a
   // search parks at the same pop whatever arena the pool happens to hand it
-  const long long pcap = min((long long)P.arena_pops << (2 * min(parks, 12)), (long long)SLOT3_IDX_MASK - 1);
+  // (a head arena sized for the planner's known longest search, pops_grant, lifts it: hastar_capi.cpp head_arenas)
+  const long long pcap = min(max((long long)P.arena_pops << (2 * min(parks, 12)), (long long)A.pops_grant),
+                             (long long)SLOT3_IDX_MASK - 1);
   const int closed_lim = (int)min((long long)A.closed3_cap, pcap + 1);
   const int open_lim = (int)min((long long)A.open3_cap, 2 + (long long)(P.span_alloc - 1) * pcap + 64);
   STAMP_T tloop = STAMP_NOW();
@@ -1862,7 +1864,10 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
       R->n_closed3 = c.n_closed3;
       R->ps3_next = c.ps3.next;
       R->ps3_free = c.ps3.free;
-      R->parks = parks + 1;
+      // the next capacity step beyond this arena's (a head arena's grant may exceed several)
+      int np = parks + 1;
+      while (np < 12 && ((long long)P.arena_pops << (2 * np)) <= pcap) ++np;
+      R->parks = np;
       R->park_arena = c.slot;
       R->ok = 0;
       R->path_len = 0;
@@ -2751,9 +2756,9 @@ static int wide_dbg() {
   return e ? std::atoi(e) : 0;
 }
 static void launch_wide_cf(dim3 g, hipStream_t st, const PlannerDev* d, int n, const SlotArena* a, const int* o,
-                           int* nx, long long hp, int resume, int dbg, int first_static = 0) {
-  hipLaunchKernelGGL(hastar_search_wide_kernel<WideA>, g, dim3(64 * WIDE_WAVES), 0, st, d, n, a, o, nx, hp, resume, dbg, 0,
-                     first_static);
+                           int* nx, long long hp, int resume, int dbg, int first_static = 0, int arena_base = 0) {
+  hipLaunchKernelGGL(hastar_search_wide_kernel<WideA>, g, dim3(64 * WIDE_WAVES), 0, st, d, n, a, o, nx, hp, resume, dbg,
+                     arena_base, first_static);
 }
 hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, const int* d_order,
                          long long hard_pops, hipStream_t st) {
@@ -2763,7 +2768,8 @@ hipError_t launch_resume(const PlannerDev* d_descs, int n, const SlotArena* d_ar
   return hipGetLastError();
 }
 hipError_t launch_search_wide(const PlannerDev* d_descs, int n, const SlotArena* d_arenas, int n_slots,
-                              const int* d_order, int* d_next, long long hard_pops, hipStream_t st, int head) {
+                              const int* d_order, int* d_next, long long hard_pops, hipStream_t st, int head,
+                              int arena_base) {
   // head = 0: the whole queue (counter reset to 0); head = 1: the head of a split queue
   // (workgroup b takes entry b first; the caller set the counter past the head)
   if (!head) {
@@ -2771,7 +2777,7 @@ hipError_t launch_search_wide(const PlannerDev* d_descs, int n, const SlotArena*
     hipError_t e = hipMemcpyAsync(d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return e;
   }
-  launch_wide_cf(dim3(n_slots), st, d_descs, n, d_arenas, d_order, d_next, hard_pops, 0, wide_dbg(), head);
+  launch_wide_cf(dim3(n_slots), st, d_descs, n, d_arenas, d_order, d_next, hard_pops, 0, wide_dbg(), head, arena_base);
   return hipGetLastError();
 }
 int search_slots_per_cu() {

@@ -205,7 +205,7 @@ constexpr int ASTAR_LDS_CAP = 1024;
 // belongs to the wave that runs the search, not to the planner: a persistent kernel with
 // W slots serves any number of planners, and the planners keep only their maps.
 struct SlotArena {
-  Node3* open3;     int open3_cap;   int pad0;
+  Node3* open3;     int open3_cap;   int pops_grant;  // > 0: a head arena's own outer capacity in pops (else the planner's rule)
   Closed3* closed3; int closed3_cap; int pad1;
   Slot3* slots3;    uint32_t slots3_mask; int pad2;
   Node2* open2;     int open2_cap;   int pad3;

@@ -82,6 +82,7 @@ def load_library():
     L.hastar_debug_astar_modes.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_timing.argtypes = [vp, C.POINTER(C.c_ulonglong)]
     L.hastar_debug_slots.argtypes = [vp, C.POINTER(C.c_longlong)]
+    L.hastar_debug_head_arenas.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_hw_id.argtypes = [vp, ip]
     L.hastar_debug_split.argtypes = [vp, fp]
     L.hastar_debug_relaxed_pool.argtypes = [vp, C.POINTER(C.c_longlong)]
@@ -390,6 +391,13 @@ class HybridAStar:
         _check(load_library().hastar_debug_slots(self.h, out))
         return {"resident_slots": out[0], "waves_per_cu": out[1], "arenas": out[2], "arena_mib": out[3],
                 "head_cus": out[4]}
+
+    def head_arenas(self):
+        """The device's head arenas of split launches (after a search parked in one): how many,
+        pool arenas carved per head arena (0 = an allocation of their own), their capacity in pops."""
+        out = (C.c_longlong * 3)()
+        _check(load_library().hastar_debug_head_arenas(self.h, out))
+        return {"n": out[0], "pool_k": out[1], "grant": out[2]}
 
     def split_ms(self):
         """The device's last split launch: ms to head start, head end, bulk start, bulk end."""

@@ -177,8 +177,44 @@ def test_split_launch_head_and_bulk(gpu, oracle_lib, monkeypatch, mode):
     for i, ((cfg, proto), o) in enumerate(zip(cases, os_)):
         compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"split launch planner {i}")
     slots = {int(g.timing()[2]) for g in gs}
-    head = gs[0].slots()["head_cus"]
-    assert any(s < head for s in slots) and any(s >= head for s in slots), (slots, head)
+    sl = gs[0].slots()
+    head, n_arenas = sl["head_cus"], sl["arenas"]
+    on_head = [s < head or s >= n_arenas for s in slots]  # head arenas have slot ids n_arenas + b
+    assert any(on_head) and not all(on_head), (slots, head)
+
+
+def test_split_launch_head_arenas(gpu, oracle_lib, monkeypatch):
+    """Head arenas: searches that parked in a split launch (64-pop arenas) make the next split
+    launches give the latency CUs arenas sized for them, so the head's searches run through
+    without parking.  Every result is the oracle's in all three calls, and after a launch
+    without the split (pool arenas back in their plain layout) too."""
+    monkeypatch.setenv("HASTAR_WIDE", "0")
+    monkeypatch.setenv("HASTAR_SPLIT", "1")
+    cases = [synthetic(256, 36, 10 + (s % 4) * 10, s) for s in range(1, 25)] + [synthetic(512, 72, 50, 1)]
+    gs, os_ = [], []
+    for cfg, proto in cases:
+        cfg.values["max_pops"] = 64
+        g, o = _pair(gpu, oracle_lib, cfg, proto)
+        gs.append(g)
+        os_.append(o)
+    vels, starts = [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases]
+    parks = []
+    for rep in range(4):
+        if rep == 3:
+            monkeypatch.setenv("HASTAR_SPLIT", "0")
+        for g, o in zip(gs, os_):
+            g.reset()
+            o.reset()
+        res, _ = gpu.find_path_batch(gs, vels, starts, cap=8192)
+        for i, ((cfg, proto), o) in enumerate(zip(cases, os_)):
+            compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"head arenas, call {rep}, planner {i}")
+        ha = gs[0].head_arenas()
+        head_parks = [r["stats"]["parks"] for g, r in zip(gs, res) if int(g.timing()[2]) >= gs[0].slots()["arenas"]]
+        parks.append((sum(r["stats"]["parks"] for r in res), ha, head_parks))
+    assert parks[0][0] > 0 and parks[0][1]["n"] == 0, parks       # first call: plain arenas, searches park
+    assert parks[1][1]["n"] > 0 and parks[1][1]["grant"] > 64, parks  # then head arenas, sized for them
+    assert parks[1][2] and not any(parks[1][2]), parks                # the head's searches did not park
+    assert parks[3][1]["n"] == 0, parks                               # released by the unsplit launch
 
 
 @pytest.mark.parametrize("wide", KERNELS)
