@@ -1107,11 +1107,20 @@ struct OuterLds {
   Q3L q[OUTER_LDS_CAP];
   float g[OUTER_LDS_CAP];
 };
+// Path walks (as RBT<CachedAcc3>, rbtree_dev.h): lanes [0, plen) remember the last walk's
+// nodes.  A new walk has every path lane read its node's current quad at once (one parallel
+// ds_read_b128) and follows the path for as long as its own decision at depth d leads to the
+// node at depth d + 1 under the current links: the shared prefix costs one LDS round trip and a
+// ballot instead of a chain of dependent steps.  Links are re-read, never cached, so rotations,
+// erases and reused indices need no bookkeeping: the prefix followed is the walk itself.
 struct LdsAcc3 {
-  static constexpr bool kPathWalk = false;
+  static constexpr bool kPathWalk = true;
   LAS Q3L* q;
   LAS float* gg;
   GAS Node3* t;  // payload records (open3)
+  int lane;
+  int pid;       // this lane's node of the last walk's path (lane = depth)
+  int plen;      // path lanes [0, plen) (wave-uniform)
   __device__ __forceinline__ int L(int x) const { return ufi(q[x].l); }
   __device__ __forceinline__ int R(int x) const { return ufi(q[x].r); }
   __device__ __forceinline__ int P(int x) const { return ufi(q[x].p); }
@@ -1137,7 +1146,89 @@ struct LdsAcc3 {
     o.r = ufi((int)(int16_t)(w.z >> 16));
     return o;
   }
-  __device__ __forceinline__ Quad quad_at(int x, int) const { return quad(x); }
+  __device__ __forceinline__ Quad quad_at(int x, int depth) {
+    if (lane == depth) pid = x;
+    return quad(x);
+  }
+  // the walks of std::set::find / _M_get_insert_unique_pos: CachedAcc3::path_walk's contract
+  __device__ __forceinline__ void path_walk(uint32_t k, float f, bool ins, int* y_, uint32_t* yk_, float* yf_,
+                                            bool* comp_, int* rj_, uint32_t* rk_, float* rf_) {
+    int y = 0, depth = 0;
+    uint32_t yk = 0;
+    float yf = 0.0f;
+    bool comp = true;
+    int rj = -1;
+    uint32_t rk = 0;
+    float rf = 0.0f;
+    int x = P(0);
+    if (x != NIL && plen > 0 && __builtin_amdgcn_readlane(pid, 0) == x) {
+      const bool inpath = lane < plen;
+      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+      v4u w = {0u, 0u, 0xffffffffu, 0u};
+      if (inpath) __builtin_memcpy(&w, (const Q3L*)&q[pid], sizeof(Q3L));
+      const uint32_t ck = w.x;
+      const float cf = __uint_as_float(w.y);
+      const int cl = (int)(int16_t)(w.z & 0xffffu), cr = (int)(int16_t)(w.z >> 16);
+      const bool left = ins ? rb_less(k, f, ck, cf) : !rb_less(ck, cf, k, f);
+      const int child = left ? cl : cr;
+      const int nxt = __shfl_down(pid, 1, 64);
+      const bool cont = inpath && lane + 1 < plen && child == nxt;
+      const uint64_t stop = __ballot(!cont);
+      const int D = (int)__ffsll((unsigned long long)stop) - 1;  // node D is on the path; leave it via child
+      const uint64_t below = D >= 63 ? ~0ull : ((2ull << D) - 1);
+      const uint64_t lmask = __ballot(inpath && left) & below;
+      if (ins) {
+        y = __builtin_amdgcn_readlane(pid, D);
+        yk = (uint32_t)__builtin_amdgcn_readlane((int)ck, D);
+        yf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), D));
+        comp = (lmask >> D) & 1ull;
+        const uint64_t rmask = __ballot(inpath && !left) & below;
+        if (rmask) {
+          const int h = 63 - __builtin_clzll(rmask);
+          rj = __builtin_amdgcn_readlane(pid, h);
+          rk = (uint32_t)__builtin_amdgcn_readlane((int)ck, h);
+          rf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), h));
+        }
+      } else if (lmask) {
+        const int h = 63 - __builtin_clzll(lmask);
+        y = __builtin_amdgcn_readlane(pid, h);
+        yk = (uint32_t)__builtin_amdgcn_readlane((int)ck, h);
+        yf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cf), h));
+      }
+      x = __builtin_amdgcn_readlane(child, D);
+      depth = D + 1;
+    }
+    while (x != NIL) {
+      const Quad qq = quad_at(x, depth++);
+      if (ins) {
+        y = x;
+        yk = qq.key;
+        yf = qq.f;
+        comp = rb_less(k, f, qq.key, qq.f);
+        if (!comp) {
+          rj = y;
+          rk = yk;
+          rf = yf;
+        }
+        x = comp ? qq.l : qq.r;
+      } else if (!rb_less(qq.key, qq.f, k, f)) {
+        y = x;
+        yk = qq.key;
+        yf = qq.f;
+        x = qq.l;
+      } else {
+        x = qq.r;
+      }
+    }
+    plen = depth < 64 ? depth : 64;
+    *y_ = y;
+    *yk_ = yk;
+    *yf_ = yf;
+    *comp_ = comp;
+    *rj_ = rj;
+    *rk_ = rk;
+    *rf_ = rf;
+  }
   __device__ __forceinline__ void leaf(int x, int p) {
     q[x].l = (int16_t)NIL;
     q[x].r = (int16_t)NIL;
@@ -1150,7 +1241,7 @@ struct LdsAcc3 {
     q[x].f = n.f;
     gg[x] = n.g;
   }
-  __device__ __forceinline__ void reset_cache() {}
+  __device__ __forceinline__ void reset_cache() { plen = 0; }
   // the popped node: key/f/links from LDS, the payload from its HBM record
   __device__ __forceinline__ Node3 node(int x) const {
     typedef int v4 __attribute__((ext_vector_type(4)));
@@ -1178,6 +1269,9 @@ __device__ __forceinline__ RBT<LdsAcc3> lds_tree(OuterLds& ol, const SearchCtx& 
   t.q = lp(ol.q);
   t.gg = lp(ol.g);
   t.t = c.open3;
+  t.lane = c.lane;
+  t.pid = NIL;
+  t.plen = 0;
   return t;
 }
 // LDS tree -> HBM records (links and colours; key, f, g and the payload are there already),
@@ -1551,7 +1645,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     // values below: the same code on the same inputs, prep_helper)
     int pe = -1;
     if constexpr (kPrep) {
-      if (gs == 16) pe = prep_find(*pr, cur.key, cur.x, cur.y, cur.h, cur.vmin, cur.ci, c.prep_epoch, lane);
+      if (gs == 16 && pr) pe = prep_find(*pr, cur.key, cur.x, cur.y, cur.h, cur.vmin, cur.ci, c.prep_epoch, lane);
     }
     float vm = 0.0f, sx = 0.0f, sy = 0.0f, sh = 0.0f, sg = 0.0f, dub = 0.0f, fc = 0.0f;
     int sbin = 0, scx = 0, scy = 0;
@@ -1622,7 +1716,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     const bool kept = lead && ((kPrep && pe >= 0) ? pkept : occv < c.thr);
     // hand the kept successors to the helper waves: the next pops are mostly among them
     if constexpr (kPrep) {
-      if (gs == 16) prep_post(*pr, kept, skey, sx, sy, sh, vm, lo + ca, c.prep_epoch, lane);
+      if (gs == 16 && pr) prep_post(*pr, kept, skey, sx, sy, sh, vm, lo + ca, c.prep_epoch, lane);
     }
     const uint64_t km = __ballot(kept);
     c.succ += __popcll(km);
@@ -1737,7 +1831,7 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
 #endif
   unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   apf_stage(P, apfs, lane);
-  if constexpr (kWide) {  // a new epoch of the helper waves' prep table: this planner, its map and APF list
+  if (kWide && pr) {  // a new epoch of the helper waves' prep table: this planner, its map and APF list
     c.prep_epoch += 1u;  // the main wave alone writes the epoch (and pidx, before the call): it counts its searches
     if (lane == 0) {
       prep_st(&pr->epoch, c.prep_epoch);
@@ -2056,7 +2150,8 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void hastar_search_wide_kernel(
   __shared__ WideLdsT<CF> W;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = (int)(threadIdx.x & 63);
-  PrepL* pr = lp(&W.prep);
+  PrepL* const tbl = lp(&W.prep);
+  PrepL* pr = tbl;
   if (wv == 0) {
     for (int e = lane; e < PREP_E; e += 64) pr->state[e] = 0u;
     if (lane == 0) {
@@ -2066,10 +2161,12 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void hastar_search_wide_kernel(
     }
   }
   __syncthreads();  // the only workgroup barrier: helpers start on an initialised table
+  const bool prep_on = !(dbg & 4);  // HASTAR_WIDE_DBG bit 2: no helper waves (diagnostics)
   if (wv > 0) {
-    prep_helper(*pr, W.apfs, descs, wv, lane);
+    if (prep_on) prep_helper(*pr, W.apfs, descs, wv, lane);
     return;
   }
+  if (!prep_on) pr = nullptr;
   SearchCtx c;
   c.A = arenas + blockIdx.x;
   c.slot = arena_base + (int)blockIdx.x;
@@ -2083,7 +2180,7 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void hastar_search_wide_kernel(
     if ((int)blockIdx.x < n_planners) {
       const int pi = order[blockIdx.x];
       c.P = descs + pi;
-      if (lane == 0) pr->pidx = pi;
+      if (lane == 0) tbl->pidx = pi;
       search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, true, dbg, pr);
     }
   } else {
@@ -2100,14 +2197,14 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void hastar_search_wide_kernel(
       if (q >= n_planners) break;
       const int pi = order[q];
       c.P = descs + pi;
-      if (lane == 0) pr->pidx = pi;
+      if (lane == 0) tbl->pidx = pi;
       if (search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, false, dbg, pr)) break;
     }
   }
   if (c.lane == 0) {
     gp(A.gens)[0] = c.gen3;
     gp(A.gens)[1] = c.gen2;
-    prep_st(&pr->stop, 1u);  // the helpers leave their loop
+    prep_st(&tbl->stop, 1u);  // the helpers leave their loop
   }
 }
 
@@ -2750,7 +2847,8 @@ hipError_t launch_search(const PlannerDev* d_descs, int n, const SlotArena* d_ar
                      d_order, d_next, hard_pops, n_prio, arena_base, head_wgs);
   return hipGetLastError();
 }
-// HASTAR_WIDE_DBG (diagnostics): bit 0 keeps the latency kernel's outer tree in HBM
+// HASTAR_WIDE_DBG (diagnostics): bit 0 keeps the latency kernel's outer tree in HBM, bit 2
+// runs it without its helper waves
 static int wide_dbg() {
   const char* e = std::getenv("HASTAR_WIDE_DBG");
   return e ? std::atoi(e) : 0;
