@@ -329,6 +329,9 @@ def main():
         balance["pool"] = planners[0].slots()
         balance["split_launch_ms"] = dict(zip(("head_start", "head_end", "bulk_start", "bulk_end"),
                                               planners[0].split_ms()))
+        pool = balance["pool"]  # the library splits a batch over 4x the CU count (hastar_capi.cpp batch_shape)
+        split_launch = (os.environ.get("HASTAR_SPLIT", "1") != "0" and pool["head_cus"] > 0
+                        and B > 4 * (pool["resident_slots"] // max(pool["waves_per_cu"], 1)))
         timings = {"qids": np.asarray(qids), "pops": last.stats["pops"].copy(),
                    "astar_pops": last.stats["astar_pops"].copy(),
                    "warm": np.array([p.timing() for p in planners], dtype=np.float64)}
@@ -426,10 +429,18 @@ def main():
                           else "contiguous blocks",
             "roofline": {"bound": "latency", "roof": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                         "kernel": "hastar_search_kernel", "kernel_ms": avg_kernel_ms,
+                         "kernel": ("hastar_search_kernel + hastar_search_wide_kernel (split launch: the batch "
+                                    "kernel beside the latency kernel on the queue's head)" if split_launch
+                                    else "hastar_search_kernel"),
+                         "kernel_ms": avg_kernel_ms,
                          "alg_bytes_per_launch": float(np.mean(alg_bytes)),
-                         "note": "dependent per-wave round trips bound the search, not HBM bandwidth "
-                                 "(SQ/TCC counters in profiles/, DESIGN.md §4.1)"},
+                         "note": "kernel_ms: HIP events from the fork to the join of the launch; achieved = "
+                                 "SURVEY §8(d) algorithmic bytes of the whole batch / kernel_ms.  traffic: HBM bytes "
+                                 "per launch from a PMC pass (FETCH_SIZE/WRITE_SIZE, profiles/pmc_search_summary.json) "
+                                 "of the same batch with HASTAR_SPLIT=0 (the batch kernel alone: counter collection "
+                                 "serialises the split launch's two kernels), null unless its kernel-source hash "
+                                 "matches this build.  Dependent per-wave round trips bound the search, not HBM "
+                                 "bandwidth (SQ/TCC counters in profiles/, DESIGN.md §4.1)"},
         }
         if map_build:
             out["map_build"] = map_build
@@ -763,8 +774,8 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
             "tick_budget_ms": 50.0, "success_rate": oks / max(len(ids) * args.steps, 1), "setup_s_per_gpu": t_setup,
             "roofline": {"bound": "latency", "roof": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": None,
-                         "kernel": "hastar_search_kernel", "kernel_ms": avg_k,
-                         "alg_bytes_per_launch": float(np.mean(alg))},
+                         "kernel": "hastar_search_wide_kernel (the latency kernel: one search per CU)",
+                         "kernel_ms": avg_k, "alg_bytes_per_launch": float(np.mean(alg))},
         }
         if rx["kernel_ms"]:
             out["relaxed_mode"] = {

@@ -26,6 +26,7 @@ ap.add_argument("--cfg5-pairs", type=int, nargs="*", default=None,
                 help="profile cfg5 replan loops instead (pair ids, bench.py --workload cfg5): every tick's search, "
                      "summed over --ticks ticks (the latency kernel)")
 ap.add_argument("--ticks", type=int, default=6)
+ap.add_argument("--skip-ticks", type=int, default=0, help="cfg5: run but do not sum the first ticks (cold memo)")
 args = ap.parse_args()
 names = ["pop", "expand", "open_bookkeeping", "astar", "shot", "reconstruct", "loop", "astar_hbm_mode"]
 def cfg5_runs(pair):
@@ -47,13 +48,15 @@ def runs():
     if args.cfg5_pairs is not None:
         for pair in args.cfg5_pairs:
             tot, stt, mss = None, None, 0.0
-            for p, st, ms in cfg5_runs(pair):
+            for t, (p, st, ms) in enumerate(cfg5_runs(pair)):
+                if t < args.skip_ticks:
+                    continue
                 cyc = p.cycles()
                 tot = list(cyc) if tot is None else [a + b for a, b in zip(tot, cyc)]
                 stt = dict(st) if stt is None else {k: stt[k] + st[k] if isinstance(st[k], int) and k not in
                                                     ("pop_digest", "closed_digest", "status") else st[k] for k in st}
                 mss += ms
-            yield f"cfg5 pair {pair} x {args.ticks} ticks", p, tot, stt, mss
+            yield f"cfg5 pair {pair} ticks {args.skip_ticks}..{args.ticks - 1}", p, tot, stt, mss
         return
     for s in args.seeds:
         gen = synthetic_ref if args.generator == "mt19937" else synthetic
@@ -87,6 +90,7 @@ for s, p, cyc, st, ms in runs():
                                                                  (32, "neighbour_loop"), (33, "lane_precompute"),
                                                                  (34, "replace_path"))},
                           astar_setup_per_search=round(cyc[35] / max(st["astar_searches"], 1)),
+                          prep={"taken": cyc[36], "computed_here": cyc[37]},
                           outer_per_pop={n: round(cyc[13 + i] / max(st["pops"], 1))
                                          for i, n in enumerate(["find3", "insert3", "unlink3", "succ_gen", "apf",
                                                                 "dubins", "insert_walk", "insert_link",

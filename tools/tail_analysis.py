@@ -20,6 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=23552)
 ap.add_argument("--steps", type=int, default=2)
 ap.add_argument("--clock", action="store_true", help="stamps build: shader clock of the searches under load")
+ap.add_argument("--dump", default=None, help="save every step's per-query {duration ms, slot} to this .npz")
 a = ap.parse_args()
 args = bench.parse_args(["--batch", str(a.batch)])
 if args.grid is None:
@@ -29,12 +30,16 @@ planners, _ = bench.build_planners(gpu, cfgs, 0)
 vels = [c[1]["vel"] for c in cfgs]
 starts = [c[1]["start"] for c in cfgs]
 bufs = gpu.BatchBuffers(planners, cap=8192)
+dumps = {}
 for step in range(a.steps):
     gpu.reset_batch(bufs)
     r = gpu.find_path_batch_arrays(planners, vels, starts, buffers=bufs)
     t = np.array([p.timing() for p in planners], dtype=np.float64)
     t0, t1 = t[:, 0].min(), t[:, 1].max()
     dur = (t[:, 1] - t[:, 0]) * 1e-5  # ms
+    dumps[f"dur{step}"] = dur
+    dumps[f"slot{step}"] = t[:, 2]
+    dumps[f"start{step}"] = (t[:, 0] - t[:, 0].min()) * 1e-5
     slots = len(set(int(s) for s in t[:, 2]))
     span = (t1 - t0) * 1e-5
     grid = np.linspace(t0, t1, 11)
@@ -60,3 +65,5 @@ for step in range(a.steps):
                       "sum_dur_ms": float(dur.sum()), "ideal_ms": float(dur.sum() / slots),
                       "busy_frac": float(dur.sum() / (slots * span)), "longest_ms": float(dur.max()),
                       "busy_slots_by_decile": busy}), flush=True)
+if a.dump:
+    np.savez(a.dump, **dumps)
