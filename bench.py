@@ -284,12 +284,13 @@ def main():
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     r0 = step()
+    cold_s = time.perf_counter() - t0
     progress("cold first step done")
     # the first step's outcome of a stratified sample (every 64th query and the 8 with the most
     # pops), paths included, for the bit-exact check against the oracle after the timed region
+    # (host-side bookkeeping of the bench, outside the step's time)
     strat = sorted(set(range(0, B, 64)) | set(np.argsort(-r0.stats["pops"], kind="stable")[:8].tolist()))
     cold_sample = {i: r0.result(i) for i in strat} if (rank == 0 and not args.no_cpu_baseline) else None
-    cold_s = time.perf_counter() - t0
     cold_pops = int(r0.stats["pops"].sum())
     cold_s, cold_pops_all = reduce_over_ranks(dist, cold_s, cold_pops, f"cuda:{device}")
     for _ in range(max(args.warmup - 1, 0)):

@@ -420,8 +420,11 @@ __device__ __forceinline__ float apf_field(const PlannerDev& P, const ApfStage& 
 // half-width r + apf_reach around it misses (cx, cy) cannot pass the exact pre-test of any
 // successor: the obstacle list is culled once, then lanes run over (candidate, kept
 // obstacle) pairs, and every successor's in-radius terms are summed in obstacle order.
-__device__ __forceinline__ float apf_fused_k(const PlannerDev& P, const ApfStage& S, ApfCand* __restrict__ kept, float cx,
-                                             float cy, float sx, float sy, float sh, uint64_t cmask, int gs, int lane) {
+// kStageKept: the cull list is the stage's own (S.kept); else `kept_arg` (a helper wave's)
+template <bool kStageKept>
+__device__ __forceinline__ float apf_fused_t(const PlannerDev& P, ApfStage& S, ApfCand* kept_arg, float cx, float cy,
+                                             float sx, float sy, float sh, uint64_t cmask, int gs, int lane) {
+  ApfCand* __restrict__ kept = kStageKept ? S.kept : kept_arg;
   float fc = 0.0f;
   if (cmask == 0) return fc;
   int C = APF_MAXC + 1;
@@ -486,10 +489,14 @@ __device__ __forceinline__ float apf_fused_k(const PlannerDev& P, const ApfStage
   wave_lds_sync();
   return fc;
 }
-// the same with the stage's own cull buffer (a helper wave of the latency kernel brings its own)
 __device__ __forceinline__ float apf_fused(const PlannerDev& P, ApfStage& S, float cx, float cy, float sx, float sy,
                                            float sh, uint64_t cmask, int gs, int lane) {
-  return apf_fused_k(P, S, S.kept, cx, cy, sx, sy, sh, cmask, gs, lane);
+  return apf_fused_t<true>(P, S, nullptr, cx, cy, sx, sy, sh, cmask, gs, lane);
+}
+// the same with a cull buffer of the caller's (a helper wave of the latency kernel brings its own)
+__device__ __forceinline__ float apf_fused_k(const PlannerDev& P, ApfStage& S, ApfCand* kept, float cx, float cy,
+                                             float sx, float sy, float sh, uint64_t cmask, int gs, int lane) {
+  return apf_fused_t<false>(P, S, kept, cx, cy, sx, sy, sh, cmask, gs, lane);
 }
 
 // Dubins.cpp:326-563 sampling of the chosen word, wave-parallel (64 samples per step).

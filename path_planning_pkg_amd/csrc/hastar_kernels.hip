@@ -1095,7 +1095,7 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, OT& o3, const Succ& s, flo
 // of the batch's longest at 9,414; when the pool cannot take one more pop the tree moves to
 // the HBM records (same indices: only links and colours are copied) and the search continues
 // behind the register cache (RBT<CachedAcc3>).
-constexpr int OUTER_LDS_CAP = 5056;  // (5504 before round 4: the helper waves' prep table took the rest)
+constexpr int OUTER_LDS_CAP = 4688;  // (5504 before round 4: the helper waves' prep table took the rest)
 struct alignas(16) Q3L {
   uint32_t key;
   float f;
@@ -1243,11 +1243,12 @@ struct LdsAcc3 {
   }
   __device__ __forceinline__ void reset_cache() { plen = 0; }
   // the popped node: key/f/links from LDS, the payload from its HBM record
-  __device__ __forceinline__ Node3 node(int x) const {
+  __device__ __forceinline__ Node3 node(int x) const { return node_q(x, quad(x)); }
+  // the same with its quad already read (the pop issues its closed-set probe in between)
+  __device__ __forceinline__ Node3 node_q(int x, const Quad& a) const {
     typedef int v4 __attribute__((ext_vector_type(4)));
     const GAS v4* h = (const GAS v4*)&t[x];
     const v4 b = h[1], d = h[2];
-    const Quad a = quad(x);
     Node3 n;
     n.key = a.key;
     n.f = a.f;
@@ -1326,7 +1327,7 @@ __device__ __forceinline__ bool lds_outer_load(SearchCtx& c, OuterLds& ol, int l
 // seq << 2 | phase, phase 0 = empty / being written by the main wave, 1 = posted, 2 = a helper
 // computes it, 3 = done.  The main wave overwrites only entries that no helper holds (a CAS to
 // phase 0); a helper claims a posted entry by CAS 1 -> 2 and alone moves it 2 -> 3.
-constexpr int PREP_E = 32;   // entries (the latest requests; cfg5 pops: 78 % of nodes were inserted within the last 32)
+constexpr int PREP_E = 64;   // entries, one per lane (the latest requests: with 32, 77 % of cfg5's warm pops found theirs)
 constexpr int PREP_C = 4;    // candidates per entry: action windows of at most 4 (16-lane groups)
 constexpr int PREP_HELPERS = 3;
 struct alignas(16) PrepIn {  // the inputs of one expansion
@@ -1422,7 +1423,7 @@ __device__ __forceinline__ void prep_post(PrepL& pr, bool post, uint32_t skey, f
 
 // helper wave h (1..3): claim the newest posted expansion, compute it, publish it; returns when
 // the main wave has set `stop`
-__device__ void prep_helper(PrepL& pr, const ApfStage& apfs, const PlannerDev* __restrict__ descs, int h, int lane) {
+__device__ void prep_helper(PrepL& pr, ApfStage& apfs, const PlannerDev* __restrict__ descs, int h, int lane) {
   ApfCand* kept_buf = (ApfCand*)pr.kept[h - 1];
   for (;;) {
     const int e = lane & (PREP_E - 1);
@@ -1560,12 +1561,22 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     }
     STAMP_T tp = STAMP_NOW();
     const int b = o3.begin();
-    const Node3 top = o3.node(b);  // usually cached: the leftmost node was touched by the last walks
     // the closed-set probe is issued first; its HBM latency overlaps the erase, which
     // does not depend on it (HybridAStar.cpp:109-111 order is kept: the insert itself
-    // reads the popped node's fields, captured in `top`)
+    // reads the popped node's fields, captured in `top`).  HBM tree: the node is usually
+    // cached (the leftmost node was touched by the last walks).  LDS tree: the key comes from
+    // LDS, so the probe and the payload's HBM read are in flight together.
     uint32_t ph;
-    const v2u p0 = closed3_probe(c, top.key, &ph);
+    v2u p0;
+    Node3 top;
+    if constexpr (kLdsOuter) {
+      const Quad tq = o3.quad(b);
+      p0 = closed3_probe(c, tq.key, &ph);
+      top = o3.node_q(b, tq);
+    } else {
+      top = o3.node(b);
+      p0 = closed3_probe(c, top.key, &ph);
+    }
     o3.unlink(b);
     tpool_free(o3, c.ps3, b);
     bool fresh;
@@ -1646,6 +1657,9 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     int pe = -1;
     if constexpr (kPrep) {
       if (gs == 16 && pr) pe = prep_find(*pr, cur.key, cur.x, cur.y, cur.h, cur.vmin, cur.ci, c.prep_epoch, lane);
+#ifdef HASTAR_STAMPS
+      if (gs == 16 && pr) c.cyc[pe >= 0 ? 36 : 37]++;  // prepared expansions taken / computed here
+#endif
     }
     float vm = 0.0f, sx = 0.0f, sy = 0.0f, sh = 0.0f, sg = 0.0f, dub = 0.0f, fc = 0.0f;
     int sbin = 0, scx = 0, scy = 0;
@@ -1898,9 +1912,12 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
   float cost = FLT_MAX;
   // the planner's outer capacity after `parks` resumes (4x each), bounded by this arena: a
   // search parks at the same pop whatever arena the pool happens to hand it
-  // (a head arena sized for the planner's known longest search, pops_grant, lifts it: hastar_capi.cpp head_arenas)
-  const long long pcap = min(max((long long)P.arena_pops << (2 * min(parks, 12)), (long long)A.pops_grant),
-                             (long long)SLOT3_IDX_MASK - 1);
+  // (on the latency kernel, a head arena sized for the planner's known longest search, pops_grant,
+  // lifts it: hastar_capi.cpp head_acquire.  Only that kernel gets head arenas; the batch kernel's
+  // code stays as it was: an unused branch there moved its register allocation and cost 4 %)
+  long long prule = (long long)P.arena_pops << (2 * min(parks, 12));
+  if constexpr (kWide) prule = max(prule, (long long)A.pops_grant);
+  const long long pcap = min(prule, (long long)SLOT3_IDX_MASK - 1);
   const int closed_lim = (int)min((long long)A.closed3_cap, pcap + 1);
   const int open_lim = (int)min((long long)A.open3_cap, 2 + (long long)(P.span_alloc - 1) * pcap + 64);
   STAMP_T tloop = STAMP_NOW();
@@ -1960,7 +1977,8 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
       R->ps3_free = c.ps3.free;
       // the next capacity step beyond this arena's (a head arena's grant may exceed several)
       int np = parks + 1;
-      while (np < 12 && ((long long)P.arena_pops << (2 * np)) <= pcap) ++np;
+      if constexpr (kWide)
+        while (np < 12 && ((long long)P.arena_pops << (2 * np)) <= pcap) ++np;
       R->parks = np;
       R->park_arena = c.slot;
       R->ok = 0;

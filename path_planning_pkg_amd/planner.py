@@ -478,8 +478,12 @@ class BatchBuffers:
         n = len(planners)
         self.n, self.cap = n, cap
         self.hs = (C.c_void_p * n)(*[p.h.value for p in planners])
-        self.xyh = np.empty((n, cap, 3), np.float32)
-        self.curv = np.empty((n, cap), np.float32)
+        # zero-filled here, so that their pages are mapped once at set-up, not at a first call's
+        # path copies (np.empty maps nothing until the first write)
+        self.xyh = np.zeros((n, cap, 3), np.float32)
+        self.xyh.fill(0.0)
+        self.curv = np.zeros((n, cap), np.float32)
+        self.curv.fill(0.0)
         self.ln = np.zeros(n, np.int32)
         self.ok = np.zeros(n, np.int32)
         self.cost = np.zeros(n, np.float32)
