@@ -105,8 +105,9 @@ int hastar_reset_batch(const hastar_handle* hs, int n);
 /* Scheduling hint (no counterpart in the reference): the planner's expected search cost, the
  * key of the longest-first order of its next batched find_path (larger first; equal keys keep
  * the caller's order; units: 10-ns ticks of expected search time).  After every exact search the
- * library sets it to that search's duration; 0 (a fresh planner) = unknown: the planner is then keyed by its last boxes' distances to the straight start-goal
- * route.  Results never depend on it, only the order in
+ * library keys the planner by the longer of its last two search durations (a hint set here counts
+ * alone until the next search); 0 (a fresh planner) = unknown: the planner is then keyed by its
+ * last boxes' distances to the straight start-goal route.  Results never depend on it, only the order in
  * which a batch's searches start and, for a large batch, which of them run on the latency
  * CUs. */
 int hastar_set_cost_hint(hastar_handle h, long long hint);

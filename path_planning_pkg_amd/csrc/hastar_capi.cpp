@@ -580,6 +580,8 @@ struct hastar_handle_s {
   SearchResult last{};
   bool have_last = false;
   long long last_pops = 0;      // work estimate for longest-first scheduling (last search's duration)
+  long long prev_pops = 0;      // the one before (the key is the longer of the two: a replan loop
+                                // whose long searches alternate with short ones stays at the head)
   std::vector<float> boxes_w;   // the last update_obstacles(boxes) call's boxes (world frame): cold-order key
   int row0 = 0, row1 = 0;       // map-build row window [row0, row1) (hastar_set_row_window); [0, N) by default
   std::shared_ptr<struct BatchSlab> batch;  // planners of one hastar_create_batch_f32 share it
@@ -1014,6 +1016,7 @@ int hastar_reset(hastar_handle h) {
 int hastar_set_cost_hint(hastar_handle h, long long hint) {
   if (!h) return fail(HASTAR_EINVAL, "null handle");
   h->last_pops = hint;
+  h->prev_pops = 0;
   return HASTAR_OK;
 }
 
@@ -1803,6 +1806,7 @@ static int finish_batch(DeviceCtx& DC, const hastar_handle* hs, int n, float* xy
     // pops, inner A* pops and shots by what they cost where the search ran.  (A schedule-free
     // work key, 1566 x pops + 1058 x inner pops from a fit of the cfg3 durations, settled the
     // steps at 3.03 s against 2.74 s: profiles/r03h_bench_long.json; HASTAR_LPT_WORK=1.)
+    if (lpt) h->prev_pops = h->last_pops;
     if (lpt) h->last_pops = (lpt_work_key() || R.t_end <= R.t_start)
                                 ? 1 + 1566LL * (long long)R.pops + 1058LL * (long long)R.astar_pops
                                 : (long long)(R.t_end - R.t_start);
@@ -1923,7 +1927,9 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   std::vector<long long> key(n);
   int n_cold = 0;
   for (int i = 0; i < n; ++i) {
-    key[i] = hs[i]->last_pops;
+    // the longer of the planner's last two searches (cfg4's longest queries alternate long and
+    // short replans; keyed by the last one alone, a long one ran in the bulk and parked there)
+    key[i] = hs[i]->last_pops > 0 ? std::max(hs[i]->last_pops, hs[i]->prev_pops) : 0;
     n_cold += key[i] <= 0;
   }
   if (n_cold > 0)
