@@ -30,7 +30,9 @@ def trace(args):
     disp = [r for r in kt if KERNEL in r["Kernel_Name"]]
     disp.sort(key=lambda r: int(r["Start_Timestamp"]))
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in disp]
-    timed = durs[args.warmup: args.warmup + args.steps]
+    # hastar_reserve's empty warm-up launch (every wave exits at its first queue read) is not a step
+    steps = [d for d in durs if d >= 1.0]
+    timed = steps[args.warmup: args.warmup + args.steps]
     stats = rows(args.dir, "kernel_stats.csv")
     out = {"kernel": KERNEL, "dispatches_ms": durs, "timed_dispatches_ms": timed,
            "timed_mean_ms": sum(timed) / len(timed) if timed else None,
