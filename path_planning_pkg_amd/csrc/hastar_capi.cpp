@@ -229,6 +229,7 @@ struct DeviceCtx {
   void* head_slab = nullptr;      // the own allocation
   long long head_grant = 0;       // their outer capacity in pops (SlotArena::pops_grant)
   long long head_want = 0;        // pops of the longest search that parked in a split launch
+  int head_extra = 0;             // latency CUs added to the head: searches that parked in a split launch
   SlotArena* d_head = nullptr;    // their descriptors (head_n); the head kernel's slot ids start at n_arenas
   std::vector<SlotArena> h_head;
   SlotArena* d_resume = nullptr;  // arena descriptors of a resume launch
@@ -507,7 +508,7 @@ int head_release(DeviceCtx& D) {
 
 // Head arenas for a split launch with `head` latency CUs, each holding a search of head_want
 // pops (+25 %): an own allocation when the HBM keeps kHeadroom beside it, else k consecutive
-// pool arenas each, while at most a quarter of the launch's `slots` arenas go to them.  None
+// pool arenas each, while at most a third of the launch's `slots` arenas go to them.  None
 // when no search needs them or neither way has the room.
 int head_acquire(DeviceCtx& D, int head, int span, int slots) {
   // (a parked search outgrew its planner's capacity rule, P.arena_pops << 2 parks, whatever
@@ -529,7 +530,7 @@ int head_acquire(DeviceCtx& D, int head, int span, int slots) {
   } else {
     D.head_slab = nullptr;
     k = (int)((each + D.arena_bytes - 1) / D.arena_bytes);
-    if ((long long)head * k > slots / 4) return 0;  // the bulk would lose too many arenas
+    if ((long long)head * k > slots / 3) return 0;  // the bulk would lose too many arenas
   }
   D.h_head.assign((size_t)head, SlotArena{});
   for (int b = 0; b < head; ++b) {
@@ -1713,7 +1714,11 @@ static BatchShape batch_shape(const DeviceCtx& DC, int n) {
   // HASTAR_SPLIT=0/1 forces it off/on.
   b.split = !b.wide && DC.head_cus > 0 && n > 4 * DC.n_cu;
   if (const char* e = std::getenv("HASTAR_SPLIT")) b.split = !b.wide && DC.head_cus > 0 && std::atoi(e) != 0;
-  b.head = b.split ? std::min(DC.head_cus, n) : 0;
+  // the head grows by the searches that parked in the last split launch (they get head arenas
+  // and a CU each from the start: cfg4's > 262 k-pop replans), up to one CU in 8
+  // (only for a batch many times the CU count: a forced split of a small batch keeps head_cus)
+  const int extra = n > 4 * DC.n_cu ? DC.head_extra : 0;
+  b.head = b.split ? std::min(std::min(DC.head_cus + extra, DC.n_cu / 8), n) : 0;
   b.per_cu = DC.resident_slots / DC.n_cu;  // batch-kernel waves per CU
   b.W = std::max(1, std::min(n, b.wide ? DC.n_cu : b.split ? b.head + (DC.n_cu - b.head) * b.per_cu
                                                            : DC.resident_slots));
@@ -2165,9 +2170,16 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
     }
   }
   // a search that parked in a split launch sizes the next split launches' head arenas
-  if (split1)
+  if (split1) {
+    int parked = 0;
     for (int i = 0; i < n; ++i)
-      if (DC.h_results[i].parks > 0) DC.head_want = std::max(DC.head_want, DC.h_results[i].pops);
+      if (DC.h_results[i].parks > 0) {
+        DC.head_want = std::max(DC.head_want, DC.h_results[i].pops);
+        ++parked;
+      }
+    // searches that parked outside the head: the next split launch widens its head by as many
+    if (parked > 0) DC.head_extra = std::max(DC.head_extra, std::min(parked, DC.n_cu / 8));
+  }
   g_last_ms = ms_total;
   return finish_batch(DC, hs, n, xyh, curv, cap, len, cost, ok, stats, true);
 }
