@@ -1248,7 +1248,11 @@ struct LdsAcc3 {
   __device__ __forceinline__ Node3 node_q(int x, const Quad& a) const {
     typedef int v4 __attribute__((ext_vector_type(4)));
     const GAS v4* h = (const GAS v4*)&t[x];
-    const v4 b = h[1], d = h[2];
+    return node_pv(a, h[1], h[2]);
+  }
+  // ... and with its payload quads already loaded (PopPrefetch)
+  template <class V4>
+  __device__ __forceinline__ Node3 node_pv(const Quad& a, const V4& b, const V4& d) const {
     Node3 n;
     n.key = a.key;
     n.f = a.f;
@@ -1516,6 +1520,18 @@ __device__ void prep_helper(PrepL& pr, ApfStage& apfs, const PlannerDev* __restr
 // its pool or the closed records are about to fill; the caller moves the tree to HBM and
 // continues there, at the same pop).
 constexpr int LOOP_DONE = 0, LOOP_PARKED = 1, LOOP_MIGRATE = 2;
+// Latency kernel, LDS tree: right after a pop, the HBM reads of the NEXT pop (the payload of the
+// tree's new leftmost node and its closed-set probe) are issued, so they arrive during the
+// expansion.  The next pop takes them when its node is that one (no successor went before it,
+// and the node was not freed in between); the closed set only changes at pops, so the probe
+// is still current.
+struct PopPrefetch {
+  typedef int v4 __attribute__((ext_vector_type(4)));
+  int idx;     // node index, NIL = none
+  uint32_t ph; // its closed-set hash slot
+  v2u probe;   // the slot's {key, gen | idx}
+  v4 b, d;     // payload quads 1 and 2 of open3[idx]
+};
 struct LoopState {
   int counter, interval;
   bool shot_allowed;
@@ -1544,6 +1560,12 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
   const GoalC GC = goal_centres(r, P.goal_x, P.goal_y, P.goal_h);
   const int span = 2 * P.na + 1;
   const int open_lim_t = kLdsOuter ? min(open_lim, open_cap) : open_lim;
+  PopPrefetch pf;
+  pf.idx = NIL;
+  pf.ph = 0u;
+  pf.probe = v2u{0u, 0u};
+  pf.b = PopPrefetch::v4{0, 0, 0, 0};
+  pf.d = pf.b;
   // lanes per candidate action: 16 when the window has at most 4 actions (the Dubins
   // libm calls then spread over the group), else 4 (one Dubins word per lane)
 #ifdef HASTAR_DBG_NARROW
@@ -1571,8 +1593,18 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     Node3 top;
     if constexpr (kLdsOuter) {
       const Quad tq = o3.quad(b);
-      p0 = closed3_probe(c, tq.key, &ph);
-      top = o3.node_q(b, tq);
+      if (b == pf.idx) {
+        ph = pf.ph;
+        p0 = pf.probe;
+        top = o3.node_pv(tq, pf.b, pf.d);
+      } else {
+        p0 = closed3_probe(c, tq.key, &ph);
+        top = o3.node_q(b, tq);
+      }
+#ifdef HASTAR_STAMPS
+      if (b == pf.idx) c.cyc[38]++;  // pops served by the prefetch
+      else c.cyc[39]++;
+#endif
     } else {
       top = o3.node(b);
       p0 = closed3_probe(c, top.key, &ph);
@@ -1599,6 +1631,18 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     c.pops++;
     const int cx = key3_x(cur.key), cy = key3_y(cur.key), cbin = key3_bin(cur.key);
     dig = mix64(dig ^ digest_key(cur.key)) + (uint64_t)fbits(cur.g);
+    if constexpr (kLdsOuter) {
+      const int b2 = o3.begin();
+      pf.idx = NIL;
+      if (b2 != 0) {
+        typedef int v4 __attribute__((ext_vector_type(4)));
+        pf.probe = closed3_probe(c, o3.K(b2), &pf.ph);
+        const GAS v4* h2 = (const GAS v4*)&c.open3[b2];
+        pf.b = h2[1];
+        pf.d = h2[2];
+        pf.idx = b2;
+      }
+    }
     STAMP_ADD(0, tp);
     // goal test: Node3D::operator== compares the cell only (Node3D.h:42)
     if (cx == P.goal_cx && cy == P.goal_cy) {
@@ -1658,7 +1702,8 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     if constexpr (kPrep) {
       if (gs == 16 && pr) pe = prep_find(*pr, cur.key, cur.x, cur.y, cur.h, cur.vmin, cur.ci, c.prep_epoch, lane);
 #ifdef HASTAR_STAMPS
-      if (gs == 16 && pr) c.cyc[pe >= 0 ? 36 : 37]++;  // prepared expansions taken / computed here
+      if (gs == 16 && pr && pe >= 0) c.cyc[36]++;  // prepared expansions taken
+      if (gs == 16 && pr && pe < 0) c.cyc[37]++;   // computed here
 #endif
     }
     float vm = 0.0f, sx = 0.0f, sy = 0.0f, sh = 0.0f, sg = 0.0f, dub = 0.0f, fc = 0.0f;
@@ -1797,6 +1842,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
           STAMP_T tu3 = STAMP_NOW();
           o3.unlink(hit);
           tpool_free(o3, c.ps3, hit);
+          if (kLdsOuter && hit == pf.idx) pf.idx = NIL;  // its index may be reused by the insert
           STAMP_ADD(15, tu3);
         }
         // AStar::find_path(int, int): a memo hit probed above is still valid while no

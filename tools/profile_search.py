@@ -91,6 +91,7 @@ for s, p, cyc, st, ms in runs():
                                                                  (34, "replace_path"))},
                           astar_setup_per_search=round(cyc[35] / max(st["astar_searches"], 1)),
                           prep={"taken": cyc[36], "computed_here": cyc[37]},
+                          pop_prefetch={"hit": cyc[38], "miss": cyc[39]},
                           outer_per_pop={n: round(cyc[13 + i] / max(st["pops"], 1))
                                          for i, n in enumerate(["find3", "insert3", "unlink3", "succ_gen", "apf",
                                                                 "dubins", "insert_walk", "insert_link",
