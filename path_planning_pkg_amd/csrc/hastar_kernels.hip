@@ -1055,16 +1055,24 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLdsT<CF>& L, int s
 // std::set<Node3D>::insert (HybridAStar.cpp:173, 191) into the outer open tree (HBM nodes
 // behind the register cache, or the LDS tree of the latency kernel; the full 48-B record
 // always goes to the arena's open3[n], the LDS tree keeps key/f/g/links of its nodes).
+// where: optional {new node (NIL when the insert was dropped), parent, insert_left}
 template <class OT>
-__device__ __forceinline__ bool insert3(SearchCtx& c, OT& o3, const Succ& s, float f, int prev, int cap) {
+__device__ __forceinline__ bool insert3(SearchCtx& c, OT& o3, const Succ& s, float f, int prev, int cap,
+                                        int* where = nullptr) {
   bool left;
   const uint32_t key = key3(s.cx, s.cy, s.bin);
   STAMP_T tw = STAMP_NOW();
   const int pos = o3.insert_pos(key, f, &left);
   STAMP_ADD(19, tw);
+  if (where) where[0] = NIL;
   if (pos == -2) return true;
   const int n = tpool_alloc(o3, c.ps3, cap);
   if (n == NIL) return false;
+  if (where) {
+    where[0] = n;
+    where[1] = pos;
+    where[2] = left ? 1 : 0;
+  }
   Node3 d;
   d.key = key;
   d.f = f;
@@ -1560,12 +1568,15 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
   const GoalC GC = goal_centres(r, P.goal_x, P.goal_y, P.goal_h);
   const int span = 2 * P.na + 1;
   const int open_lim_t = kLdsOuter ? min(open_lim, open_cap) : open_lim;
-  PopPrefetch pf;
+  PopPrefetch pf, pi;  // issued after the pop / by an insert that became the leftmost
+  int pf_lm = 0;       // the LDS tree's leftmost node during an expansion (0: empty)
+  bool pi_issued = false;
   pf.idx = NIL;
   pf.ph = 0u;
   pf.probe = v2u{0u, 0u};
   pf.b = PopPrefetch::v4{0, 0, 0, 0};
   pf.d = pf.b;
+  pi = pf;
   // lanes per candidate action: 16 when the window has at most 4 actions (the Dubins
   // libm calls then spread over the group), else 4 (one Dubins word per lane)
 #ifdef HASTAR_DBG_NARROW
@@ -1593,7 +1604,11 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     Node3 top;
     if constexpr (kLdsOuter) {
       const Quad tq = o3.quad(b);
-      if (b == pf.idx) {
+      if (b == pi.idx) {
+        ph = pi.ph;
+        p0 = pi.probe;
+        top = o3.node_pv(tq, pi.b, pi.d);
+      } else if (b == pf.idx) {
         ph = pf.ph;
         p0 = pf.probe;
         top = o3.node_pv(tq, pf.b, pf.d);
@@ -1602,9 +1617,11 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
         top = o3.node_q(b, tq);
       }
 #ifdef HASTAR_STAMPS
-      if (b == pf.idx) c.cyc[38]++;  // pops served by the prefetch
+      if (b == pi.idx || b == pf.idx) c.cyc[38]++;  // pops served by a prefetch
       else c.cyc[39]++;
 #endif
+      pi.idx = NIL;
+      pi_issued = false;
     } else {
       top = o3.node(b);
       p0 = closed3_probe(c, top.key, &ph);
@@ -1634,6 +1651,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     if constexpr (kLdsOuter) {
       const int b2 = o3.begin();
       pf.idx = NIL;
+      pf_lm = b2;  // the leftmost (0: empty tree)
       if (b2 != 0) {
         typedef int v4 __attribute__((ext_vector_type(4)));
         pf.probe = closed3_probe(c, o3.K(b2), &pf.ph);
@@ -1843,6 +1861,8 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
           o3.unlink(hit);
           tpool_free(o3, c.ps3, hit);
           if (kLdsOuter && hit == pf.idx) pf.idx = NIL;  // its index may be reused by the insert
+          if (kLdsOuter && hit == pi.idx) pi.idx = NIL;
+          if (kLdsOuter && hit == pf_lm) pf_lm = o3.begin();
           STAMP_ADD(15, tu3);
         }
         // AStar::find_path(int, int): a memo hit probed above is still valid while no
@@ -1859,7 +1879,31 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
         STAMP_ADD(3, ta);
         const float f = s.g + stl_max(h1, s.dub);
         STAMP_T ti3 = STAMP_NOW();
-        if (!insert3(c, o3, s, f, ci, open_cap)) { fail = true; break; }
+        if constexpr (kLdsOuter) {
+          int wh[3];
+          if (!insert3(c, o3, s, f, ci, open_cap, wh)) { fail = true; break; }
+          // the new node became the leftmost (attached as the left child of the leftmost):
+          // it is the next pop unless a later successor goes before it, so its closed-set
+          // probe is issued now and its payload is the record just written
+          // (its own registers: overwriting a load's destination while it is in flight would
+          // wait for it; a second new leftmost in one expansion only invalidates the first)
+          if (wh[0] != NIL && wh[2] && wh[1] == pf_lm) {
+            pf_lm = wh[0];
+            if (!pi_issued) {
+              typedef int v4 __attribute__((ext_vector_type(4)));
+              pi_issued = true;
+              pi.idx = wh[0];
+              pi.probe = closed3_probe(c, key, &pi.ph);
+              pi.b = v4{wh[1], (int)((uint32_t)RB_RED | ((uint32_t)s.ci << 8)), __float_as_int(s.g),
+                        __float_as_int(s.vmin)};
+              pi.d = v4{__float_as_int(s.x), __float_as_int(s.y), __float_as_int(s.h), ci};
+            } else {
+              pi.idx = NIL;
+            }
+          }
+        } else {
+          if (!insert3(c, o3, s, f, ci, open_cap)) { fail = true; break; }
+        }
         STAMP_ADD(14, ti3);
       }
       if (c.status != 0) break;
