@@ -82,6 +82,20 @@ def test_f64_synthetic_matches_oracle(N, bins, K, seed):
     print(f"N={N} seed={seed} bit-identical:", exact)
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_f64_cfg3_queries_match_oracle(seed):
+    """cfg3 size (1024x1024x72, K = 200; bench queries 0-2): the double search is a search of its
+    own (other pop counts than the float one) and must still equal the oracle's double one."""
+    cfg, proto = synthetic_ref(1024, 72, 200, seed)
+    proto = _proto64(proto)
+    g, o = _pair(cfg)
+    drive(g, proto)
+    drive(o, proto)
+    exact = []
+    _compare(g.find_path(proto["vel"], proto["start"]), o.find_path(proto["vel"], proto["start"]), g, o, exact)
+    print(f"cfg3 seed {seed} bit-identical:", exact)
+
+
 def test_f64_arena_growth_reruns_give_the_same_result():
     """Tiny arenas: the search stops, the memo is restored and it re-runs in 4x arenas until it
     fits (no limit, HybridAStar.cpp:107): the result equals the oracle's and a default run's."""
