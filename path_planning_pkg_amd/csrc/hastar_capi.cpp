@@ -228,8 +228,15 @@ struct DeviceCtx {
   int head_k = 0, head_n = 0;     // head_k: pool arenas per carved head arena (0: own allocation)
   void* head_slab = nullptr;      // the own allocation
   long long head_grant = 0;       // their outer capacity in pops (SlotArena::pops_grant)
-  long long head_want = 0;        // pops of the longest search that parked in a split launch
-  int head_extra = 0;             // latency CUs added to the head: searches that parked in a split launch
+  long long head_want = 0;        // pops of the longest search that outgrew its plain arena (windowed max)
+  int head_extra = 0;             // latency CUs added to the head: such searches (windowed max)
+  // the last kHeadWindow split launches' {longest outgrowing search, number of them}: head_want
+  // and head_extra are their maxima, so a workload change lets the head shrink back
+  long long head_win_pops[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int head_win_cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int head_win_at = 0;
+  ArenaReq head_req;              // the requirement the head arenas were carved for
+  int head_span = 0;
   SlotArena* d_head = nullptr;    // their descriptors (head_n); the head kernel's slot ids start at n_arenas
   std::vector<SlotArena> h_head;
   SlotArena* d_resume = nullptr;  // arena descriptors of a resume launch
@@ -446,10 +453,12 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
   D.slab = nullptr;
   D.d_arenas = nullptr;
   D.n_arenas = 0;
-  if (D.head_k > 0) {  // head arenas carved from the old slab
-    D.head_k = D.head_n = 0;
-    D.head_grant = 0;
-  }
+  // head arenas (carved from the old slab, or an own allocation sized for the old requirement)
+  // do not outlive the pool: the next split launch carves them again for the new one
+  if (D.head_slab) hipFree(D.head_slab);
+  D.head_slab = nullptr;
+  D.head_k = D.head_n = 0;
+  D.head_grant = 0;
   const ArenaLayout lay = arena_layout(r);
   const size_t per = lay.total();
   // memory budget of the pool: HASTAR_ARENA_MB, else HASTAR_ARENA_FRAC (default 0.8) of
@@ -515,7 +524,10 @@ int head_acquire(DeviceCtx& D, int head, int span, int slots) {
   // the pool arena's size: the grant lifts that rule in the head arenas, hastar_kernels.hip)
   if (D.head_want <= 0 || D.arena_bytes == 0) return head_release(D);
   const long long grant = std::min(D.head_want + D.head_want / 4, (long long)SLOT3_IDX_MASK - 1);
-  if (D.head_n == head && D.head_grant == grant) return 0;
+  // reuse the current head arenas only when they were carved for this pool's requirement (a
+  // larger grid or inner capacity that joined the device since rebuilt the pool, and a wider
+  // span needs more open nodes per pop)
+  if (D.head_n == head && D.head_grant == grant && D.head_req.covers(D.areq) && D.head_span >= span) return 0;
   if (int rc = head_release(D)) return rc;
   ArenaReq r = D.areq;
   size_outer(r, grant, span);
@@ -547,6 +559,8 @@ int head_acquire(DeviceCtx& D, int head, int span, int slots) {
   D.head_k = k;
   D.head_n = head;
   D.head_grant = grant;
+  D.head_req = r;
+  D.head_span = span;
   return 0;
 }
 
@@ -2171,14 +2185,26 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   }
   // a search that parked in a split launch sizes the next split launches' head arenas
   if (split1) {
-    int parked = 0;
+    // searches that outgrew their plain arena (parked, or ran through on a head arena's grant):
+    // the next split launches give the head arenas room for the longest of them and widen the
+    // head by their number, as long as one of the last kHeadWindow split launches had any
+    long long want = 0;
+    int big = 0;
     for (int i = 0; i < n; ++i)
-      if (DC.h_results[i].parks > 0) {
-        DC.head_want = std::max(DC.head_want, DC.h_results[i].pops);
-        ++parked;
+      if (DC.h_results[i].parks > 0 || DC.h_results[i].pops > (long long)hs[i]->max_pops) {
+        want = std::max(want, (long long)DC.h_results[i].pops);
+        ++big;
       }
-    // searches that parked outside the head: the next split launch widens its head by as many
-    if (parked > 0) DC.head_extra = std::max(DC.head_extra, std::min(parked, DC.n_cu / 8));
+    constexpr int kHeadWindow = 8;
+    DC.head_win_pops[DC.head_win_at] = want;
+    DC.head_win_cnt[DC.head_win_at] = std::min(big, DC.n_cu / 8);
+    DC.head_win_at = (DC.head_win_at + 1) % kHeadWindow;
+    DC.head_want = 0;
+    DC.head_extra = 0;
+    for (int w = 0; w < kHeadWindow; ++w) {
+      DC.head_want = std::max(DC.head_want, DC.head_win_pops[w]);
+      DC.head_extra = std::max(DC.head_extra, DC.head_win_cnt[w]);
+    }
   }
   g_last_ms = ms_total;
   return finish_batch(DC, hs, n, xyh, curv, cap, len, cost, ok, stats, true);

@@ -15,6 +15,9 @@
 #include <cfloat>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -123,13 +126,14 @@ int arena_alloc(hastar64_handle h) {
                bdc = al256((size_t)h->dub_cap * sizeof(double)), bch = al256((size_t)closed3 * sizeof(int)),
                bg = 256;
   const size_t total = b3 + bc + bs + b2 + bcell + bd + bdc + bch + bg;
+  // the new arena is allocated before the old one is freed: when it cannot be, the planner keeps
+  // its current arena and the device descriptor's pointers into it (the caller restores the caps)
+  void* fresh = nullptr;
+  if (hipMalloc(&fresh, total) != hipSuccess)
+    return fail64(HASTAR_EOVERFLOW, "search arena of " + std::to_string(total >> 20) + " MiB cannot be allocated");
   HIPCHK64(hipStreamSynchronize(h->st));
   if (h->arena) hipFree(h->arena);
-  h->arena = nullptr;
-  if (hipMalloc(&h->arena, total) != hipSuccess) {
-    h->arena = nullptr;
-    return fail64(HASTAR_EOVERFLOW, "search arena of " + std::to_string(total >> 20) + " MiB cannot be allocated");
-  }
+  h->arena = fresh;
   char* q = static_cast<char*>(h->arena);
   D.open3 = reinterpret_cast<Node3d*>(q); q += b3;
   D.open3_cap = (int)open3;
@@ -486,6 +490,7 @@ int hastar64_find_path(hastar64_handle h, double vel, const double start[3], dou
   *cost = DBL_MAX;
   *ok = 0;
   h->last_len = 0;
+  if (!h->arena) return fail64(HASTAR_ENOMEM, "the planner has no search arena");
   // Vector3D::get_rotated_vector (common.h:162-169) of the start relative to the goal
   const double rx = start[0] - h->goal3x, ry = start[1] - h->goal3y;
   const double c = std::cos(h->grid_heading), s = std::sin(h->grid_heading);
@@ -520,16 +525,18 @@ int hastar64_find_path(hastar64_handle h, double vel, const double start[3], dou
     if (!R.need) break;
     HIPCHK64(hipMemcpyAsync(D.nm_f, h->snap_f, NN * sizeof(double), hipMemcpyDeviceToDevice, h->st));
     HIPCHK64(hipMemcpyAsync(D.visited, h->snap_vis, vis_bytes, hipMemcpyDeviceToDevice, h->st));
-    if (R.need & NEED_OUTER) h->pops_cap *= 4;
+    const int was_pops = h->pops_cap, was_astar = h->astar_cap, was_dub = h->dub_cap;
+    if (R.need & NEED_OUTER) h->pops_cap = (int)std::min<long long>(4ll * h->pops_cap, 1ll << 30);
     if (R.need & NEED_INNER) h->astar_cap = (int)std::min<long long>(4ll * h->astar_cap, 1ll << 30);
     if (R.need & NEED_SHOT) h->dub_cap = (int)std::min<long long>(4ll * h->dub_cap, 1ll << 28);
     ++h->reruns;
     if (int rc = arena_alloc(h)) {  // no larger arena: the reference's failure pair, status EOVERFLOW
       status = rc;
-      // leave the planner usable: a default-size arena again
-      h->pops_cap = 65536;
-      h->astar_cap = (int)std::min<size_t>(NN + 16, 65536);
-      arena_alloc(h);
+      // the planner keeps its current arena (arena_alloc frees it only after a larger one is
+      // allocated), so it stays usable with the capacities that arena was carved for
+      h->pops_cap = was_pops;
+      h->astar_cap = was_astar;
+      h->dub_cap = was_dub;
       break;
     }
   }
@@ -591,6 +598,28 @@ int hastar64_copy_path(hastar64_handle h, double* xyh, double* curv, int cap, in
   return HASTAR_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// velocity-profile staging of one device (hastar_velocity_profile_batch_f64)
+struct VelStage64 {
+  std::mutex mu;
+  hipStream_t st = nullptr;
+  char* base = nullptr;
+  size_t cap = 0;
+};
+VelStage64& vel_stage64(int device) {
+  static std::mutex mu;
+  static std::map<int, std::unique_ptr<VelStage64>> all;
+  std::lock_guard<std::mutex> lk(mu);
+  std::unique_ptr<VelStage64>& p = all[device];
+  if (!p) p.reset(new VelStage64());
+  return *p;
+}
+}  // namespace
+
+extern "C" {
+
 // VelocityGenerator<double> (VelocityGenerator.cpp:7-84) over n paths, host buffers in and out
 int hastar_velocity_profile_batch_f64(int device, const hastar_velocity_params_f64* vp, int n, const long long* offsets,
                                       const double* xyh, const double* curv, const double* vel_init,
@@ -611,13 +640,20 @@ int hastar_velocity_profile_batch_f64(int device, const hastar_velocity_params_f
   const size_t b_off = al256((size_t)(n + 1) * 8), b_x = al256((size_t)pts * 3 * 8), b_c = al256((size_t)pts * 8),
                b_v = al256((size_t)n * 8), b_f = al256((size_t)n);
   const size_t total = b_off + b_x + 2 * b_c + 2 * b_v + 2 * b_f;
-  char* base = nullptr;
-  HIPCHK64(hipMalloc(reinterpret_cast<void**>(&base), total));
-  struct Free {
-    char* p;
-    ~Free() { hipFree(p); }
-  } fr{base};
-  char* q = base;
+  // one staging slab and stream per device, grown and reused (LocalPlanner<double> profiles
+  // one path per tick): no allocation or device-wide synchronisation per call
+  VelStage64& S = vel_stage64(device);
+  std::lock_guard<std::mutex> lk(S.mu);
+  if (!S.st) HIPCHK64(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+  if (total > S.cap) {
+    HIPCHK64(hipStreamSynchronize(S.st));
+    if (S.base) hipFree(S.base);
+    S.base = nullptr;
+    S.cap = 0;
+    HIPCHK64(hipMalloc(reinterpret_cast<void**>(&S.base), total + total / 2));
+    S.cap = total + total / 2;
+  }
+  char* q = S.base;
   long long* d_off = reinterpret_cast<long long*>(q); q += b_off;
   double* d_x = reinterpret_cast<double*>(q); q += b_x;
   double* d_c = reinterpret_cast<double*>(q); q += b_c;
@@ -626,18 +662,19 @@ int hastar_velocity_profile_batch_f64(int device, const hastar_velocity_params_f
   double* d_vm = reinterpret_cast<double*>(q); q += b_v;
   unsigned char* d_fl = reinterpret_cast<unsigned char*>(q); q += b_f;
   unsigned char* d_feas = reinterpret_cast<unsigned char*>(q);
-  hipStream_t st = nullptr;
-  HIPCHK64(hipMemcpy(d_off, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice));
-  HIPCHK64(hipMemcpy(d_x, xyh, (size_t)pts * 3 * 8, hipMemcpyHostToDevice));
-  HIPCHK64(hipMemcpy(d_c, curv, (size_t)pts * 8, hipMemcpyHostToDevice));
-  HIPCHK64(hipMemcpy(d_v0, vel_init, (size_t)n * 8, hipMemcpyHostToDevice));
-  HIPCHK64(hipMemcpy(d_vm, vmax_curr, (size_t)n * 8, hipMemcpyHostToDevice));
-  HIPCHK64(hipMemcpy(d_fl, flags, (size_t)n, hipMemcpyHostToDevice));
+  hipStream_t st = S.st;
+  HIPCHK64(hipMemcpyAsync(d_off, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, st));
+  HIPCHK64(hipMemcpyAsync(d_x, xyh, (size_t)pts * 3 * 8, hipMemcpyHostToDevice, st));
+  HIPCHK64(hipMemcpyAsync(d_c, curv, (size_t)pts * 8, hipMemcpyHostToDevice, st));
+  HIPCHK64(hipMemcpyAsync(d_v0, vel_init, (size_t)n * 8, hipMemcpyHostToDevice, st));
+  HIPCHK64(hipMemcpyAsync(d_vm, vmax_curr, (size_t)n * 8, hipMemcpyHostToDevice, st));
+  HIPCHK64(hipMemcpyAsync(d_fl, flags, (size_t)n, hipMemcpyHostToDevice, st));
   const VelParams64 P{vp->max_velocity, vp->coast_velocity, vp->max_lat_acc, vp->max_lat_acc * vp->max_lat_acc,
                       vp->max_long_acc, vp->max_long_dec};
   HIPCHK64(launch64_velocity(P, n, d_off, d_x, d_c, d_v0, d_vm, d_fl, d_vel, d_feas, st));
-  HIPCHK64(hipMemcpy(velocity, d_vel, (size_t)pts * 8, hipMemcpyDeviceToHost));
-  HIPCHK64(hipMemcpy(feasible, d_feas, (size_t)n, hipMemcpyDeviceToHost));
+  HIPCHK64(hipMemcpyAsync(velocity, d_vel, (size_t)pts * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK64(hipMemcpyAsync(feasible, d_feas, (size_t)n, hipMemcpyDeviceToHost, st));
+  HIPCHK64(hipStreamSynchronize(st));
   return HASTAR_OK;
 }
 

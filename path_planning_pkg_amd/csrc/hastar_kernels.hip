@@ -290,17 +290,31 @@ struct LdsAcc {
   LAS AStarLdsT<CF>* s;
   int lane;
   uint32_t cb;
+  // The header's links (node 0: root, leftmost, rightmost) are also kept in wave-uniform
+  // registers: the pop's begin(), every link's leftmost/rightmost/root checks and the erase's
+  // root and leftmost updates read them without an LDS round trip.  Writes go to both, so the
+  // LDS header stays exact (the HBM migration copies it).
+  int hp, hl, hr;
   // every field is accessed through its own type (no type punning: with strict aliasing a
   // 16-bit store through an int* view would not be ordered against int loads)
-  __device__ __forceinline__ int L(int x) const { return ufi(s->lr[x].l); }
-  __device__ __forceinline__ int R(int x) const { return ufi(s->lr[x].r); }
-  __device__ __forceinline__ int P(int x) const { return ufi(s->p[x]); }
+  __device__ __forceinline__ int L(int x) const { return x == 0 ? hl : ufi(s->lr[x].l); }
+  __device__ __forceinline__ int R(int x) const { return x == 0 ? hr : ufi(s->lr[x].r); }
+  __device__ __forceinline__ int P(int x) const { return x == 0 ? hp : ufi(s->p[x]); }
   __device__ __forceinline__ int C(int x) const {
     return (int)(((uint32_t)__builtin_amdgcn_readlane((int)cb, x >> 5) >> (x & 31)) & 1u);
   }
-  __device__ __forceinline__ void sL(int x, int v) { s->lr[x].l = (int16_t)v; }
-  __device__ __forceinline__ void sR(int x, int v) { s->lr[x].r = (int16_t)v; }
-  __device__ __forceinline__ void sP(int x, int v) { s->p[x] = (int16_t)v; }
+  __device__ __forceinline__ void sL(int x, int v) {
+    s->lr[x].l = (int16_t)v;
+    hl = x == 0 ? v : hl;
+  }
+  __device__ __forceinline__ void sR(int x, int v) {
+    s->lr[x].r = (int16_t)v;
+    hr = x == 0 ? v : hr;
+  }
+  __device__ __forceinline__ void sP(int x, int v) {
+    s->p[x] = (int16_t)v;
+    hp = x == 0 ? v : hp;
+  }
   __device__ __forceinline__ void sC(int x, int v) {
     const uint32_t bit = 1u << (x & 31);
     const uint32_t nw = v == RB_BLACK ? (cb | bit) : (cb & ~bit);
@@ -1129,13 +1143,25 @@ struct LdsAcc3 {
   int lane;
   int pid;       // this lane's node of the last walk's path (lane = depth)
   int plen;      // path lanes [0, plen) (wave-uniform)
-  __device__ __forceinline__ int L(int x) const { return ufi(q[x].l); }
-  __device__ __forceinline__ int R(int x) const { return ufi(q[x].r); }
-  __device__ __forceinline__ int P(int x) const { return ufi(q[x].p); }
+  // the header's links (root, leftmost, rightmost) in wave-uniform registers as well, as
+  // LdsAcc does: read without an LDS round trip, written to both (lds_tree loads them)
+  int hp, hl, hr;
+  __device__ __forceinline__ int L(int x) const { return x == 0 ? hl : ufi(q[x].l); }
+  __device__ __forceinline__ int R(int x) const { return x == 0 ? hr : ufi(q[x].r); }
+  __device__ __forceinline__ int P(int x) const { return x == 0 ? hp : ufi(q[x].p); }
   __device__ __forceinline__ int C(int x) const { return ufi(q[x].col); }
-  __device__ __forceinline__ void sL(int x, int v) { q[x].l = (int16_t)v; }
-  __device__ __forceinline__ void sR(int x, int v) { q[x].r = (int16_t)v; }
-  __device__ __forceinline__ void sP(int x, int v) { q[x].p = (int16_t)v; }
+  __device__ __forceinline__ void sL(int x, int v) {
+    q[x].l = (int16_t)v;
+    hl = x == 0 ? v : hl;
+  }
+  __device__ __forceinline__ void sR(int x, int v) {
+    q[x].r = (int16_t)v;
+    hr = x == 0 ? v : hr;
+  }
+  __device__ __forceinline__ void sP(int x, int v) {
+    q[x].p = (int16_t)v;
+    hp = x == 0 ? v : hp;
+  }
   __device__ __forceinline__ void sC(int x, int v) { q[x].col = (uint8_t)v; }
   __device__ __forceinline__ uint32_t K(int x) const { return ufu(q[x].key); }
   __device__ __forceinline__ float F(int x) const { return uff(q[x].f); }
@@ -1285,6 +1311,9 @@ __device__ __forceinline__ RBT<LdsAcc3> lds_tree(OuterLds& ol, const SearchCtx& 
   t.lane = c.lane;
   t.pid = NIL;
   t.plen = 0;
+  t.hp = ufi(t.q[0].p);
+  t.hl = ufi(t.q[0].l);
+  t.hr = ufi(t.q[0].r);
   return t;
 }
 // LDS tree -> HBM records (links and colours; key, f, g and the payload are there already),
@@ -1568,15 +1597,12 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
   const GoalC GC = goal_centres(r, P.goal_x, P.goal_y, P.goal_h);
   const int span = 2 * P.na + 1;
   const int open_lim_t = kLdsOuter ? min(open_lim, open_cap) : open_lim;
-  PopPrefetch pf, pi;  // issued after the pop / by an insert that became the leftmost
-  int pf_lm = 0;       // the LDS tree's leftmost node during an expansion (0: empty)
-  bool pi_issued = false;
+  PopPrefetch pf;  // issued after the pop
   pf.idx = NIL;
   pf.ph = 0u;
   pf.probe = v2u{0u, 0u};
   pf.b = PopPrefetch::v4{0, 0, 0, 0};
   pf.d = pf.b;
-  pi = pf;
   // lanes per candidate action: 16 when the window has at most 4 actions (the Dubins
   // libm calls then spread over the group), else 4 (one Dubins word per lane)
 #ifdef HASTAR_DBG_NARROW
@@ -1604,11 +1630,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     Node3 top;
     if constexpr (kLdsOuter) {
       const Quad tq = o3.quad(b);
-      if (b == pi.idx) {
-        ph = pi.ph;
-        p0 = pi.probe;
-        top = o3.node_pv(tq, pi.b, pi.d);
-      } else if (b == pf.idx) {
+      if (b == pf.idx) {
         ph = pf.ph;
         p0 = pf.probe;
         top = o3.node_pv(tq, pf.b, pf.d);
@@ -1617,11 +1639,9 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
         top = o3.node_q(b, tq);
       }
 #ifdef HASTAR_STAMPS
-      if (b == pi.idx || b == pf.idx) c.cyc[38]++;  // pops served by a prefetch
+      if (b == pf.idx) c.cyc[38]++;  // pops served by a prefetch
       else c.cyc[39]++;
 #endif
-      pi.idx = NIL;
-      pi_issued = false;
     } else {
       top = o3.node(b);
       p0 = closed3_probe(c, top.key, &ph);
@@ -1651,7 +1671,6 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     if constexpr (kLdsOuter) {
       const int b2 = o3.begin();
       pf.idx = NIL;
-      pf_lm = b2;  // the leftmost (0: empty tree)
       if (b2 != 0) {
         typedef int v4 __attribute__((ext_vector_type(4)));
         pf.probe = closed3_probe(c, o3.K(b2), &pf.ph);
@@ -1861,8 +1880,6 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
           o3.unlink(hit);
           tpool_free(o3, c.ps3, hit);
           if (kLdsOuter && hit == pf.idx) pf.idx = NIL;  // its index may be reused by the insert
-          if (kLdsOuter && hit == pi.idx) pi.idx = NIL;
-          if (kLdsOuter && hit == pf_lm) pf_lm = o3.begin();
           STAMP_ADD(15, tu3);
         }
         // AStar::find_path(int, int): a memo hit probed above is still valid while no
@@ -1879,31 +1896,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
         STAMP_ADD(3, ta);
         const float f = s.g + stl_max(h1, s.dub);
         STAMP_T ti3 = STAMP_NOW();
-        if constexpr (kLdsOuter) {
-          int wh[3];
-          if (!insert3(c, o3, s, f, ci, open_cap, wh)) { fail = true; break; }
-          // the new node became the leftmost (attached as the left child of the leftmost):
-          // it is the next pop unless a later successor goes before it, so its closed-set
-          // probe is issued now and its payload is the record just written
-          // (its own registers: overwriting a load's destination while it is in flight would
-          // wait for it; a second new leftmost in one expansion only invalidates the first)
-          if (wh[0] != NIL && wh[2] && wh[1] == pf_lm) {
-            pf_lm = wh[0];
-            if (!pi_issued) {
-              typedef int v4 __attribute__((ext_vector_type(4)));
-              pi_issued = true;
-              pi.idx = wh[0];
-              pi.probe = closed3_probe(c, key, &pi.ph);
-              pi.b = v4{wh[1], (int)((uint32_t)RB_RED | ((uint32_t)s.ci << 8)), __float_as_int(s.g),
-                        __float_as_int(s.vmin)};
-              pi.d = v4{__float_as_int(s.x), __float_as_int(s.y), __float_as_int(s.h), ci};
-            } else {
-              pi.idx = NIL;
-            }
-          }
-        } else {
-          if (!insert3(c, o3, s, f, ci, open_cap)) { fail = true; break; }
-        }
+        if (!insert3(c, o3, s, f, ci, open_cap)) { fail = true; break; }
         STAMP_ADD(14, ti3);
       }
       if (c.status != 0) break;
