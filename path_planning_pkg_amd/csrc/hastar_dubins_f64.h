@@ -2,10 +2,12 @@
 // T = double): the shortest CSC word of one start pose and its sampled path, one thread.
 // Used by the unit kernels (hastar_units.hip: Dubins<double> of include/hastar_units.h) and by
 // the double planner's search (hastar_f64.hip: HybridAStar<double>'s heuristic and shots).
-// Device f64 sin/cos/atan2/acos agree with glibc's to an ulp or two, not always bit for bit.
+// Its sin/cos/atan2 are ports of glibc 2.35's (hastar_libm64.h), bit for bit the host's; acos is
+// correctly rounded, which glibc's is on all but ~0.1 % of arguments.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "hastar_device.h"
+#include "hastar_libm64.h"
 
 namespace hastar {
 
@@ -21,7 +23,7 @@ __device__ inline double dub_word_d(const DubD& D, int w, double csx, double csy
   const double dx = cgx - csx, dy = cgy - csy;
   const double r = D.r;
   if (w == 0 || w == 3) {  // RSR / LSL
-    const double th = ::atan2(dy, dx);
+    const double th = gm64::atan2(dy, dx);
     const double sgn = (w == 0) ? 1.0 : -1.0;
     q[0] = sgn * M_PI_2 + sh;
     const double t1 = sgn * M_PI_2 + th;
@@ -40,11 +42,11 @@ __device__ inline double dub_word_d(const DubD& D, int w, double csx, double csy
     return (w == 0) ? dst + r * -(q[1] + q[3]) : dst + r * (q[1] + q[3]);
   }
   const double dist = ::sqrt(dx * dx + dy * dy);
-  const double th = ::atan2(dy, dx);
+  const double th = gm64::atan2(dy, dx);
   double t1;
   if (w == 1) {  // RSL
     q[0] = M_PI_2 + sh;
-    t1 = ::acos(2 * r / dist) + th;
+    t1 = gm64::acos(2 * r / dist) + th;
     q[2] = t1 - M_PI;
     const double tg = -M_PI_2 + gh;
     q[1] = t1 - q[0];
@@ -53,7 +55,7 @@ __device__ inline double dub_word_d(const DubD& D, int w, double csx, double csy
     if (q[3] < 0) q[3] += 2 * M_PI;
   } else {  // LSR
     q[0] = -M_PI_2 + sh;
-    t1 = -::acos(2 * r / dist) + th;
+    t1 = -gm64::acos(2 * r / dist) + th;
     q[2] = t1 + M_PI;
     const double tg = M_PI_2 + gh;
     q[1] = t1 - q[0];
@@ -61,8 +63,8 @@ __device__ inline double dub_word_d(const DubD& D, int w, double csx, double csy
     q[3] = tg - q[2];
     if (q[3] > 0) q[3] -= 2 * M_PI;
   }
-  const double ax = csx + r * ::cos(t1), ay = csy + r * ::sin(t1);
-  const double bx = cgx + r * ::cos(q[2]), by = cgy + r * ::sin(q[2]);
+  const double ax = csx + r * gm64::cos(t1), ay = csy + r * gm64::sin(t1);
+  const double bx = cgx + r * gm64::cos(q[2]), by = cgy + r * gm64::sin(q[2]);
   const double ex = bx - ax, ey = by - ay;
   const double dst = ::sqrt(ex * ex + ey * ey);
   return (w == 1) ? dst + r * (-q[1] + q[3]) : dst + r * (q[1] - q[3]);
@@ -71,14 +73,14 @@ __device__ inline double dub_word_d(const DubD& D, int w, double csx, double csy
 // length, acos of a ratio > 1, never compares shorter)
 __device__ inline double dub_shortest_d(DubD& D, double sx, double sy, double sh, double gx, double gy, double gh) {
   const double r = D.r;
-  D.cx[0] = sx + r * ::sin(sh);
-  D.cy[0] = sy - r * ::cos(sh);
-  D.cx[1] = sx - r * ::sin(sh);
-  D.cy[1] = sy + r * ::cos(sh);
-  D.cx[2] = gx + r * ::sin(gh);
-  D.cy[2] = gy - r * ::cos(gh);
-  D.cx[3] = gx - r * ::sin(gh);
-  D.cy[3] = gy + r * ::cos(gh);
+  D.cx[0] = sx + r * gm64::sin(sh);
+  D.cy[0] = sy - r * gm64::cos(sh);
+  D.cx[1] = sx - r * gm64::sin(sh);
+  D.cy[1] = sy + r * gm64::cos(sh);
+  D.cx[2] = gx + r * gm64::sin(gh);
+  D.cy[2] = gy - r * gm64::cos(gh);
+  D.cx[3] = gx - r * gm64::sin(gh);
+  D.cy[3] = gy + r * gm64::cos(gh);
   const int si[4] = {0, 0, 1, 1}, gi[4] = {2, 3, 2, 3};
   double best = 0;
   D.word = 0;
@@ -100,8 +102,8 @@ __device__ inline int dub_sample_d(const DubD& D, double* xyh, double* curv, int
   const int si[4] = {0, 0, 1, 1}, gi[4] = {2, 3, 2, 3};
   const double csx = D.cx[si[w]], csy = D.cy[si[w]], cgx = D.cx[gi[w]], cgy = D.cy[gi[w]];
   const double r = D.r;
-  const double ax = csx + r * ::cos(D.prm[0] + D.prm[1]), ay = csy + r * ::sin(D.prm[0] + D.prm[1]);
-  const double bx = cgx + r * ::cos(D.prm[2]), by = cgy + r * ::sin(D.prm[2]);
+  const double ax = csx + r * gm64::cos(D.prm[0] + D.prm[1]), ay = csy + r * gm64::sin(D.prm[0] + D.prm[1]);
+  const double bx = cgx + r * gm64::cos(D.prm[2]), by = cgy + r * gm64::sin(D.prm[2]);
   const double ex = bx - ax, ey = by - ay;
   const double lst = ::sqrt(ex * ex + ey * ey);
   const int n1 = (int)::floor((s_right ? -D.prm[1] : D.prm[1]) / D.ang_step);
@@ -111,13 +113,13 @@ __device__ inline int dub_sample_d(const DubD& D, double* xyh, double* curv, int
   const double k = 1 / r;
   double th = D.prm[0];
   for (int i = 0; i < n1; ++i) {
-    xyh[3 * i] = csx + r * ::cos(th);
-    xyh[3 * i + 1] = csy + r * ::sin(th);
+    xyh[3 * i] = csx + r * gm64::cos(th);
+    xyh[3 * i + 1] = csy + r * gm64::sin(th);
     xyh[3 * i + 2] = s_right ? wrap_pi_d(th - M_PI_2) : wrap_pi_d(th + M_PI_2);
     curv[i] = k;
     th = s_right ? th - D.ang_step : th + D.ang_step;
   }
-  const double ts = ::atan2(ey, ex), ct = ::cos(ts), st = ::sin(ts);
+  const double ts = gm64::atan2(ey, ex), ct = gm64::cos(ts), st = gm64::sin(ts);
   double dd = 0;
   for (int i = n1; i < n2; ++i) {
     xyh[3 * i] = ax + dd * ct;
@@ -128,15 +130,15 @@ __device__ inline int dub_sample_d(const DubD& D, double* xyh, double* curv, int
   }
   th = D.prm[2];
   for (int i = n2; i < n3; ++i) {
-    xyh[3 * i] = cgx + r * ::cos(th);
-    xyh[3 * i + 1] = cgy + r * ::sin(th);
+    xyh[3 * i] = cgx + r * gm64::cos(th);
+    xyh[3 * i + 1] = cgy + r * gm64::sin(th);
     xyh[3 * i + 2] = g_right ? wrap_pi_d(th - M_PI_2) : wrap_pi_d(th + M_PI_2);
     curv[i] = k;
     th = g_right ? th - D.ang_step : th + D.ang_step;
   }
   const double e = D.prm[2] + D.prm[3];
-  xyh[3 * n3] = cgx + r * ::cos(e);
-  xyh[3 * n3 + 1] = cgy + r * ::sin(e);
+  xyh[3 * n3] = cgx + r * gm64::cos(e);
+  xyh[3 * n3 + 1] = cgy + r * gm64::sin(e);
   xyh[3 * n3 + 2] = g_right ? wrap_pi_d(e - M_PI_2) : wrap_pi_d(e + M_PI_2);
   curv[n3] = 0;
   return n3 + 1;

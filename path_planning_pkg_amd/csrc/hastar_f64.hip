@@ -20,9 +20,11 @@
 //   k64_velocity      VelocityGenerator<double>::generate_velocity_profile
 //                     (VelocityGenerator.cpp:19-84), one thread per path.
 //
-// Expressions keep the reference's double arithmetic (-ffp-contract=off).  The device's f64
-// sin/cos/atan2/acos/hypot are within an ulp or two of glibc's, so this planner matches the
-// reference to a tolerance, not bit for bit (include/hastar_f64.h).
+// Expressions keep the reference's double arithmetic (-ffp-contract=off).  sin, cos, atan2 and
+// hypot are ports of glibc 2.35's routines (hastar_libm64.h), bit for bit the host libm's on every
+// argument sampled; acos is correctly rounded, which glibc's acos is on all but ~0.1 % of
+// arguments.  So this planner reproduces the reference bit for bit unless a search meets one of
+// those acos arguments (include/hastar_f64.h).
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include "hastar_device.h"
@@ -283,9 +285,9 @@ __device__ double apf_field64(const Planner64Dev& P, const GAS double* apf, doub
   double acc = 0.0;
   for (int k = 0; k < P.n_apf; ++k) {
     const double ox = apf[3 * k], oy = apf[3 * k + 1], orad = apf[3 * k + 2];
-    const double d = ::hypot(ox - px, oy - py);
+    const double d = gm64::hypot(ox - px, oy - py);
     if (d < orad) {
-      double ang = ::fabs(wrap_pi_d(ph - ::atan2(oy - py, ox - px)));
+      double ang = ::fabs(wrap_pi_d(ph - gm64::atan2(oy - py, ox - px)));
       ang = stl_maxd(P.apf_ang - ang, 0.0);
       const double t = 1.0 / d - 1.0 / orad;
       double fp = P.apf_rep * (t * t);  // std::pow(t, 2)
@@ -769,7 +771,7 @@ __global__ __launch_bounds__(64) void k64_velocity(VelParams64 vp, int n, const 
   vmax = stl_mind(vmax, vmax_curr[p]);
   const double vmax2 = vmax * vmax;
   const double v0 = vel_init[p];
-  auto step = [X](long long a, long long b) { return ::hypot(X[3 * a] - X[3 * b], X[3 * a + 1] - X[3 * b + 1]); };
+  auto step = [X](long long a, long long b) { return gm64::hypot(X[3 * a] - X[3 * b], X[3 * a + 1] - X[3 * b + 1]); };
   V[0] = v0 * v0;
   double mcur = V[0];
   for (long long i = 0; i < S - 1; ++i) {  // initial profile (VelocityGenerator.cpp:34-49)

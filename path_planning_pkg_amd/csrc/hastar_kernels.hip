@@ -19,6 +19,9 @@
 
 namespace hastar {
 
+#ifndef HASTAR_C32
+#define HASTAR_C32 0
+#endif
 #ifndef HASTAR_WAVES_PER_EU
 #define HASTAR_WAVES_PER_EU 2  // search waves per SIMD the register budget must allow
 #endif
@@ -92,7 +95,13 @@ struct SearchCtx {
   PoolState ps3, ps2;
   int n_closed3;
   uint32_t gen3, gen2;
+#if HASTAR_C32
+  // 32-bit search statistics (two SGPRs fewer each than 64-bit ones; a search would need
+  // hours to count 2^32 pops), widened when they are stored (SearchResult)
+  uint32_t pops, succ, apops, asearch, shots, amigr, apops_g;
+#else
   long long pops, succ, apops, asearch, shots, amigr, apops_g;
+#endif
   int status;
   bool cost_only;   // AStar::a_star_search(get_cost_only): memo exits + memoise (always, inside the search)
   uint32_t prep_epoch;  // latency kernel: the search's epoch in the helper waves' prep table
@@ -101,17 +110,54 @@ struct SearchCtx {
 #endif
 };
 
-// the hot fields of c.P and c.A, once per search (or per A* query)
+// Pin a wave-uniform pointer in a VGPR pair instead: the search's SGPRs are its scarce
+// registers (the batch kernel spills hundreds of them to VGPR lanes, and the inner A* loop
+// reloads them), while its VGPR budget has room.  The map and arena bases below are only ever
+// used to form per-lane or uniform global addresses, which a VGPR base serves as well.
+template <class T>
+__device__ __forceinline__ GAS T* pinv(GAS T* p) {
+  uint64_t v = (uint64_t)p;
+  asm volatile("" : "+v"(v));
+  return (GAS T*)v;
+}
+#ifndef HASTAR_VPTR
+#define HASTAR_VPTR 1
+#endif
+#if HASTAR_VPTR >= 1
+#define PIN_MAP pinv
+#else
+#define PIN_MAP pin
+#endif
+#if HASTAR_VPTR >= 2
+#define PIN_ARENA pinv
+#else
+#define PIN_ARENA pin
+#endif
+
+// the hot fields of c.P and c.A, once per search (or per A* query).  kVgprMaps: the map and
+// cell-record bases in VGPRs (the batch kernel; the latency kernel keeps them in SGPRs: its
+// VGPRs are the ones it runs short of)
+template <bool kVgprMaps = false>
 __device__ __forceinline__ void bind_hot(SearchCtx& c) {
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
-  c.occ = pin(gp(P.occ));
-  c.nm_f = pin(gp(P.nm_f));
-  c.visited = pin(gp(P.visited));
-  c.cell2 = pin(gp(A.cell2));
-  c.prevl = pin(gp(A.prevl));
-  c.slots3 = pin(gp(A.slots3));
-  c.closed3 = pin(gp(A.closed3));
+  if constexpr (kVgprMaps) {
+    c.occ = PIN_MAP(gp(P.occ));
+    c.nm_f = PIN_MAP(gp(P.nm_f));
+    c.visited = PIN_MAP(gp(P.visited));
+    c.cell2 = PIN_MAP(gp(A.cell2));
+    c.prevl = PIN_MAP(gp(A.prevl));
+    c.slots3 = PIN_ARENA(gp(A.slots3));
+    c.closed3 = PIN_ARENA(gp(A.closed3));
+  } else {
+    c.occ = pin(gp(P.occ));
+    c.nm_f = pin(gp(P.nm_f));
+    c.visited = pin(gp(P.visited));
+    c.cell2 = pin(gp(A.cell2));
+    c.prevl = pin(gp(A.prevl));
+    c.slots3 = pin(gp(A.slots3));
+    c.closed3 = pin(gp(A.closed3));
+  }
   c.open3 = pin(gp(A.open3));
   c.smask = pin(A.slots3_mask);
   c.N = pin(P.N);
@@ -290,30 +336,22 @@ struct LdsAcc {
   LAS AStarLdsT<CF>* s;
   int lane;
   uint32_t cb;
-  // The header's links (node 0: root, leftmost, rightmost) are also kept in wave-uniform
-  // registers: the pop's begin(), every link's leftmost/rightmost/root checks and the erase's
-  // root and leftmost updates read them without an LDS round trip.  Writes go to both, so the
-  // LDS header stays exact (the HBM migration copies it).
-  int hp, hl, hr;
   // every field is accessed through its own type (no type punning: with strict aliasing a
   // 16-bit store through an int* view would not be ordered against int loads)
-  __device__ __forceinline__ int L(int x) const { return x == 0 ? hl : ufi(s->lr[x].l); }
-  __device__ __forceinline__ int R(int x) const { return x == 0 ? hr : ufi(s->lr[x].r); }
-  __device__ __forceinline__ int P(int x) const { return x == 0 ? hp : ufi(s->p[x]); }
+  __device__ __forceinline__ int L(int x) const { return ufi(s->lr[x].l); }
+  __device__ __forceinline__ int R(int x) const { return ufi(s->lr[x].r); }
+  __device__ __forceinline__ int P(int x) const { return ufi(s->p[x]); }
   __device__ __forceinline__ int C(int x) const {
     return (int)(((uint32_t)__builtin_amdgcn_readlane((int)cb, x >> 5) >> (x & 31)) & 1u);
   }
   __device__ __forceinline__ void sL(int x, int v) {
     s->lr[x].l = (int16_t)v;
-    hl = x == 0 ? v : hl;
   }
   __device__ __forceinline__ void sR(int x, int v) {
     s->lr[x].r = (int16_t)v;
-    hr = x == 0 ? v : hr;
   }
   __device__ __forceinline__ void sP(int x, int v) {
     s->p[x] = (int16_t)v;
-    hp = x == 0 ? v : hp;
   }
   __device__ __forceinline__ void sC(int x, int v) {
     const uint32_t bit = 1u << (x & 31);
@@ -1919,7 +1957,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
 template <class CF, bool kWide>
 __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLdsT<CF>& alds, OuterLds* ol,
                                            long long hard_pops, bool resume, int dbg = 0, PrepL* pr = nullptr) {
-  bind_hot(c);
+  bind_hot<!kWide>(c);
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
   const int lane = c.lane;
