@@ -19,9 +19,6 @@
 
 namespace hastar {
 
-#ifndef HASTAR_C32
-#define HASTAR_C32 0
-#endif
 #ifndef HASTAR_WAVES_PER_EU
 #define HASTAR_WAVES_PER_EU 2  // search waves per SIMD the register budget must allow
 #endif
@@ -95,13 +92,9 @@ struct SearchCtx {
   PoolState ps3, ps2;
   int n_closed3;
   uint32_t gen3, gen2;
-#if HASTAR_C32
-  // 32-bit search statistics (two SGPRs fewer each than 64-bit ones; a search would need
+  // 32-bit search statistics (two SGPRs fewer each than 64-bit ones: a search would need
   // hours to count 2^32 pops), widened when they are stored (SearchResult)
   uint32_t pops, succ, apops, asearch, shots, amigr, apops_g;
-#else
-  long long pops, succ, apops, asearch, shots, amigr, apops_g;
-#endif
   int status;
   bool cost_only;   // AStar::a_star_search(get_cost_only): memo exits + memoise (always, inside the search)
   uint32_t prep_epoch;  // latency kernel: the search's epoch in the helper waves' prep table
@@ -120,19 +113,6 @@ __device__ __forceinline__ GAS T* pinv(GAS T* p) {
   asm volatile("" : "+v"(v));
   return (GAS T*)v;
 }
-#ifndef HASTAR_VPTR
-#define HASTAR_VPTR 1
-#endif
-#if HASTAR_VPTR >= 1
-#define PIN_MAP pinv
-#else
-#define PIN_MAP pin
-#endif
-#if HASTAR_VPTR >= 2
-#define PIN_ARENA pinv
-#else
-#define PIN_ARENA pin
-#endif
 
 // the hot fields of c.P and c.A, once per search (or per A* query).  kVgprMaps: the map and
 // cell-record bases in VGPRs (the batch kernel; the latency kernel keeps them in SGPRs: its
@@ -141,14 +121,14 @@ template <bool kVgprMaps = false>
 __device__ __forceinline__ void bind_hot(SearchCtx& c) {
   const PlannerDev& P = *c.P;
   const SlotArena& A = *c.A;
-  if constexpr (kVgprMaps) {
-    c.occ = PIN_MAP(gp(P.occ));
-    c.nm_f = PIN_MAP(gp(P.nm_f));
-    c.visited = PIN_MAP(gp(P.visited));
-    c.cell2 = PIN_MAP(gp(A.cell2));
-    c.prevl = PIN_MAP(gp(A.prevl));
-    c.slots3 = PIN_ARENA(gp(A.slots3));
-    c.closed3 = PIN_ARENA(gp(A.closed3));
+  if constexpr (kVgprMaps) {  // (the outer tree's slots3/closed3 stay in SGPRs: in VGPRs they spilled to scratch)
+    c.occ = pinv(gp(P.occ));
+    c.nm_f = pinv(gp(P.nm_f));
+    c.visited = pinv(gp(P.visited));
+    c.cell2 = pinv(gp(A.cell2));
+    c.prevl = pinv(gp(A.prevl));
+    c.slots3 = pin(gp(A.slots3));
+    c.closed3 = pin(gp(A.closed3));
   } else {
     c.occ = pin(gp(P.occ));
     c.nm_f = pin(gp(P.nm_f));
