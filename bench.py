@@ -855,6 +855,7 @@ def cpu_baseline_cfg5(pairs, budget_s, ticks):
 
     pops, wall, n = 0, 0.0, 0
     tick_max = np.zeros(ticks)
+    per_tick = [[] for _ in range(ticks)]  # every replayed pair's find_path ms, per tick
     replay = {}
     with ThreadPoolExecutor(T) as ex:
         while n < len(pairs) and wall < 4 * budget_s:
@@ -864,12 +865,23 @@ def cpu_baseline_cfg5(pairs, budget_s, ticks):
             for j, (p, ms, keys) in enumerate(rnd):
                 pops += p
                 tick_max = np.maximum(tick_max, ms)
+                for t in range(ticks):
+                    per_tick[t].append(ms[t])
                 replay[n + j] = keys
             n += len(rnd)
+
+    def makespan(ms, cores):  # longest-processing-time-first list schedule of one tick's pairs
+        load = [0.0] * cores
+        for x in sorted(ms, reverse=True):
+            load[load.index(min(load))] += x
+        return max(load)
     return ({"value": pops / wall if wall > 0 else None, "unit": "expansions/s", "cores": T, "kind": "port",
              "sample": f"first {n} pairs of rank 0 x {ticks} ticks (same call sequence as the GPU run), find_path "
                        f"only, {T} threads with one private planner each (oracle/hastar_oracle.cpp, -O3)",
-             "tick_ms_one_core_per_pair": float(tick_max.mean()) if n else None}, replay)
+             "tick_ms_one_core_per_pair": float(tick_max.mean()) if n else None,
+             # the same ticks on this box's T host threads: each tick's replayed pairs list-scheduled
+             # longest first over T cores (a tick of 64 pairs on 16 threads takes at least 4 pairs' time)
+             f"tick_ms_{T}_threads": float(np.mean([makespan(m, T) for m in per_tick])) if n else None}, replay)
 
 
 def parity_sample(cfgs, gpu, qids):

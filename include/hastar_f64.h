@@ -13,10 +13,12 @@
  * the reference's exact open/closed-set semantics.  Per-call scalar preparation (grid frame,
  * motion tables, raster parameters, start node) is done on the host with the reference's
  * double arithmetic and glibc libm; the kernels' APF field, Dubins lengths and shot sampling
- * use the device's f64 sin/cos/atan2/acos/hypot, which agree with glibc to an ulp or two but
- * not always bit for bit — so results match the reference to a tolerance (same goal
- * decision and closed set in every tested case, cost within 1e-12 relative),
- * not bit for bit like the float planner.  There is no CPU fallback.
+ * use ports of glibc 2.35's own sin/cos/atan2/acos/hypot (csrc/hastar_libm64.h: bit for bit
+ * the host libm on every sampled argument), so results equal the reference's bit for bit, as
+ * the float planner's do: success, cost, statistics, closed set, path and memo
+ * (tests/test_gpu_f64.py; the oracle is the reference's algorithm instantiated for double,
+ * parity with the reference itself being pinned by its Dubins/VehicleModel double vectors
+ * only).  There is no CPU fallback.
  *
  * Status codes, statistics and the path output format are those of include/hastar.h.
  */

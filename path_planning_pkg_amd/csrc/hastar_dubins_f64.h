@@ -2,8 +2,7 @@
 // T = double): the shortest CSC word of one start pose and its sampled path, one thread.
 // Used by the unit kernels (hastar_units.hip: Dubins<double> of include/hastar_units.h) and by
 // the double planner's search (hastar_f64.hip: HybridAStar<double>'s heuristic and shots).
-// Its sin/cos/atan2 are ports of glibc 2.35's (hastar_libm64.h), bit for bit the host's; acos is
-// correctly rounded, which glibc's is on all but ~0.1 % of arguments.
+// Its sin/cos/atan2/acos are ports of glibc 2.35's (hastar_libm64.h), bit for bit the host's.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "hastar_device.h"

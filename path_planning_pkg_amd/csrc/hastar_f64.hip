@@ -20,11 +20,10 @@
 //   k64_velocity      VelocityGenerator<double>::generate_velocity_profile
 //                     (VelocityGenerator.cpp:19-84), one thread per path.
 //
-// Expressions keep the reference's double arithmetic (-ffp-contract=off).  sin, cos, atan2 and
-// hypot are ports of glibc 2.35's routines (hastar_libm64.h), bit for bit the host libm's on every
-// argument sampled; acos is correctly rounded, which glibc's acos is on all but ~0.1 % of
-// arguments.  So this planner reproduces the reference bit for bit unless a search meets one of
-// those acos arguments (include/hastar_f64.h).
+// Expressions keep the reference's double arithmetic (-ffp-contract=off).  sin, cos, atan2, acos
+// and hypot are ports of glibc 2.35's routines (hastar_libm64.h), bit for bit the host libm's on
+// every argument sampled, so this planner reproduces the reference bit for bit
+// (include/hastar_f64.h).
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include "hastar_device.h"

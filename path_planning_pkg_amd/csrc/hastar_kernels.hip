@@ -115,8 +115,9 @@ __device__ __forceinline__ GAS T* pinv(GAS T* p) {
 }
 
 // the hot fields of c.P and c.A, once per search (or per A* query).  kVgprMaps: the map and
-// cell-record bases in VGPRs (the batch kernel; the latency kernel keeps them in SGPRs: its
-// VGPRs are the ones it runs short of)
+// cell-record bases in VGPRs (the batch kernel: SGPR spills 740 -> 563 with 32-bit counters,
+// +3-5 % expansions/s, profiles/r05d_ab_vgpr_pins.jsonl; the latency kernel keeps them in SGPRs:
+// there the VGPR pins cost 9 % on cfg5, profiles/r05f_cfg5_ab.jsonl)
 template <bool kVgprMaps = false>
 __device__ __forceinline__ void bind_hot(SearchCtx& c) {
   const PlannerDev& P = *c.P;

@@ -1,16 +1,24 @@
 // hastar_libm64.h — the f64 libm of the double planner's device code (hastar_f64.hip,
 // hastar_dubins_f64.h): sin, cos, atan2, acos and hypot as HybridAStar<double> calls them
-// (Dubins.cpp:23-33, 185-263, 331-417; Grid3D.cpp:212-213).
+// (Dubins.cpp:23-33, 185-263, 331-417; Grid3D.cpp:212-213; VelocityGenerator.cpp:40-84).
 //
 // The device libm (ocml) differs from the host's glibc 2.35 in the last bit on 3 % (sin, cos) to
-// 27 % (atan2) of the planner's arguments (tools/libm64_fingerprint.hip, profiles/r05_libm64_*).
-// glibc rounds these functions correctly, or nearly so, so these routines compute each value as
-// a double-double (about 100 correct bits) and round it once: the correctly rounded result,
-// which is glibc's wherever glibc rounds correctly.  The same code runs on the host (the
-// fingerprint tool checks device == host and both against glibc).  Every operation is an IEEE
-// basic operation or an explicit fma, and the build has -ffp-contract=off, so the results do
-// not depend on where they are computed.  Constants: hastar_libm64_tables.h
-// (tools/gen_libm64_tables.py, decimal arithmetic at 80 digits).
+// 27 % (atan2) of the planner's arguments (tools/libm64_fingerprint.hip, profiles/r05_libm64_ocml
+// .jsonl), and glibc itself is not correctly rounded (a double-double evaluation rounded once
+// still differed on ~0.1 % of arguments).  So these are ports of glibc 2.35's own routines, in the
+// variants the x86-64 libm dispatches to on FMA hardware (__sin_fma, __cos_fma,
+// __ieee754_atan2_fma, __ieee754_acos_fma; hypot has no FMA variant): the IBM Accurate
+// Mathematical Library algorithms of sysdeps/ieee754/dbl-64 (s_sin.c, e_atan2.c, e_asin.c without
+// their removed slow paths) and Borges' hypot (e_hypot.c), with every fused multiply-add GCC forms
+// in that build written out (a product fuses into an addition or subtraction in the same basic
+// block when all its uses are such).  Their accurate tables (uatan2.tbl, asncs.tbl, root.tbl) and
+// the atan2/acos series constants are data read from this container's libm.so.6
+// (tools/extract_glibc_{atan,acos}_table.py: the table points of Gal's accurate-table method cannot
+// be recomputed); sin/cos's table and constants are recomputed (tools/gen_libm64_tables.py).
+// Result: bit for bit the host glibc on 2e8 device samples per function and 5e7 host samples
+// (tests/test_libm64_ports.py, profiles/r05_libm64_gm64.jsonl).  Every operation is an IEEE basic
+// operation or an explicit fma and the build has -ffp-contract=off, so device and host agree.
+// glibc is LGPL-2.1 (NOTICE).
 #pragma once
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -19,6 +27,7 @@
 #include <cstdint>
 #include "hastar_libm64_tables.h"
 #include "hastar_libm64_atan_table.h"
+#include "hastar_libm64_acos_table.h"
 
 #if defined(__HIPCC__)
 #define GM64_HD __host__ __device__ __forceinline__
@@ -278,19 +287,80 @@ GM64_HD double atan2(double y, double x) {
   return std::copysign(z, y);
 }
 
-// ---- acos: 2 atan(sqrt((1 - x) / (1 + x))) -------------------------------------------------
+// ---- acos: glibc 2.35's algorithm (sysdeps/ieee754/dbl-64/e_asin.c without its removed slow
+// paths, the __ieee754_acos_fma variant: GCC's fusions written out) on asncs.tbl / root.tbl
+// (hastar_libm64_acos_table.h) --------------------------------------------------------------
+namespace ac {
+constexpr double hp0 = 0x1.921fb54442d18p+0, hp1 = 0x1.1a62633145c07p-54, pi = 0x1.921fb54442d18p+1, t27 = 0x1p27;
+constexpr double f1 = 0x1.55555555554f9p-3, f2 = 0x1.333333336127dp-4, f3 = 0x1.6db6dae42c0e4p-5,
+                 f4 = 0x1.f1c7e04f4ad99p-6, f5 = 0x1.6e442c822d419p-6, f6 = 0x1.292d80f453c72p-6;
+constexpr double rt0 = 0x1.fffffffecc1ddp-1, rt1 = 0x1.fffffff757304p-2, rt2 = 0x1.800496769c91ap-2,
+                 rt3 = 0x1.4006318d1dab9p-2;
+}  // namespace ac
+GM64_HD double ac_poly_f(double v) {  // ((((f6 v + f5) v + f4) v + f3) v + f2) v + f1
+  double p = fma_(v, ac::f6, ac::f5);
+  p = fma_(v, p, ac::f4);
+  p = fma_(v, p, ac::f3);
+  p = fma_(v, p, ac::f2);
+  return fma_(v, p, ac::f1);
+}
+// one asncs interval: n its first entry, K the index of its last series coefficient
+GM64_HD double ac_table(double x, int m_pos, int n, int K) {
+  const double xx = (m_pos ? x : -x) - kAsncs[n];
+  double q = kAsncs[n + K];
+  for (int i = K - 1; i >= 2; --i) q = fma_(xx, q, kAsncs[n + i]);
+  const double p = fma_(xx * xx, q, kAsncs[n + K + 1]);
+  const double t = fma_(xx, kAsncs[n + 1], p);
+  const double ya = kAsncs[n + K + 2];
+  if (m_pos) return (ac::hp1 - t) + (ac::hp0 - ya);
+  return (t + ac::hp1) + (ya + ac::hp0);
+}
 GM64_HD double acos(double x) {
-  if (std::isnan(x)) return x + x;
-  const double ax = std::fabs(x);
-  if (ax > 1.0) return (x - x) / (x - x);
-  if (x == 1.0) return 0.0;
-  if (x == -1.0) return kPi[0];
-  const dd q = div(two_sum(1.0, -x), two_sum(1.0, x));
-  const dd s = sqrt_dd(q);
-  dd r = (s.hi <= 1.0) ? atan01(s) : sub(tab2(kPio2dd), atan01(div(dd{1.0, 0.0}, s)));
-  r.hi *= 2.0;
-  r.lo *= 2.0;
-  return round_dd(r);
+  uint64_t bx;
+  __builtin_memcpy(&bx, &x, 8);
+  const int32_t m = (int32_t)(bx >> 32);
+  const uint32_t lo = (uint32_t)bx;
+  const uint32_t k = (uint32_t)m & 0x7fffffffu;
+  const int pos = m > 0;
+  if (k < 0x3c880000u) return ac::hp0;
+  if (k < 0x3fc00000u) {  // |x| < 0.125
+    const double x2 = x * x;
+    const double p = ac_poly_f(x2);
+    const double r = ac::hp0 - x;
+    const double cor = fma_(-p, x * x2, ((ac::hp0 - r) - x) + ac::hp1);
+    return r + cor;
+  }
+  if (k < 0x3fd00000u) return ac_table(x, pos, 11 * (int)((k >> 15) & 0x1f), 6);            // [0.125, 0.25)
+  if (k < 0x3fe00000u) return ac_table(x, pos, 11 * (int)((k >> 14) & 0x3f) + 352, 6);      // [0.25, 0.5)
+  if (k < 0x3fe80000u) return ac_table(x, pos, 12 * (int)((k >> 13) & 0x7f) + 1056, 7);     // [0.5, 0.75)
+  if (k < 0x3fed8000u) return ac_table(x, pos, 13 * (int)((k >> 13) & 0x7f) + 992, 8);      // [0.75, 0.921875)
+  if (k < 0x3fee8000u) return ac_table(x, pos, 14 * (int)((k >> 13) & 0x7f) + 884, 9);      // [0.921875, 0.953125)
+  if (k < 0x3fef0000u) return ac_table(x, pos, 15 * (int)((k >> 13) & 0x7f) + 768, 10);     // [0.953125, 0.96875)
+  if (k < 0x3ff00000u) {  // [0.96875, 1): 2 asin(sqrt(z)), z = (1 - |x|) / 2
+    const double z = 0.5 * (pos ? (1.0 - x) : (x + 1.0));
+    uint64_t bz;
+    __builtin_memcpy(&bz, &z, 8);
+    double t = kInroot[(int)((bz >> 46) & 0x7f)] * kPowtwo[511 - (int)(bz >> 53)];
+    const double r = fma_(-(t * t), z, 1.0);
+    t = t * fma_(r, fma_(r, fma_(r, ac::rt3, ac::rt2), ac::rt1), ac::rt0);
+    const double c = z * t;
+    const double u = fma_(-(0.5 * t), c, 1.5);
+    const double y = fma_(-ac::t27, c, fma_(c, ac::t27, c));
+    const double cc = fma_(-y, y, z) / fma_(u, c, y);
+    const double pz = ac_poly_f(z) * z;
+    const double pyc = pz * (y + cc);
+    if (!pos) {
+      const double cor = (ac::hp1 - cc) - pyc;
+      const double res = (ac::hp0 - y) + cor;
+      return res + res;
+    }
+    const double res = (cc + pyc) + y;
+    return res + res;
+  }
+  if (k == 0x3ff00000u && lo == 0u) return pos ? 0.0 : ac::pi;
+  if (k > 0x7ff00000u || (k == 0x7ff00000u && lo != 0u)) return x + x;
+  const double zz = x - x;
+  return zz / zz;
 }
 
 // ---- sin / cos: glibc 2.35's algorithm (sysdeps/ieee754/dbl-64/s_sin.c, the __sin_fma /

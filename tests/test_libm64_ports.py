@@ -2,8 +2,8 @@
 glibc 2.35, on the host (CPU test; tools/libm64_fingerprint.hip runs the same comparison on the
 device, `-m gpu` in test_gpu_f64.py).
 
-sin, cos, atan2 and hypot are ports of glibc's routines and must match bit for bit; acos is
-correctly rounded, which glibc's acos is not on ~0.1 % of arguments (pinned as a bound).
+sin, cos, atan2, acos and hypot are ports of glibc's routines (the FMA variants the x86-64 libm
+dispatches to) and must match bit for bit.
 Arguments: the planner's ranges (headings and arc sums, centre and obstacle offsets in metres,
 2 r / dist) plus edge cases."""
 import subprocess
@@ -65,11 +65,6 @@ def ports(tmp_path_factory):
     return {int(a): int(b) for a, b in (line.split() for line in out if line.strip())}
 
 
-@pytest.mark.parametrize("fn,name", [(0, "sin"), (1, "cos"), (2, "atan2"), (4, "hypot")])
+@pytest.mark.parametrize("fn,name", [(0, "sin"), (1, "cos"), (2, "atan2"), (3, "acos"), (4, "hypot")])
 def test_glibc_ports_bit_exact(ports, fn, name):
     assert ports[fn] == 0, f"{name}: {ports[fn]} mismatches with the host glibc"
-
-
-def test_acos_correctly_rounded_close_to_glibc(ports):
-    # glibc 2.35's acos misrounds ~0.1 % of arguments; the correctly rounded port differs there only
-    assert ports[3] < 400000 * 2e-3, ports[3]

@@ -21,17 +21,19 @@ find $R/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 # profiler serialises the split launch's two kernels, and a 1-step bench then ran > 3 min)
 export HASTAR_SPLIT=0
 B=$(python3 -c "import json;print(json.load(open('$OUT/bench.json'))['config']['queries_per_gpu'])")
-for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 400 rocprofv3 --pmc $C --output-format csv --kernel-include-regex hastar_search_kernel -d $R/$C -o pmc -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --latency-queries 0 --relaxed-batch 0 > $OUT/pmc_$C.log 2>&1 || { tail -5 $OUT/pmc_$C.log; exit 1; }
+for C in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"; do
+  n=${C%% *}
+  timeout -s KILL 400 rocprofv3 --pmc $C --output-format csv --kernel-include-regex hastar_search_kernel -d $R/$n -o pmc -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --latency-queries 0 --relaxed-batch 0 > $OUT/pmc_$n.log 2>&1 || { tail -5 $OUT/pmc_$n.log; exit 1; }
 done
-python3 tools/prof_summary.py pmc $R/FETCH_SIZE $R/WRITE_SIZE $OUT/pmc_search_summary.json --batch $B --grid 1024 || exit 1
+python3 tools/prof_summary.py pmc $R/FETCH_SIZE $R/WRITE_SIZE $OUT/pmc_search_summary.json --rdreq $R/TCC_EA0_RDREQ_sum --batch $B --grid 1024 || exit 1
 cat $OUT/pmc_search_summary.json
 # 3. SQ instruction mix / wait states of the batch kernel (one 1-step bench per pass)
 for pass in "SQA SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU" \
-            "SQB SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA"; do
+            "SQB SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA" \
+            "SQC SQC_ICACHE_HITS SQC_ICACHE_MISSES TCC_HIT_sum TCC_MISS_sum"; do
   set -- $pass
   name=$1; shift
   timeout -s KILL 400 rocprofv3 --pmc "$@" --output-format csv --kernel-include-regex hastar_search_kernel -d $R/$name -o pmc \
     -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --latency-queries 0 --relaxed-batch 0 > $OUT/pmc_$name.log 2>&1 || { tail -5 $OUT/pmc_$name.log; exit 1; }
 done
-python3 tools/prof_summary.py counters $OUT/counters_search.json $R/SQA $R/SQB --batch $B --dispatch -1 || exit 1
+python3 tools/prof_summary.py counters $OUT/counters_search.json $R/SQA $R/SQB $R/SQC --batch $B --dispatch -1 || exit 1

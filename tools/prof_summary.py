@@ -58,13 +58,30 @@ def pmc(args):
     from path_planning_pkg_amd.buildinfo import search_kernel_hash
     out = {"kernel": KERNEL, "batch": args.batch, "grid": args.grid, "dispatch_index": i,
            "kernel_src_sha": search_kernel_hash(), "fetch_size_kib": f_kib, "write_size_kib": w_kib,
-           "hbm_bytes_per_launch": (2 * f_kib + w_kib) * 1024.0,
-           "note": "traffic = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 B per MI355X_MICROARCH.md §HBM; the search "
-                   "kernel's loads are mostly narrow scattered accesses, for which the guide's gfx950 FETCH_SIZE "
-                   "calibration is unverified",
            "fetch_all_dispatches_kib": fetch, "write_all_dispatches_kib": write}
+    if args.rdreq:
+        # the L2's read requests to the fabric by size: their bytes are the calibrated read traffic
+        # (tools/fetch_calib.hip, profiles/r05_fetch_calib.json: on gfx950 every L2 miss of a
+        # narrow scattered load, like a wide streaming one, is one 128-B request, and FETCH_SIZE
+        # tallies it at 64 B, so FETCH_SIZE reads exactly half of these bytes)
+        n = {k: per_dispatch(args.rdreq, k)[i] for k in ("TCC_EA0_RDREQ_128B_sum", "TCC_EA0_RDREQ_64B_sum",
+                                                         "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_sum")}
+        rd = 128.0 * n["TCC_EA0_RDREQ_128B_sum"] + 64.0 * n["TCC_EA0_RDREQ_64B_sum"] + 32.0 * n["TCC_EA0_RDREQ_32B_sum"]
+        out["rdreq"] = n
+        out["read_bytes_calibrated"] = rd
+        out["fetch_size_factor"] = rd / (f_kib * 1024.0)
+        out["hbm_bytes_per_launch"] = rd + w_kib * 1024.0
+        out["note"] = ("traffic = read bytes from the L2's fabric read requests by size (128 B x RDREQ_128B + 64 B x "
+                       "RDREQ_64B + 32 B x RDREQ_32B; fetch_size_factor = those bytes / FETCH_SIZE, 2.00 on this "
+                       "kernel as on the calibration patterns of tools/fetch_calib.hip) + WRITE_SIZE x 1024 B; "
+                       "Infinity-Cache hits are counted (MI355X_MICROARCH.md §HBM)")
+    else:
+        out["hbm_bytes_per_launch"] = (2 * f_kib + w_kib) * 1024.0
+        out["fetch_size_factor"] = 2.0
+        out["note"] = ("traffic = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 B: the factor 2 is calibrated for this "
+                       "kernel's narrow scattered loads by tools/fetch_calib.hip (profiles/r05_fetch_calib.json)")
     Path(args.out).write_text(json.dumps(out, indent=1))
-    print(json.dumps({k: out[k] for k in ("fetch_size_kib", "write_size_kib", "hbm_bytes_per_launch")}))
+    print(json.dumps({k: out[k] for k in ("fetch_size_kib", "write_size_kib", "hbm_bytes_per_launch", "fetch_size_factor")}))
 
 
 def counters(args):
@@ -91,6 +108,10 @@ def counters(args):
                 der[k.lower() + "_frac_of_wave_cycles"] = c[k] / c["SQ_WAVE_CYCLES"]
     if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c and c["TCC_HIT_sum"] + c["TCC_MISS_sum"] > 0:
         der["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    if c.get("SQC_ICACHE_HITS") is not None and c.get("SQC_ICACHE_MISSES") is not None:
+        tot = c["SQC_ICACHE_HITS"] + c["SQC_ICACHE_MISSES"]
+        if tot > 0:
+            der["icache_hit_rate"] = c["SQC_ICACHE_HITS"] / tot
     if c.get("SQ_WAVES") and c.get("SQ_WAVE_CYCLES"):
         der["mean_wave_lifetime_cycles"] = 4.0 * c["SQ_WAVE_CYCLES"] / c["SQ_WAVES"]  # quad-cycles -> cycles
     insts = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD",
@@ -115,6 +136,7 @@ p = sub.add_parser("pmc")
 p.add_argument("fetch")
 p.add_argument("write")
 p.add_argument("out")
+p.add_argument("--rdreq", default=None, help="pass directory with TCC_EA0_RDREQ_{128B,64B,32B,}_sum")
 p.add_argument("--batch", type=int, required=True)
 p.add_argument("--grid", type=int, default=1024)
 p.add_argument("--dispatch", type=int, default=-1)
