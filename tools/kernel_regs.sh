@@ -13,14 +13,14 @@ import sys, re
 cur = {}
 rows = []
 for line in sys.stdin:
-    m = re.match(r'\s+\.(name|sgpr_count|vgpr_count|sgpr_spill_count|vgpr_spill_count|private_segment_fixed_size|group_segment_fixed_size):\s+(\S+)', line)
+    m = re.match(r'\s+\.(name|sgpr_count|vgpr_count|agpr_count|sgpr_spill_count|vgpr_spill_count|private_segment_fixed_size|group_segment_fixed_size):\s+(\S+)', line)
     if not m: continue
     k, v = m.groups()
     if k == 'name': cur = {'name': v}; rows.append(cur)
     else: cur[k] = v
 for r in rows:
     if 'search' in r['name'] and 'k_' not in r['name']:
-        print(r['name'][:60], 'vgpr', r.get('vgpr_count'), 'sgpr', r.get('sgpr_count'), 'sgpr_spill', r.get('sgpr_spill_count'),
+        print(r['name'][:60], 'vgpr', r.get('vgpr_count'), 'agpr', r.get('agpr_count'), 'sgpr', r.get('sgpr_count'), 'sgpr_spill', r.get('sgpr_spill_count'),
               'vgpr_spill', r.get('vgpr_spill_count'), 'scratch', r.get('private_segment_fixed_size'), 'lds', r.get('group_segment_fixed_size'))
 "
 rm -rf $T
