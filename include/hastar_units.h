@@ -5,8 +5,8 @@
  *
  * Every call runs on the HIP device `device` (gfx950); there is no CPU path: without a
  * device each call returns HASTAR_EDEVICE.  Host buffers in and out.  float is bit-exact
- * with the reference (glibc float libm ports); double uses the device's double libm for
- * the Dubins words (within ~1e-15 relative of glibc) and is bit-exact elsewhere.
+ * with the reference (glibc float libm ports); double too (ports of glibc 2.35's double
+ * sin/cos/atan2/acos, csrc/hastar_libm64.h).
  */
 #ifndef PATH_PLANNING_PKG_AMD_HASTAR_UNITS_H
 #define PATH_PLANNING_PKG_AMD_HASTAR_UNITS_H

@@ -1,7 +1,7 @@
 // Dubins.h — drop-in planning::Dubins<T> (reference include/path_planning_pkg/Dubins.h:
 // 21-60, lib/Dubins.cpp), computed on the MI355X through include/hastar_units.h.
 // T = float is bit-exact with the reference (the search kernel's glibc float ports);
-// T = double uses the device's double libm for the CSC words (within ~1e-15 relative).
+// T = double runs ports of glibc 2.35's double libm for the CSC words: bit-exact as well.
 // Like the reference object, the last call's word and parameters are kept (get_path_type).
 #ifndef DUBINS
 #define DUBINS

@@ -10,7 +10,7 @@
 //
 // Both instantiations of the reference exist (HybridAStar.cpp:285-286): T = float over
 // include/hastar.h (bit-exact with the reference), T = double over include/hastar_f64.h (the
-// GPU search in f64; tolerance parity: device f64 libm).  The ROS node runs
+// GPU search in f64 on ports of glibc 2.35's double libm: bit-exact).  The ROS node runs
 // float (local_planner.cpp:509) and compiles LocalPlanner<double> too (:378-500).
 // Differences a caller can observe:
 //   * a HIP/device failure throws std::runtime_error (the reference has no device to fail);

@@ -5,8 +5,8 @@
 //
 // Same constructor and generate_velocity_profile signature, so local_planner.cpp:164-165,
 // 323, 332, 451, 460 compile unchanged against this header.  Both instantiations of the
-// reference exist (VelocityGenerator.cpp:88-89): float (bit-exact) and double (device f64
-// libm: within 1e-12 relative of the reference).  Differences a caller can observe:
+// reference exist (VelocityGenerator.cpp:88-89): float and double, both bit-exact (the double
+// one on ports of glibc 2.35's hypot/atan2).  Differences a caller can observe:
 //   * an empty path (undefined behaviour in the reference) or a device failure throws
 //     std::runtime_error;
 //   * generate_velocity_profiles (not in the reference) profiles many paths in one launch;

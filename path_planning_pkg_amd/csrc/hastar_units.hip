@@ -7,10 +7,9 @@
 //                    of nodes (one thread per node) from the handle's offset tables.
 //
 // T = float runs the same bit-exact expressions as the search kernel (the glibc float
-// ports of glibc_mathf.h; the float Dubins reuses hastar_device.h).  T = double uses the
-// device's double libm: its sin/cos/atan2/acos are within an ulp or two of glibc's but not
-// always identical, so double results match the reference to ~1e-15 relative (tests pin
-// them against the reference's own double golden vectors, printed at %g precision).
+// ports of glibc_mathf.h; the float Dubins reuses hastar_device.h).  T = double runs the
+// ports of glibc 2.35's double sin/cos/atan2/acos (hastar_libm64.h), the functions the host's
+// libm dispatches to, so double results are bit-identical to the reference's too.
 #include <hip/hip_runtime.h>
 #include "hastar_device.h"
 #include "hastar_units_dev.h"
@@ -29,10 +28,10 @@ template <> struct UM<float> {
   __device__ static int bin(float h, float prec) { return heading_bin(h, prec); }
 };
 template <> struct UM<double> {
-  __device__ static double sin(double x) { return ::sin(x); }
-  __device__ static double cos(double x) { return ::cos(x); }
-  __device__ static double atan2(double y, double x) { return ::atan2(y, x); }
-  __device__ static double acos(double x) { return ::acos(x); }
+  __device__ static double sin(double x) { return gm64::sin(x); }
+  __device__ static double cos(double x) { return gm64::cos(x); }
+  __device__ static double atan2(double y, double x) { return gm64::atan2(y, x); }
+  __device__ static double acos(double x) { return gm64::acos(x); }
   __device__ static double wrap(double a) { return wrap_pi_d(a); }
   // common.h:31-36 with T = double: round(h / prec) * prec, then (r + pi) / prec truncated
   __device__ static int bin(double h, double prec) {
