@@ -337,6 +337,10 @@ def main():
                    "astar_pops": last.stats["astar_pops"].copy(),
                    "warm": np.array([p.timing() for p in planners], dtype=np.float64)}
         progress("timed steps done")
+        # the last timed replan of the same stratified sample, paths included, for the oracle's
+        # replay of the whole call sequence (the node map's f values persist across reset, so a
+        # later replan is not the first one again)
+        last_sample = {i: last.result(i) for i in cold_sample} if cold_sample is not None else None
         vel_prof = velocity_profile_phase(gpu, last, device, vels)  # before any other find_path
         # the outcome arrays of the last timed step outlive the later steps on the same buffers
         # (paths are not kept: only the velocity phase above reads them)
@@ -452,7 +456,8 @@ def main():
             # not the predicted-costliest head of the GPU batch), latency queries first
             sample = lat_ids + [i for i in np.argsort(qids, kind="stable") if i not in lat_ids]
             progress("parity sample")
-            out["parity_sample"] = parity_sample(cfgs, cold_sample, [qids[i] for i in sorted(cold_sample)])
+            out["parity_sample"] = parity_sample(cfgs, cold_sample, [qids[i] for i in sorted(cold_sample)],
+                                                 last_sample, args.warmup + args.steps)
             progress("cpu baseline")
             cb = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps, lat_ids, sample)
             out["cpu_baseline"] = cb
@@ -884,42 +889,61 @@ def cpu_baseline_cfg5(pairs, budget_s, ticks):
              f"tick_ms_{T}_threads": float(np.mean([makespan(m, T) for m in per_tick])) if n else None}, replay)
 
 
-def parity_sample(cfgs, gpu, qids):
-    """Bit-exact check at the bench's own size, outside the timed region: the first (cold) step's
-    result of a stratified sample of the batch (`gpu`: planner index -> result, every 64th query
-    plus the 8 longest) against the oracle's reset + find_path on the same maps, on the host's
-    threads: success, cost bits, the search statistics and digests, path and curvature bits."""
+def parity_sample(cfgs, gpu, qids, gpu_last=None, replans=1):
+    """Bit-exact check at the bench's own size, outside the timed region: a stratified sample of
+    the batch (`gpu`: planner index -> result of the first, cold step; every 64th query plus the 8
+    longest) against the oracle on the same maps, on the host's threads.  The oracle replays the
+    GPU planner's whole call sequence, `replans` x (reset + find_path); its first replan is compared
+    with `gpu` and its last with `gpu_last` (the last timed step): success, cost bits, the search
+    statistics and digests, path and curvature bits."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle.pyoracle import OraclePlanner
     from tests.scenarios import drive
     idx = sorted(gpu)
+    replans = replans if gpu_last is not None else 1
 
     def run(i):
         o = OraclePlanner(cfgs[i][0])
         drive(o, cfgs[i][1])
-        o.reset()
-        r = o.find_path(cfgs[i][1]["vel"], cfgs[i][1]["start"])
+        out = []
+        for k in range(replans):
+            o.reset()
+            r = o.find_path(cfgs[i][1]["vel"], cfgs[i][1]["start"])
+            if k == 0 or k == replans - 1:
+                out.append(r)
         o.close()
-        return r
+        return out
 
     t0 = time.perf_counter()
     with ThreadPoolExecutor(cpu_threads()) as ex:
         res = list(ex.map(run, idx))
     keys = ("pops", "successors", "astar_pops", "astar_searches", "shots", "closed_size", "pop_digest",
             "closed_digest", "via_shot")
-    bad = []
-    for i, q, o in zip(idx, qids, res):
-        g = gpu[i]
-        same = (g["ok"] == o["ok"] and np.float32(g["cost"]).tobytes() == np.float32(o["cost"]).tobytes()
+
+    def same(g, o):
+        return (g["ok"] == o["ok"] and np.float32(g["cost"]).tobytes() == np.float32(o["cost"]).tobytes()
                 and all(g["stats"][k] == o["stats"][k] for k in keys)
                 and g["path"].tobytes() == o["path"].tobytes() and g["curvature"].tobytes() == o["curvature"].tobytes())
-        if not same:
+
+    bad, bad_last = [], []
+    for i, q, o in zip(idx, qids, res):
+        if not same(gpu[i], o[0]):
             bad.append(int(q))
-    return {"queries": len(idx), "bit_exact": not bad, "mismatched_queries": bad[:16],
-            "pops_checked": int(sum(int(gpu[i]["stats"]["pops"]) for i in idx)),
-            "path_poses_checked": int(sum(len(gpu[i]["path"]) for i in idx)), "oracle_s": time.perf_counter() - t0,
-            "note": "first (cold) step of every 64th query and the 8 longest, against the oracle's reset + "
-                    "find_path: success, cost, statistics, pop/closed digests, path and curvature bits"}
+        if gpu_last is not None and not same(gpu_last[i], o[-1]):
+            bad_last.append(int(q))
+    out = {"queries": len(idx), "bit_exact": not bad and not bad_last, "mismatched_queries": bad[:16],
+           "pops_checked": int(sum(int(gpu[i]["stats"]["pops"]) for i in idx)),
+           "path_poses_checked": int(sum(len(gpu[i]["path"]) for i in idx)), "oracle_s": time.perf_counter() - t0,
+           "note": "first (cold) step of every 64th query and the 8 longest, against the oracle's reset + "
+                   "find_path: success, cost, statistics, pop/closed digests, path and curvature bits"}
+    if gpu_last is not None:
+        out["last_timed_step"] = {
+            "replans_replayed": replans, "bit_exact": not bad_last, "mismatched_queries": bad_last[:16],
+            "pops_checked": int(sum(int(gpu_last[i]["stats"]["pops"]) for i in idx)),
+            "path_poses_checked": int(sum(len(gpu_last[i]["path"]) for i in idx)),
+            "note": "the same queries' last timed replan against the oracle's replay of every replan before it "
+                    "(reset + find_path each; warm-up and timed steps): the same fields"}
+    return out
 
 
 def cpu_baseline(cfgs, gpu_results, budget_s, replans, lat_ids, sample=None):

@@ -76,18 +76,32 @@ def test_parity_sample_compares_every_field():
     assert bench.parity_sample(cfgs, bent, [0, 1, 2])["mismatched_queries"] == [2]
 
 
-def test_cfg5_parity_compares_every_pair_and_tick():
+def test_parity_sample_replays_every_replan_for_the_last_step():
+    """With the last timed step given, the oracle replays reset + find_path `replans` times (the
+    node map's f values persist across reset, HybridAStar.cpp:49-52) and compares its last replan
+    with it; a one-bit difference in the last step's path fails that check alone."""
     import numpy as np
     import bench
-    r = dict(ok=True, cost=1.5, path=np.ones((3, 3), np.float32), curvature=np.zeros(3, np.float32),
-             stats=dict(pops=7, pop_digest=11, closed_digest=13))
-    k = bench.tick_key(r)
-    g = [[k, k], [k, k]]
-    out = bench.cfg5_parity(g, {0: [k, k], 1: [k, k]}, [5, 6])
-    assert out["bit_exact"] and out["searches"] == 4 and out["pops_checked"] == 28
-    r2 = dict(r, path=r["path"].copy())
-    r2["path"][1, 2] = np.nextafter(np.float32(1), np.float32(2))
-    out = bench.cfg5_parity(g, {0: [k, k], 1: [k, bench.tick_key(r2)]}, [5, 6])
-    assert not out["bit_exact"] and out["mismatched_pair_ticks"] == [[6, 1]]
-    # a pair the oracle did not replay (budget) leaves the readout partial, never "bit_exact"
-    assert not bench.cfg5_parity(g, {0: [k, k]}, [5, 6])["bit_exact"]
+    from oracle.pyoracle import OraclePlanner
+    from tests.scenarios import drive, synthetic_ref
+    cfgs = [synthetic_ref(256, 36, 20, s) for s in (1, 3)]
+    first, fourth = {}, {}
+    for i, (cfg, proto) in enumerate(cfgs):
+        o = OraclePlanner(cfg)
+        drive(o, proto)
+        for k in range(4):
+            o.reset()
+            r = o.find_path(proto["vel"], proto["start"])
+            if k == 0:
+                first[i] = r
+        fourth[i] = r
+        o.close()
+    r = bench.parity_sample(cfgs, first, [0, 1], fourth, 4)
+    assert r["bit_exact"] and r["last_timed_step"]["bit_exact"] and r["last_timed_step"]["replans_replayed"] == 4, r
+    p = fourth[1]["path"].copy()
+    p.view(np.uint32)[0, 0] ^= 1
+    bent = dict(fourth)
+    bent[1] = dict(fourth[1], path=p)
+    r = bench.parity_sample(cfgs, first, [7, 8], bent, 4)
+    assert r["mismatched_queries"] == [] and not r["bit_exact"], r
+    assert r["last_timed_step"]["mismatched_queries"] == [8], r
