@@ -285,6 +285,7 @@ def main():
     t0 = time.perf_counter()
     r0 = step()
     cold_s = time.perf_counter() - t0
+    cold_handoffs = planners[0].handoffs()
     progress("cold first step done")
     # the first step's outcome of a stratified sample (every 64th query and the 8 with the most
     # pops), paths included, for the bit-exact check against the oracle after the timed region
@@ -330,6 +331,8 @@ def main():
         balance["pool"] = planners[0].slots()
         balance["split_launch_ms"] = dict(zip(("head_start", "head_end", "bulk_start", "bulk_end"),
                                               planners[0].split_ms()))
+        # searches the last step's split launch moved from batch slots to free latency CUs
+        balance["handoffs"] = planners[0].handoffs()
         pool = balance["pool"]  # the library splits a batch over 4x the CU count (hastar_capi.cpp batch_shape)
         split_launch = (os.environ.get("HASTAR_SPLIT", "1") != "0" and pool["head_cus"] > 0
                         and B > 4 * (pool["resident_slots"] // max(pool["waves_per_cu"], 1)))
@@ -413,7 +416,7 @@ def main():
             "kernel_only_value": pops_all / elapsed * ms_per_step / avg_kernel_ms,
             "kernel_ms_per_step": [float(k) for k in kernel_ms],
             **({"step_diag": diag} if diag else {}),
-            "cold_first_step": {"value": cold_pops_all / cold_s, "ms": cold_s * 1e3,
+            "cold_first_step": {"value": cold_pops_all / cold_s, "ms": cold_s * 1e3, "handoffs": cold_handoffs,
                                 "note": "first launch of the batch: no longest-first history (the library orders the "
                                         "queue by its cold key: boxes near the start-goal route, hastar.h "
                                         "hastar_set_cost_hint); the device pool was reserved at setup "

@@ -46,6 +46,8 @@ int hastar_debug_head_arenas(hastar_handle h, long long* out3);
 /* the device's last split launch (hastar_find_path_batch of a large batch): ms from the timed
  * region's start to the head kernel's start and end, and to the bulk kernel's start and end */
 int hastar_debug_split(hastar_handle h, float* out4);
+/* searches the device's last split launch handed from batch-kernel slots to latency CUs */
+int hastar_debug_handoffs(hastar_handle h, int* out);
 /* resume arenas carved from idle slot arenas of the pool so far (process-wide count) */
 int hastar_debug_pooled_resumes(long long* out);
 /* The device's relaxed-mode arena pool: {arenas (= resident workgroups of a relaxed launch), MiB each}. */

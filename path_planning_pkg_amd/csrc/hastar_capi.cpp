@@ -181,6 +181,10 @@ struct DeviceCtx {
   hipStream_t head_st = nullptr, bulk_st = nullptr;
   hipEvent_t ev_fork = nullptr, ev_head = nullptr, ev_bulk = nullptr, ev_hs = nullptr, ev_bs = nullptr;
   float split_ms[4] = {0, 0, 0, 0};  // last split launch: head start / end, bulk start / end after ev0
+  // handoff board of split launches (HandoffBoard, hastar_layout.h): every pool and head arena
+  // descriptor points at it; enabled only while a split launch runs
+  HandoffBoard* d_board = nullptr;
+  int handoffs = 0;                  // searches the last split launch handed to latency CUs
   // map-update scratch (relocation target + claim table, raster hit counters)
   size_t scratch_cap = 0;
   float* tmp = nullptr;
@@ -482,9 +486,16 @@ int arenas_acquire(DeviceCtx& D, const ArenaReq& need, int n) {
     D.slab = nullptr;
     return fail(HASTAR_ENOMEM, "search arenas: hipMalloc of " + std::to_string(per * (size_t)n >> 20) + " MiB failed");
   }
+  if (!D.d_board) {
+    HIPCHK(dalloc(&D.d_board, 1));
+    HIPCHK(hipMemsetAsync(D.d_board, 0, sizeof(HandoffBoard), D.stream));
+  }
   std::vector<SlotArena> host(n);
   char* base = static_cast<char*>(D.slab);
-  for (int i = 0; i < n; ++i) HIPCHK(carve_arena(base + per * (size_t)i, r, lay, &host[i], D.stream));
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(carve_arena(base + per * (size_t)i, r, lay, &host[i], D.stream));
+    host[i].board = D.d_board;
+  }
   HIPCHK(dalloc(&D.d_arenas, (size_t)n));
   HIPCHK(hipMemcpyAsync(D.d_arenas, host.data(), (size_t)n * sizeof(SlotArena), hipMemcpyHostToDevice, D.stream));
   HIPCHK(hipStreamSynchronize(D.stream));
@@ -550,6 +561,7 @@ int head_acquire(DeviceCtx& D, int head, int span, int slots) {
                            : static_cast<char*>(D.slab) + D.arena_bytes * (size_t)b * k;
     HIPCHK(carve_arena(at, r, lay, &D.h_head[(size_t)b], D.stream));
     D.h_head[(size_t)b].pops_grant = (int)grant;
+    D.h_head[(size_t)b].board = D.d_board;
   }
   if (D.d_head) hipFree(D.d_head);
   D.d_head = nullptr;
@@ -1968,6 +1980,16 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
   // an explicit pop budget (0 = none: a search runs until the reference's loop would end)
   long long hard_pops = 0;
   if (const char* e = std::getenv("HASTAR_MAX_POPS_HARD")) hard_pops = std::atoll(e);
+  // a split launch's batch-kernel search is offered to free latency CUs after this many pops
+  // (DESIGN.md §4.1 "Handoff"): a remedy for a queue ordered without history, where the cold key
+  // can rank a long search far down the queue, onto a batch slot.  With the measured pops of
+  // the planners' last searches the longest ones start on the latency CUs, and handoffs measured
+  // 1 % slower (profiles/r05k_handoff_ab.jsonl): on only when more than an eighth of the batch
+  // has no history (HASTAR_HANDOFF_WARM=1: always)
+  int handoff_pops = 32768;
+  if (const char* e = std::getenv("HASTAR_HANDOFF_POPS")) handoff_pops = std::atoi(e);
+  const char* hw_env = std::getenv("HASTAR_HANDOFF_WARM");
+  if (!(hw_env && std::atoi(hw_env) != 0) && (long long)n_cold * 8 <= (long long)n) handoff_pops = 0;
   // every result starts as "not run" (a wave that parks a search stops taking work, so a
   // launch can end with queue entries nobody took)
   HIPCHK(hipMemsetAsync(DC.d_results, 0xff, (size_t)n * sizeof(SearchResult), st));
@@ -1993,6 +2015,19 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
           // `head` (pool arenas from max(head, hoff))
           const int init[4] = {head, 0, 0, 0};
           hipError_t e = hipMemcpyAsync(DC.d_next, init, sizeof(init), hipMemcpyHostToDevice, st);
+          // the handoff board: every entry empty, enabled with the offer threshold (pops) unless
+          // HASTAR_HANDOFF_POPS=0
+          if (e == hipSuccess) e = hipMemsetAsync(DC.d_board, 0, offsetof(HandoffBoard, entry), st);
+          if (e == hipSuccess && handoff_pops > 0) {
+            // the header alone (the words before `state`), staged like `init` above
+            alignas(16) unsigned char hdr[offsetof(HandoffBoard, state)] = {};
+            HandoffBoard* H = reinterpret_cast<HandoffBoard*>(hdr);
+            H->enabled = 1;
+            H->thr = handoff_pops;
+            H->n = std::min(DC.n_arenas, HANDOFF_CAP);
+            H->pool = DC.d_arenas;
+            e = hipMemcpyAsync(DC.d_board, hdr, sizeof(hdr), hipMemcpyHostToDevice, st);
+          }
           if (e == hipSuccess) e = hipEventRecord(DC.ev_fork, st);
           if (e == hipSuccess) e = hipStreamWaitEvent(DC.head_st, DC.ev_fork, 0);
           if (e == hipSuccess) e = hipStreamWaitEvent(DC.bulk_st, DC.ev_fork, 0);
@@ -2018,6 +2053,12 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
       }))
     return r;
   if (split1) {
+    // the board is read back and disabled before any other launch (resume passes run the
+    // batch kernel without it)
+    int hdr[6] = {0, 0, 0, 0, 0, 0};
+    HIPCHK(hipMemcpy(hdr, DC.d_board, sizeof(hdr), hipMemcpyDeviceToHost));
+    DC.handoffs = hdr[5];
+    HIPCHK(hipMemsetAsync(DC.d_board, 0, offsetof(HandoffBoard, state), st));
     hipEventElapsedTime(&DC.split_ms[0], DC.ev0, DC.ev_hs);
     hipEventElapsedTime(&DC.split_ms[1], DC.ev0, DC.ev_head);
     hipEventElapsedTime(&DC.split_ms[2], DC.ev0, DC.ev_bs);
@@ -2896,6 +2937,12 @@ int hastar_debug_relaxed_pool(hastar_handle h, long long* out2) {
 int hastar_debug_split(hastar_handle h, float* out4) {
   if (!h || !h->dc || !out4) return fail(HASTAR_EINVAL, "bad argument");
   for (int i = 0; i < 4; ++i) out4[i] = h->dc->split_ms[i];
+  return 0;
+}
+
+int hastar_debug_handoffs(hastar_handle h, int* out) {
+  if (!h || !h->dc || !out) return fail(HASTAR_EINVAL, "bad argument");
+  *out = h->dc->handoffs;
   return 0;
 }
 

@@ -1575,7 +1575,64 @@ __device__ void prep_helper(PrepL& pr, ApfStage& apfs, const PlannerDev* __restr
 // status), LOOP_PARKED (the arena cannot take one more pop) or LOOP_MIGRATE (LDS tree only:
 // its pool or the closed records are about to fill; the caller moves the tree to HBM and
 // continues there, at the same pop).
-constexpr int LOOP_DONE = 0, LOOP_PARKED = 1, LOOP_MIGRATE = 2;
+constexpr int LOOP_DONE = 0, LOOP_PARKED = 1, LOOP_MIGRATE = 2, LOOP_HANDOFF = 3;
+
+// ---- handoff of a long batch-kernel search to a free latency CU (HandoffBoard, hastar_layout.h)
+// Every board word another CU polls is accessed by agent-scope atomics (write-through, no stale
+// L1 copy); the search state itself (arena records, SearchResult, the planner's maps) is
+// published by the batch wave's agent-scope release before READY and read by the latency wave
+// after its agent-scope acquire (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ uint32_t ho_ld(GAS uint32_t* p) {
+  return __hip_atomic_load((uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ho_st(GAS uint32_t* p, uint32_t v) {
+  __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ho_ld64(GAS uint64_t* p) {
+  const uint32_t lo = ho_ld((GAS uint32_t*)p), hi = ho_ld((GAS uint32_t*)p + 1);
+  return ((uint64_t)hi << 32) | lo;
+}
+// the board of a split launch's batch-kernel wave, or null (no split launch, an arena without
+// a board, or an arena index past the board)
+__device__ __forceinline__ GAS HandoffBoard* ho_board(const SearchCtx& c) {
+  GAS HandoffBoard* hb = gp(c.A->board);
+  if (hb == nullptr || c.slot >= HANDOFF_CAP || hb->enabled == 0) return nullptr;
+  return hb;
+}
+// Batch kernel, at a pop boundary every 64 pops: offer the search once it has run thr pops;
+// true when a latency wave has claimed the offer (the caller parks the search for it).
+__device__ __forceinline__ bool ho_poll(SearchCtx& c) {
+  GAS HandoffBoard* hb = ho_board(c);
+  if (hb == nullptr || c.pops < (uint32_t)hb->thr) return false;
+  GAS uint32_t* st = &hb->state[c.slot];
+  const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)ho_ld(st));
+  if (v == HANDOFF_CLAIMED) return true;
+#ifndef BISECT_NOPOST
+  if (v == HANDOFF_EMPTY && c.lane == 0) {
+    GAS HandoffEntry* e = &hb->entry[c.slot];
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    ho_st((GAS uint32_t*)&e->t_start, (uint32_t)t);
+    ho_st((GAS uint32_t*)&e->t_start + 1, (uint32_t)(t >> 32));
+    ho_st((GAS uint32_t*)&e->slot, (uint32_t)c.slot);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the entry before its state
+    ho_st(st, HANDOFF_POSTED);
+    atomicAdd((int*)&hb->posted, 1);
+  }
+#endif
+  return false;
+}
+// Batch kernel, after a search that may have offered itself (not handed over): withdraw the
+// offer, or release a claimer that came too late.
+__device__ __forceinline__ void ho_withdraw(SearchCtx& c) {
+  GAS HandoffBoard* hb = ho_board(c);
+  if (hb == nullptr || c.pops < (uint32_t)hb->thr) return;
+  if (c.lane == 0) {
+    GAS uint32_t* st = &hb->state[c.slot];
+    const uint32_t old = atomicCAS((uint32_t*)st, HANDOFF_POSTED, HANDOFF_EMPTY);
+    if (old == HANDOFF_POSTED) atomicSub((int*)&hb->posted, 1);
+    else if (old == HANDOFF_CLAIMED) ho_st(st, HANDOFF_CANCELLED);
+  }
+}
 // Latency kernel, LDS tree: right after a pop, the HBM reads of the NEXT pop (the payload of the
 // tree's new leftmost node and its closed-set probe) are issued, so they arrive during the
 // expansion.  The next pop takes them when its node is that one (no successor went before it,
@@ -1636,6 +1693,11 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
       if (kLdsOuter) return LOOP_MIGRATE;  // the HBM loop continues (and parks if it must)
       parked = true;
       break;
+    }
+    if constexpr (!kPrep) {  // batch kernel: a free latency CU may take this search over
+#ifndef BISECT_NOPOLL
+      if ((c.pops & 63u) == 0u && ho_poll(c)) return LOOP_HANDOFF;
+#endif
     }
     STAMP_T tp = STAMP_NOW();
     const int b = o3.begin();
@@ -2048,7 +2110,11 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
     c.o3.reset_cache();
     code = search_loop<CF, false, kWide>(c, c.o3, apfs, alds, S, hard_pops, closed_lim, open_lim, A.open3_cap, pr);
   }
-  const bool parked = code == LOOP_PARKED;
+  const bool handoff = code == LOOP_HANDOFF;  // (batch kernel only) a latency wave takes it over
+  const bool parked = code == LOOP_PARKED || handoff;
+  if constexpr (!kWide) {
+    if (!handoff) ho_withdraw(c);
+  }
   counter = S.counter;
   interval = S.interval;
   shot_allowed = S.shot_allowed;
@@ -2077,17 +2143,19 @@ __device__ __forceinline__ bool search_one(SearchCtx& c, ApfStage& apfs, AStarLd
       R->n_closed3 = c.n_closed3;
       R->ps3_next = c.ps3.next;
       R->ps3_free = c.ps3.free;
-      // the next capacity step beyond this arena's (a head arena's grant may exceed several)
+      // the next capacity step beyond this arena's (a head arena's grant may exceed several);
+      // a handoff is no capacity step: the search continues in this arena with its capacity
       int np = parks + 1;
       if constexpr (kWide)
         while (np < 12 && ((long long)P.arena_pops << (2 * np)) <= pcap) ++np;
-      R->parks = np;
+      R->parks = handoff ? parks : np;
       R->park_arena = c.slot;
       R->ok = 0;
       R->path_len = 0;
-      R->status = SEARCH_PARKED;
+      R->status = handoff ? SEARCH_HANDOFF : SEARCH_PARKED;
     }
     wave_lds_sync();
+    if (handoff) c.status = SEARCH_HANDOFF;  // the kernel publishes it (READY) and stops
     return true;
   }
   if (c.status != 0) ok = 0;
@@ -2220,6 +2288,9 @@ void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners, 
   c.cost_only = true;
   c.gen3 = gp(A.gens)[0];
   c.gen2 = gp(A.gens)[1];
+  c.status = 0;
+  GAS HandoffBoard* const hb = ho_board(c);  // a split launch's board: this wave counts as running
+  if (hb != nullptr && c.lane == 0) atomicAdd((int*)&hb->bulk_active, 1);
   for (bool first = true;; first = false) {
     int q = 0;
     if (first && head) {
@@ -2234,12 +2305,25 @@ void hastar_search_kernel(const PlannerDev* __restrict__ descs, int n_planners, 
     if (q < n_prio) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(0);
     c.P = descs + order[q];
-    // a parked search keeps its state in this wave's arena: the wave takes no more work
-    if (search_one<NarrowA, false>(c, apfs[w], alds[w], nullptr, hard_pops, false)) break;
+    // a parked search keeps its state in this wave's arena: the wave takes no more work (a
+    // handed-over one too: the latency wave continues it in this arena)
+    if (search_one<NarrowA, false>(c, apfs[w], alds[w], nullptr, hard_pops, false)) {
+      if (c.status == SEARCH_HANDOFF) {
+        // publish the parked state (arena records, SearchResult, the planner's maps) and the
+        // planner: READY.  The latency wave copies the records out of this arena, which no
+        // other search uses in this launch: the wave takes no more work
+        if (c.lane == 0) ho_st((GAS uint32_t*)&hb->entry[c.slot].pidx, (uint32_t)order[q]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (c.lane == 0) ho_st(&hb->state[c.slot], HANDOFF_READY);
+      }
+      break;
+    }
   }
   if (c.lane == 0) {
     gp(A.gens)[0] = c.gen3;
     gp(A.gens)[1] = c.gen2;
+    if (hb != nullptr) atomicSub((int*)&hb->bulk_active, 1);
   }
 }
 
@@ -2262,6 +2346,65 @@ using WideLds = WideLdsT<WideA>;
 static_assert(sizeof(WideLds) <= 163840, "the latency kernel's LDS must fit one CU");
 // Wave 0 runs the searches; waves 1 .. PREP_HELPERS precompute expansions for it (prep_helper).
 constexpr int WIDE_WAVES = 1 + PREP_HELPERS;
+// One wave copies `bytes` (a multiple of 16) of 16-B-aligned records, 4 x 16 B per lane in flight.
+__device__ __forceinline__ void copy_records(GAS void* dst, const GAS void* src, size_t bytes, int lane) {
+  GAS v4i* d = (GAS v4i*)dst;
+  const GAS v4i* s = (const GAS v4i*)src;
+  const size_t n = bytes / 16;
+  size_t i = (size_t)lane;
+  for (; i + 192 < n; i += 256) {
+    const v4i a = s[i], b = s[i + 64], e = s[i + 128], f = s[i + 192];
+    d[i] = a;
+    d[i + 64] = b;
+    d[i + 128] = e;
+    d[i + 192] = f;
+  }
+  for (; i < n; i += 64) d[i] = s[i];
+}
+
+// Latency kernel of a split launch: claim the oldest search a batch-kernel wave offers
+// (HandoffBoard) and wait for its wave to park it (READY).  Returns the entry (= the arena the
+// search's state stays in), or -1: no offer, or the search ended before its wave saw the claim.
+__device__ __forceinline__ int ho_claim(const SearchCtx& c, GAS HandoffBoard* hb) {
+  if (ho_ld((GAS uint32_t*)&hb->posted) == 0u) return -1;
+  const int n = min(hb->n, HANDOFF_CAP);
+  uint64_t key = ~0ull;  // (offer time << 12 | entry) of this lane's oldest offer
+  for (int i = c.lane; i < n; i += 64) {
+    if (ho_ld(&hb->state[i]) == HANDOFF_POSTED) {
+      const uint64_t k = (ho_ld64((GAS uint64_t*)&hb->entry[i].t_start) << 12) | (uint64_t)i;
+      key = k < key ? k : key;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)key, o, 64), hi = __shfl_xor((uint32_t)(key >> 32), o, 64);
+    const uint64_t k = ((uint64_t)hi << 32) | lo;
+    key = k < key ? k : key;
+  }
+  const uint32_t klo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)key);
+  const uint32_t khi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(key >> 32));
+  if (klo == 0xffffffffu && khi == 0xffffffffu) return -1;
+  const int i = (int)(klo & 4095u);
+  GAS uint32_t* st = &hb->state[i];
+  uint32_t got = 0;
+  if (c.lane == 0) got = atomicCAS((uint32_t*)st, HANDOFF_POSTED, HANDOFF_CLAIMED);
+  got = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)got, 0, 64));
+  if (got != HANDOFF_POSTED) return -1;  // withdrawn or taken meanwhile
+  if (c.lane == 0) atomicSub((int*)&hb->posted, 1);
+  // the batch wave answers within 64 pops: READY (parked for us) or CANCELLED (it ended first)
+  uint32_t v;
+  for (;;) {
+    v = (uint32_t)__builtin_amdgcn_readfirstlane((int)ho_ld(st));
+    if (v != HANDOFF_CLAIMED) break;
+    __builtin_amdgcn_s_sleep(16);
+  }
+  if (v != HANDOFF_READY) {
+    if (c.lane == 0) atomicCAS((uint32_t*)st, HANDOFF_CANCELLED, HANDOFF_EMPTY);
+    return -1;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return i;
+}
+
 template <class CF>
 __global__ __launch_bounds__(64 * WIDE_WAVES) void hastar_search_wide_kernel(
     const PlannerDev* __restrict__ descs, int n_planners, const SlotArena* __restrict__ arenas,
@@ -2306,19 +2449,55 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void hastar_search_wide_kernel(
   } else {
     // first_static: workgroup b runs queue entry b first (the head of a longest-first queue
     // split over this kernel and the batch kernel, whose counter starts after the head)
+    // a split launch's latency CU prefers a long search the batch kernel offers (HandoffBoard)
+    // to a new one from the queue, and once the queue is drained it waits for offers while
+    // batch-kernel waves still run (bounded: 30 s without one, so every wave reaches its end)
+    GAS HandoffBoard* const hb = first_static ? gp(A.board) : nullptr;
+    const bool handoffs = hb != nullptr && hb->enabled != 0;
     for (bool first = true;; first = false) {
-      int q = 0;
+      int q = 0, ho = -1;
       if (first && first_static) {
         q = (int)blockIdx.x;
       } else {
-        if (c.lane == 0) q = atomicAdd(next, 1);
-        q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
+        if (handoffs) ho = ho_claim(c, hb);
+        if (ho < 0) {
+          if (c.lane == 0) q = atomicAdd(next, 1);
+          q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
+          if (q >= n_planners && handoffs) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+              ho = ho_claim(c, hb);
+              if (ho >= 0) break;
+              if (__builtin_amdgcn_readfirstlane((int)ho_ld((GAS uint32_t*)&hb->bulk_active)) <= 0) break;
+              if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) break;
+              __builtin_amdgcn_s_sleep(64);
+            }
+          }
+          if (ho < 0 && q >= n_planners) break;
+        }
       }
-      if (q >= n_planners) break;
-      const int pi = order[q];
+      int pi;
+      if (ho >= 0) {
+        // the handed-over search: its open-tree nodes and closed records (the parked state,
+        // SearchResult) are copied by index into this wave's arena, as a host resume copies
+        // them, and it continues here in resume mode
+        pi = __builtin_amdgcn_readfirstlane((int)ho_ld((GAS uint32_t*)&hb->entry[ho].pidx));
+        const GAS SlotArena* src = gp(hb->pool) + ho;
+        const GAS SearchResult* R = gp(descs[pi].result);
+        copy_records(gp(A.open3), gp(src->open3), (size_t)R->ps3_next * sizeof(Node3), lane);
+        copy_records(gp(A.closed3), gp(src->closed3), (size_t)R->n_closed3 * sizeof(Closed3), lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every load of the batch arena is back
+        if (lane == 0) {
+          ho_st(&hb->state[ho], HANDOFF_COPIED);
+          atomicAdd((int*)&hb->handoffs, 1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the copies before the search's loads
+      } else {
+        pi = order[q];
+      }
       c.P = descs + pi;
       if (lane == 0) tbl->pidx = pi;
-      if (search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, false, dbg, pr)) break;
+      if (search_one<CF, true>(c, W.apfs, W.alds, &W.ol, hard_pops, ho >= 0, dbg, pr)) break;
     }
   }
   if (c.lane == 0) {

@@ -94,6 +94,38 @@ constexpr int NSTAMP = 40;
 // Search status codes of SearchResult::status besides 0 / HASTAR_E* (host-side only).
 constexpr int SEARCH_NOT_RUN = -1;  // the host's sentinel: no wave took this planner
 constexpr int SEARCH_PARKED = 1;    // the arena filled up at a pop boundary: state kept for a resume
+constexpr int SEARCH_HANDOFF = 2;   // (in flight only) a bulk wave handed the search to a latency CU
+
+// Handoff board of a split launch ("Handoff"): a batch-kernel wave whose search
+// has run `thr` pops offers it (POSTED, in the entry of its arena index); a latency-kernel wave
+// that is free claims the oldest offer (CLAIMED); the batch wave parks the search at its next
+// check (every 64 pops) exactly as a capacity park does, in its own arena, and publishes it
+// (READY) and takes no more work; the latency wave copies the parked records into its own arena
+// (COPIED) and continues the search there in resume mode, as a host resume would.  A search
+// that ends before its wave sees the claim is withdrawn (CANCELLED; the latency wave empties the
+// entry).  No side waits for the other except a claimer for its claimed entry, answered within
+// 64 pops or at the search's end.
+constexpr uint32_t HANDOFF_EMPTY = 0, HANDOFF_POSTED = 2, HANDOFF_CLAIMED = 3, HANDOFF_READY = 4,
+                   HANDOFF_CANCELLED = 5, HANDOFF_COPIED = 6;
+constexpr int HANDOFF_CAP = 4096;  // entries (arena indices 0 .. HANDOFF_CAP-1 can offer)
+struct SlotArena;
+struct alignas(16) HandoffEntry {
+  unsigned long long t_start;      // when the search was offered (s_memrealtime): claims take the oldest
+  int slot;                        // the batch wave's arena index (the search's state stays there)
+  int pidx;                        // the planner (index into the launch's descriptors), set at READY
+};
+struct HandoffBoard {
+  int enabled;      // 1 only while a split launch runs (the host sets it per launch)
+  int thr;          // pops after which a batch-kernel search is offered
+  int posted;       // entries in state POSTED (a claimer scans only when > 0)
+  int bulk_active;  // batch-kernel waves still running (latency waves wait for offers until 0)
+  int n;            // entries in use (the pool's arena count)
+  int handoffs;     // searches handed over in this launch (diagnostic)
+  const SlotArena* pool;  // the pool's arena descriptors (entry slot s = pool + s)
+  int pad[8];
+  uint32_t state[HANDOFF_CAP];
+  HandoffEntry entry[HANDOFF_CAP];
+};
 
 // Per-search result block (written by the search kernel, read by the host).
 // A search whose arena cannot take one more pop PARKS (status SEARCH_PARKED): the open tree
@@ -215,6 +247,7 @@ struct SlotArena {
   float* dub_xyh; float* dub_curv; int dub_cap; int pad5;
   int* out_chain;   int chain_cap;   int pad6;
   int* prevl;       // {prev link, g bits} of the LDS-resident A* tree nodes (2 x A_CAP)
+  HandoffBoard* board;  // the device's handoff board (pool and head arenas; null elsewhere)
 };
 
 // Scratch of one planner in the RELAXED (non-parity) search mode (hastar_relaxed.hip,

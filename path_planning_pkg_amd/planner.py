@@ -85,6 +85,7 @@ def load_library():
     L.hastar_debug_head_arenas.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_hw_id.argtypes = [vp, ip]
     L.hastar_debug_split.argtypes = [vp, fp]
+    L.hastar_debug_handoffs.argtypes = [vp, C.POINTER(C.c_int)]
     L.hastar_debug_relaxed_pool.argtypes = [vp, C.POINTER(C.c_longlong)]
     L.hastar_debug_pooled_resumes.argtypes = [C.POINTER(C.c_longlong)]
     L.hastar_velocity_profile_batch.argtypes = [C.c_int, C.POINTER(HastarVelocityParams), C.c_int,
@@ -404,6 +405,12 @@ class HybridAStar:
         out = np.zeros(4, np.float32)
         _check(load_library().hastar_debug_split(self.h, fptr(out)))
         return [float(v) for v in out]
+
+    def handoffs(self):
+        """Searches the device's last split launch handed from batch-kernel slots to latency CUs."""
+        out = C.c_int(0)
+        _check(load_library().hastar_debug_handoffs(self.h, C.byref(out)))
+        return int(out.value)
 
     def relaxed_pool(self):
         """The device's relaxed-mode arena pool: (arenas, MiB per arena)."""

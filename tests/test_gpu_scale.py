@@ -217,6 +217,40 @@ def test_split_launch_head_arenas(gpu, oracle_lib, monkeypatch):
     assert parks[3][1]["n"] == 0, parks                               # released by the unsplit launch
 
 
+@pytest.mark.parametrize("max_pops", [0, 256])
+def test_split_launch_handoff(gpu, oracle_lib, monkeypatch, max_pops):
+    """Handoff (HandoffBoard): with HASTAR_HANDOFF_POPS=64 every batch-kernel
+    search past 64 pops is offered to the latency CUs, which claim offers as they come free; the
+    claimed searches park at their next 64-pop check, are copied into the latency wave's arena and
+    continue there in resume mode.  Every result is the oracle's, bit for bit, searches were
+    handed over, and a second call on the same pool (planners with history: HASTAR_HANDOFF_WARM
+    keeps handoffs on) agrees too.  max_pops = 256: capacity parks (and their host resumes) on
+    top of the handoffs (offers at 64, 128 and 192 pops come before the first park)."""
+    monkeypatch.setenv("HASTAR_WIDE", "0")
+    monkeypatch.setenv("HASTAR_SPLIT", "1")
+    monkeypatch.setenv("HASTAR_HANDOFF_POPS", "64")
+    monkeypatch.setenv("HASTAR_HANDOFF_WARM", "1")  # the second call has history: handoffs stay on
+    cases = [synthetic(256, 36, 10 + (s % 4) * 10, s) for s in range(1, 49)] + [synthetic(512, 72, 50, 1)]
+    gs, os_ = [], []
+    for cfg, proto in cases:
+        if max_pops:
+            cfg.values["max_pops"] = max_pops
+        g, o = _pair(gpu, oracle_lib, cfg, proto)
+        gs.append(g)
+        os_.append(o)
+    vels, starts = [c[1]["vel"] for c in cases], [c[1]["start"] for c in cases]
+    handed = []
+    for rep in range(2):
+        for g, o in zip(gs, os_):
+            g.reset()
+            o.reset()
+        res, _ = gpu.find_path_batch(gs, vels, starts, cap=8192)
+        for i, ((cfg, proto), o) in enumerate(zip(cases, os_)):
+            compare_results(res[i], o.find_path(proto["vel"], proto["start"]), f"handoff, call {rep}, planner {i}")
+        handed.append(gs[0].handoffs())
+    assert max(handed) > 0, handed
+
+
 @pytest.mark.parametrize("wide", KERNELS)
 def test_cfg3_survey_reference_cases(gpu, oracle_lib, monkeypatch, wide):
     """The survey's own cases, 256² to 2048² including cfg3 seeds 1 and 3 (std::mt19937 inputs,
