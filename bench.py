@@ -176,6 +176,9 @@ def parse_args(argv=None):
     ap.add_argument("--max-astar-nodes", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--parity-all", action="store_true",
+                    help="check EVERY query's cold step against the oracle (success, cost bits, statistics, "
+                         "pop/closed digests; about a minute of 16 host threads at cfg3)")
     ap.add_argument("--step-diag", action="store_true",
                     help="per-step schedule diagnostics in the JSON line (reads every search's timing per step)")
     ap.add_argument("--latency-queries", type=int, default=3)
@@ -292,6 +295,7 @@ def main():
     # (host-side bookkeeping of the bench, outside the step's time)
     strat = sorted(set(range(0, B, 64)) | set(np.argsort(-r0.stats["pops"], kind="stable")[:8].tolist()))
     cold_sample = {i: r0.result(i) for i in strat} if (rank == 0 and not args.no_cpu_baseline) else None
+    cold_all = (r0.stats.copy(), r0.cost.copy(), r0.ok.copy()) if (rank == 0 and args.parity_all) else None
     cold_pops = int(r0.stats["pops"].sum())
     cold_s, cold_pops_all = reduce_over_ranks(dist, cold_s, cold_pops, f"cuda:{device}")
     for _ in range(max(args.warmup - 1, 0)):
@@ -461,6 +465,9 @@ def main():
             progress("parity sample")
             out["parity_sample"] = parity_sample(cfgs, cold_sample, [qids[i] for i in sorted(cold_sample)],
                                                  last_sample, args.warmup + args.steps)
+            if cold_all is not None:
+                progress("parity of every query")
+                out["parity_all"] = parity_all(cfgs, *cold_all, qids)
             progress("cpu baseline")
             cb = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps, lat_ids, sample)
             out["cpu_baseline"] = cb
@@ -947,6 +954,36 @@ def parity_sample(cfgs, gpu, qids, gpu_last=None, replans=1):
             "note": "the same queries' last timed replan against the oracle's replay of every replan before it "
                     "(reset + find_path each; warm-up and timed steps): the same fields"}
     return out
+
+
+def parity_all(cfgs, stats, cost, ok, qids):
+    """Every query of the batch (`--parity-all`): the first (cold) step's outcome against the
+    oracle's reset + find_path on the same maps, on the host's threads: success, cost bits and
+    every statistic and digest (paths: parity_sample's stratified subset)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle.pyoracle import OraclePlanner
+    from tests.scenarios import drive
+    keys = ("pops", "successors", "astar_pops", "astar_searches", "shots", "closed_size", "pop_digest",
+            "closed_digest", "via_shot")
+
+    def run(i):
+        o = OraclePlanner(cfgs[i][0])
+        drive(o, cfgs[i][1])
+        o.reset()
+        r = o.find_path(cfgs[i][1]["vel"], cfgs[i][1]["start"])
+        o.close()
+        same = (bool(ok[i]) == bool(r["ok"]) and np.float32(cost[i]).tobytes() == np.float32(r["cost"]).tobytes()
+                and all((int(stats[k][i]) - int(r["stats"][k])) % (1 << 64) == 0 for k in keys))
+        return same, int(r["stats"]["pops"])
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cpu_threads()) as ex:
+        res = list(ex.map(run, range(len(cfgs))))
+    bad = [int(qids[i]) for i, (same, _) in enumerate(res) if not same]
+    return {"queries": len(cfgs), "bit_exact": not bad, "mismatched_queries": bad[:16], "n_mismatched": len(bad),
+            "pops_checked": int(sum(p for _, p in res)), "oracle_s": time.perf_counter() - t0,
+            "note": "every query's first (cold) step against the oracle's reset + find_path: success, cost bits, "
+                    "statistics, pop/closed digests"}
 
 
 def cpu_baseline(cfgs, gpu_results, budget_s, replans, lat_ids, sample=None):

@@ -105,3 +105,30 @@ def test_parity_sample_replays_every_replan_for_the_last_step():
     r = bench.parity_sample(cfgs, first, [7, 8], bent, 4)
     assert r["mismatched_queries"] == [] and not r["bit_exact"], r
     assert r["last_timed_step"]["mismatched_queries"] == [8], r
+
+
+def test_parity_all_checks_every_query():
+    """bench.parity_all (--parity-all): every query's cold-step statistics, digests (compared
+    modulo 2^64, whatever the integer width they arrive in), success and cost bits."""
+    import numpy as np
+    import bench
+    from oracle.pyoracle import OraclePlanner
+    from tests.scenarios import drive, synthetic_ref
+    cfgs = [synthetic_ref(256, 36, 20, s) for s in (1, 2)]
+    keys = ("pops", "successors", "astar_pops", "astar_searches", "shots", "closed_size", "pop_digest",
+            "closed_digest", "via_shot")
+    st = np.zeros(2, dtype=[(k, "i8") for k in keys])
+    cost, ok = np.zeros(2, np.float32), np.zeros(2, np.int32)
+    for i, (cfg, proto) in enumerate(cfgs):
+        o = OraclePlanner(cfg)
+        drive(o, proto)
+        o.reset()
+        r = o.find_path(proto["vel"], proto["start"])
+        o.close()
+        for k in keys:
+            st[k][i] = np.uint64(r["stats"][k]).astype(np.int64)
+        cost[i], ok[i] = r["cost"], r["ok"]
+    assert bench.parity_all(cfgs, st, cost, ok, [5, 6])["bit_exact"]
+    st["closed_digest"][1] ^= 1
+    r = bench.parity_all(cfgs, st, cost, ok, [5, 6])
+    assert r["mismatched_queries"] == [6] and r["n_mismatched"] == 1
