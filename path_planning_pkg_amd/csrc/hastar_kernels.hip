@@ -693,19 +693,111 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
 }
 
 // insert (AStar.cpp:172-183) into the LDS tree: rank-decided unless shape-dependent
+// ---- deferred inner tree ------------------------------------------------------------
+// An inner search keeps only its f-ordered ring while no shape-dependent event has happened:
+// the pop takes the ring's first node (the tree's leftmost), and an insert's position comes
+// from its rank neighbours, so the red-black links are not needed.  Each tree operation is
+// logged instead ({node, insert flag} and its rank neighbours {pred, at}; the pop's and the
+// expansion's entries in lanes 0.., stored to the arena's open2 area at the end of the pop).
+// At the first event that needs the tree (a find or insert walk, a migration to HBM, or a full
+// log) the log is replayed into an empty tree: the same libstdc++ link / erase calls in the
+// same order give the same shape, so results are identical.  Searches that end without an
+// event never build their tree.  The replay rewrites the links, which also thread the pool's
+// free list: the list is rebuilt afterwards from the dead markers (the set of free nodes is
+// what decides allocation, not its order).
+struct Pend {
+  uint32_t lo, hi;  // lane j: entry j of this pop (lo = node | insert << 31, hi = pred | at << 16)
+  int n;            // entries pending (wave-uniform, in a VGPR)
+  int logn;         // entries in the log; < 0: the tree is live (no deferral)
+};
+__device__ __forceinline__ bool pend_on(const Pend& pd) { return __builtin_amdgcn_readfirstlane(pd.logn) >= 0; }
+__device__ __forceinline__ void pend_add(Pend& pd, int lane, int x, bool ins, int pred, int at) {
+  const bool me = lane == pd.n;
+  pd.lo = me ? ((uint32_t)x | (ins ? 0x80000000u : 0u)) : pd.lo;
+  pd.hi = me ? (((uint32_t)pred & 0xffffu) | ((uint32_t)at << 16)) : pd.hi;
+  pd.n += 1;
+}
+template <class CF>
+__device__ __forceinline__ void pend_replay(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AStarLdsT<CF>& L, Pend& pd) {
+  auto apply = [&](uint32_t lo, uint32_t hi) {
+    const int x = (int)(lo & 0xffffu);
+    if (lo >> 31) {
+      const int pred = (int)(int16_t)(hi & 0xffffu), at = (int)(int16_t)(hi >> 16);
+      int parent;
+      bool left;
+      if (pred == NIL && at == NIL) {  // into the empty tree
+        parent = 0;
+        left = true;
+      } else if (pred == NIL) {
+        parent = at;
+        left = true;
+      } else if (at == NIL || tr.R(pred) == NIL) {
+        parent = pred;
+        left = false;
+      } else {
+        parent = at;
+        left = true;
+      }
+      tr.link(left, x, parent);
+    } else {
+      tr.unlink(x);
+    }
+  };
+  const int lane = c.lane;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's log stores are in L2
+  tr.cb = 0;
+  tr.clear();
+  const int logn = __builtin_amdgcn_readfirstlane(pd.logn);
+  GAS uint32_t* lg = (GAS uint32_t*)gp(c.A->open2);
+  for (int base = 0; base < logn; base += 64) {
+    uint32_t lo = 0, hi = 0;
+    if (base + lane < logn) {  // (L1-bypassing loads: the lines were written since any earlier read)
+      lo = __hip_atomic_load((uint32_t*)&lg[2 * (base + lane)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      hi = __hip_atomic_load((uint32_t*)&lg[2 * (base + lane) + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const int cnt = min(64, logn - base);
+    for (int j = 0; j < cnt; ++j)
+      apply((uint32_t)__builtin_amdgcn_readlane((int)lo, j), (uint32_t)__builtin_amdgcn_readlane((int)hi, j));
+  }
+  const int np = __builtin_amdgcn_readfirstlane(pd.n);
+  for (int j = 0; j < np; ++j)
+    apply((uint32_t)__builtin_amdgcn_readlane((int)pd.lo, j), (uint32_t)__builtin_amdgcn_readlane((int)pd.hi, j));
+  wave_lds_sync();
+  // the free list again: every dead pool node (key 0xffffffff; node 0 is the header)
+  const int used = c.ps2.next;
+  int head = NIL;
+  for (int base = (used - 1) & ~63; base >= 0; base -= 64) {
+    const int i = base + lane;
+    const bool dead = i >= 1 && i < used && ufu(L.kf[i].key) == 0xffffffffu;
+    const uint64_t m = __ballot(dead);
+    const uint64_t above = m & ~((2ull << lane) - 1ull);  // dead lanes above this one
+    const int nxt = above ? base + (int)__ffsll((unsigned long long)above) - 1 : head;
+    if (dead) L.lr[i].l = (int16_t)nxt;
+    if (m) head = base + (int)__ffsll((unsigned long long)m) - 1;
+  }
+  c.ps2.free = head;
+  wave_lds_sync();
+  pd.logn = -1;
+  pd.n = 0;
+}
+
 template <class CF>
 __device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AStarLdsT<CF>& L, Ring& rg, uint32_t key,
                                            float fn, float gn, int prev, const SameCell& sc, const RankOut& rb,
-                                           int* node_out) {
+                                           int* node_out, Pend& pd) {
   *node_out = NIL;
-  int parent;
-  bool left;
+  int parent = 0;
+  bool left = true;
+  bool logged = false;
   if (sc.cnt >= 2 || (sc.cnt == 1 && sc.f > fn)) {  // a node of this cell lies right of fn
+    if (pend_on(pd)) pend_replay(c, tr, L, pd);  // the walk needs the tree
     parent = tr.insert_pos(key, fn, &left);
     if (parent == -2) return true;
   } else {
     if ((rb.at != NIL && rb.at_f == fn) || (rb.pred != NIL && rb.pred == sc.idx)) return true;  // dropped
-    if (rg.n == 0) {
+    if (pend_on(pd)) {
+      logged = true;  // its place is its rank neighbours: linked when the log is replayed
+    } else if (rg.n == 0) {
       parent = 0;
       left = true;
     } else if (rb.pred == NIL) {
@@ -723,7 +815,8 @@ __device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AS
   if (n == NIL) return false;
   tr.payload(n, key, fn, gn, prev);
   STAMP_T t_l = STAMP_NOW();
-  tr.link(left, n, parent);
+  if (logged) pend_add(pd, c.lane, n, true, rg.n == 0 ? NIL : rb.pred, rg.n == 0 ? NIL : rb.at);
+  else tr.link(left, n, parent);
   STAMP_ADD(25, t_l);
   STAMP_T t_r = STAMP_NOW();
   ring_insert(L, rg, rb.r, n, c.lane);
@@ -781,7 +874,7 @@ __device__ __forceinline__ float hit_g(const SearchCtx& c, AStarLdsT<CF>& L, int
 // (*result = cost-to-goal or FLT_MAX).
 template <class CF>
 __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AStarLdsT<CF>& L, Ring& rg, int adx,
-                                               int ady, float acost, float* result) {
+                                               int ady, float acost, float* result, Pend& pd) {
   const PlannerDev& P = *c.P;
   const int lane = c.lane;
   const int nact = P.diag ? 8 : 4;
@@ -794,10 +887,14 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
   // inner search in both modes and on both kernels alike)
   const int acap = c.A->open2_cap < P.astar_cap ? c.A->open2_cap : P.astar_cap;
   const int lim = CF::CAP < acap ? CF::CAP : acap;
+  // the log's capacity in 8-B entries (the open2 area, unused until a migration), less one
+  // pop's entries (1 + 2 per neighbour)
+  const int log_lim = c.A->open2_cap * (int)(sizeof(Node2) / 8) - (1 + 2 * 8);
   while (rg.n > 0) {
     if (c.ps2.next + 8 > lim) return false;
+    if (pend_on(pd) && __builtin_amdgcn_readfirstlane(pd.logn) > log_lim) pend_replay(c, tr, L, pd);
     STAMP_T t_pop = STAMP_NOW();
-    const int b = tr.begin();
+    const int b = pend_on(pd) ? ((int)L.ring[rg.head] & (CF::CAP - 1)) : tr.begin();
     const Quad top = tr.quad(b);
     const int tx = (int)(top.key >> 16), ty = (int)(top.key & 0xffffu);
     const uint32_t tcell = (uint32_t)tx * (uint32_t)c.N + (uint32_t)ty;
@@ -818,7 +915,8 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
       cr = gload(&cells[cell]);
     }
     STAMP_T t_u = STAMP_NOW();
-    tr.unlink(b);
+    if (pend_on(pd)) pend_add(pd, lane, b, false, NIL, NIL);
+    else tr.unlink(b);
     STAMP_ADD(24, t_u);
     free_lds(c, tr, b);
     ring_erase(L, rg, 0, lane);
@@ -939,6 +1037,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
       } else {
         rank2(L, rg, fprobe, fn, lane, ra, rb);
         if (sc.cnt >= 2 || (sc.cnt == 1 && sc.f < fprobe)) {
+          if (pend_on(pd)) pend_replay(c, tr, L, pd);
           hit = tr.find(key, fprobe);  // shape-dependent: the exact tree walk
         } else if (ra.at != NIL && (ra.at_f == fprobe || ra.at == sc.idx)) {
           hit = ra.at;
@@ -949,7 +1048,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
       if (hit == 0) {
         STAMP_T t_i = STAMP_NOW();
         int nn;
-        if (!insert_lds(c, tr, L, rg, key, fn, gn, ci, sc, rb, &nn)) { c.status = -75; *result = FLT_MAX; return true; }
+        if (!insert_lds(c, tr, L, rg, key, fn, gn, ci, sc, rb, &nn, pd)) { c.status = -75; *result = FLT_MAX; return true; }
         if (lane == k) {  // Node2D::set_accumulated_cost; the cell's nm_f is written even
           st_on = true;   // when the insert is dropped (AStar.cpp:172-183)
           st_cell = (uint32_t)ki * (uint32_t)c.N + (uint32_t)kj;
@@ -968,7 +1067,8 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
           rank2(L, rg, hf, hf, lane, h1, h2);
           hit_rank = h1.r;
         }
-        tr.unlink(hit);
+        if (pend_on(pd)) pend_add(pd, lane, hit, false, NIL, NIL);
+        else tr.unlink(hit);
         free_lds(c, tr, hit);
         freed = true;
         ring_erase(L, rg, hit_rank, lane);
@@ -979,7 +1079,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
         RankOut r1;
         rank2(L, rg, fn, fn, lane, r1, rb);
         int nn;
-        if (!insert_lds(c, tr, L, rg, key, fn, gn, ci, sc, rb, &nn)) { c.status = -75; *result = FLT_MAX; return true; }
+        if (!insert_lds(c, tr, L, rg, key, fn, gn, ci, sc, rb, &nn, pd)) { c.status = -75; *result = FLT_MAX; return true; }
         if (lane == k) {
           st_on = true;
           st_cell = (uint32_t)ki * (uint32_t)c.N + (uint32_t)kj;
@@ -1000,6 +1100,11 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
         if (st_pv) pvg_store(c, L, st_node, ci, st_g);
         open_cell(cells, st_cell, open_cgen, st_g, ci, c.gen2, st_hint);
       }
+    }
+    if (pend_on(pd)) {  // this pop's log entries, one store
+      if (lane < pd.n) *(GAS v2u*)&((GAS uint32_t*)gp(c.A->open2))[2 * (pd.logn + lane)] = v2u{pd.lo, pd.hi};
+      pd.logn += pd.n;
+      pd.n = 0;
     }
     wave_lds_sync();
     STAMP_ADD(31, t_e);
@@ -1031,11 +1136,12 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLdsT<CF>& L, int s
   tl.clear();
   L.kf[0].key = 0xffffffffu;
   Ring rg{0, 0};
+  Pend pd{0u, 0u, 0, 0};  // the tree is deferred from the start
   {
     const SameCell none{0, NIL, 0.0f};
     const RankOut at0{0, NIL, 0.0f, NIL};
     int n0;
-    insert_lds(c, tl, L, rg, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL, none, at0, &n0);
+    insert_lds(c, tl, L, rg, ((uint32_t)si << 16) | (uint32_t)sj, h0, 0.0f, NIL, none, at0, &n0, pd);
     pvg_store(c, L, n0, NIL, 0.0f);  // {prev, g} of the start
     open_cell(c.cell2, (uint32_t)s_cell, c.gen2 - 1u, 0.0f, NIL, c.gen2, (uint32_t)n0);
   }
@@ -1052,7 +1158,8 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLdsT<CF>& L, int s
   }
   float result = FLT_MAX;
   STAMP_ADD(35, t_hs);
-  if (astar_loop_lds(c, tl, L, rg, adx, ady, acost, &result)) return result;
+  if (astar_loop_lds(c, tl, L, rg, adx, ady, acost, &result, pd)) return result;
+  if (pend_on(pd)) pend_replay(c, tl, L, pd);  // the migration copies the tree (into open2: the log is read first)
   // migrate the LDS tree to HBM nodes (identical indices) and continue there
   c.amigr++;
   GAS Node2* o2 = gp(A.open2);
