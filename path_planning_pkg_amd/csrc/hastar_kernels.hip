@@ -693,18 +693,37 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
 }
 
 // insert (AStar.cpp:172-183) into the LDS tree: rank-decided unless shape-dependent
+// The LDS pool's free list is threaded through the dead nodes' f field (key 0xffffffff marks
+// them), not through their links: a node freed while its erase is still in the log keeps the
+// links the replay's unlink reads.
+template <class CF>
+__device__ __forceinline__ void free_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, int x) {
+  tr.s->kf[x].key = 0xffffffffu;  // dead: never matches a cell
+  tr.s->kf[x].f = __int_as_float(c.ps2.free);
+  c.ps2.free = x;
+}
+template <class CF>
+__device__ __forceinline__ int alloc_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr) {
+  if (c.ps2.free != NIL) {
+    const int i = c.ps2.free;
+    c.ps2.free = __builtin_amdgcn_readfirstlane(__float_as_int(tr.s->kf[i].f));
+    return i;
+  }
+  if (c.ps2.next >= CF::CAP) return NIL;
+  return c.ps2.next++;
+}
+
 // ---- deferred inner tree ------------------------------------------------------------
 // An inner search keeps only its f-ordered ring while no shape-dependent event has happened:
 // the pop takes the ring's first node (the tree's leftmost), and an insert's position comes
 // from its rank neighbours, so the red-black links are not needed.  Each tree operation is
 // logged instead ({node, insert flag} and its rank neighbours {pred, at}; the pop's and the
 // expansion's entries in lanes 0.., stored to the arena's open2 area at the end of the pop).
-// At the first event that needs the tree (a find or insert walk, a migration to HBM, or a full
-// log) the log is replayed into an empty tree: the same libstdc++ link / erase calls in the
-// same order give the same shape, so results are identical.  Searches that end without an
-// event never build their tree.  The replay rewrites the links, which also thread the pool's
-// free list: the list is rebuilt afterwards from the dead markers (the set of free nodes is
-// what decides allocation, not its order).
+// At an event that needs the tree (a find or insert walk, a migration to HBM, or a full log)
+// the log is replayed into the tree as it stood at the last replay (empty at the search's
+// start): the same libstdc++ link / erase calls in the same order give the same shape, so
+// results are identical.  Then logging goes on.  Searches that end without an event never
+// build their tree; the others build it only at their events.
 struct Pend {
   uint32_t lo, hi;  // lane j: entry j of this pop (lo = node | insert << 31, hi = pred | at << 16)
   int n;            // entries pending (wave-uniform, in a VGPR)
@@ -745,8 +764,6 @@ __device__ __forceinline__ void pend_replay(SearchCtx& c, RBT<LdsAcc<CF>>& tr, A
   };
   const int lane = c.lane;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's log stores are in L2
-  tr.cb = 0;
-  tr.clear();
   const int logn = __builtin_amdgcn_readfirstlane(pd.logn);
   GAS uint32_t* lg = (GAS uint32_t*)gp(c.A->open2);
   for (int base = 0; base < logn; base += 64) {
@@ -763,21 +780,7 @@ __device__ __forceinline__ void pend_replay(SearchCtx& c, RBT<LdsAcc<CF>>& tr, A
   for (int j = 0; j < np; ++j)
     apply((uint32_t)__builtin_amdgcn_readlane((int)pd.lo, j), (uint32_t)__builtin_amdgcn_readlane((int)pd.hi, j));
   wave_lds_sync();
-  // the free list again: every dead pool node (key 0xffffffff; node 0 is the header)
-  const int used = c.ps2.next;
-  int head = NIL;
-  for (int base = (used - 1) & ~63; base >= 0; base -= 64) {
-    const int i = base + lane;
-    const bool dead = i >= 1 && i < used && ufu(L.kf[i].key) == 0xffffffffu;
-    const uint64_t m = __ballot(dead);
-    const uint64_t above = m & ~((2ull << lane) - 1ull);  // dead lanes above this one
-    const int nxt = above ? base + (int)__ffsll((unsigned long long)above) - 1 : head;
-    if (dead) L.lr[i].l = (int16_t)nxt;
-    if (m) head = base + (int)__ffsll((unsigned long long)m) - 1;
-  }
-  c.ps2.free = head;
-  wave_lds_sync();
-  pd.logn = -1;
+  pd.logn = 0;  // the tree is current; later operations are logged again
   pd.n = 0;
 }
 
@@ -811,7 +814,7 @@ __device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AS
       left = true;
     }
   }
-  const int n = tpool_alloc(tr, c.ps2, CF::CAP);
+  const int n = alloc_lds(c, tr);
   if (n == NIL) return false;
   tr.payload(n, key, fn, gn, prev);
   STAMP_T t_l = STAMP_NOW();
@@ -823,12 +826,6 @@ __device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AS
   STAMP_ADD(30, t_r);
   *node_out = n;
   return true;
-}
-
-template <class CF>
-__device__ __forceinline__ void free_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, int x) {
-  tr.s->kf[x].key = 0xffffffffu;  // dead: never matches a cell
-  tpool_free(tr, c.ps2, x);
 }
 
 // The record of a cell whose node was just inserted into the open tree (one 16-B store): not
@@ -1175,7 +1172,9 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLdsT<CF>& L, int s
       n.key = L.kf[i].key;
       n.f = L.kf[i].f;
       n.g = __int_as_float(pg.y);
-      n.l = L.lr[i].l;
+      // a dead node's l is its free-list link, kept in f in LDS (free_lds)
+      const bool dead = (uint32_t)n.key == 0xffffffffu && i > 0;  // (per lane: no uniform read)
+      n.l = dead ? __float_as_int(L.kf[i].f) : L.lr[i].l;
       n.r = L.lr[i].r;
       n.p = L.p[i];
       n.color = col;
