@@ -56,6 +56,19 @@ def test_rbtree_replica_matches_std_set(tmp_path):
     assert out.stdout.startswith("OK")
 
 
+def test_deferred_tree_replay_builds_the_same_tree(tmp_path):
+    """The deferred inner tree (hastar_kernels.hip, Pend / pend_replay): logged inserts (with
+    their in-order neighbours) and erases, replayed at random points with the kernel's parent
+    rule, give the tree the immediate operations give, link for link and colour for colour;
+    freed indices are reused while their erase is still in the log (tools/rbtree_defer_check.cpp)."""
+    exe = tmp_path / "rbtree_defer_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", str(ROOT / "path_planning_pkg_amd" / "csrc"),
+                    str(ROOT / "tools" / "rbtree_defer_check.cpp"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "100", "20000"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.startswith("OK")
+
+
 def test_relaxed_entry_point_rejects_bad_arguments():
     """hastar_find_path_relaxed_batch validates its arguments before touching a device, and
     hastar_relaxed_opts has the C layout the ctypes mirror declares (seven 4-byte fields)."""
