@@ -804,7 +804,7 @@ def run_cfg5(args, gpu, dist, torch, rank, world, device):
                 "note": "non-parity mode (hastar_find_path_relaxed_batch) on the same ticks' maps and starts as the "
                         "exact loop (rank 0); tick_ms = its find_path wall + the same batched upkeep"}
         if not args.no_cpu_baseline:
-            out["cpu_baseline"], replay = cpu_baseline_cfg5(pairs, args.cpu_seconds, args.warmup + args.steps)
+            out["cpu_baseline"], replay = cpu_baseline_cfg5(pairs, args.cpu_seconds, args.warmup + args.steps, args.warmup)
             out["parity_sample"] = cfg5_parity(gpu_ticks, replay, ids)
     if dist:
         dist.barrier()
@@ -841,14 +841,15 @@ def cfg5_parity(gpu_ticks, replay, ids):
                     "path+curvature bits (hash)"}
 
 
-def cpu_baseline_cfg5(pairs, budget_s, ticks):
+def cpu_baseline_cfg5(pairs, budget_s, ticks, warm=0):
     """The oracle replaying the same pairs' replan loops on `cpu_threads()` host threads, one
     private planner per thread (find_path timed only; ctypes calls release the GIL).  Pairs are
     taken in order, one thread per pair, in rounds of T pairs until every pair is replayed (the
     parity readout needs them all) or the rounds' parallel wall time reaches 4x the budget.
     value = pops / parallel find_path wall.  A tick's pairs are independent, so with a core per
-    pair the CPU's tick takes as long as its slowest pair (tick_ms_one_core_per_pair).  Also
-    returns {pair index: [tick_key per tick]} of the replayed pairs."""
+    pair the CPU's tick takes as long as its slowest pair (tick_ms_one_core_per_pair: the mean
+    over the timed ticks, the first `warm` ticks being the GPU run's warm-up; every tick's
+    maximum in tick_max_ms).  Also returns {pair index: [tick_key per tick]} of the replayed pairs."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle.pyoracle import OraclePlanner
     from tests.scenarios import drive, replan_tick, replan_tick_inputs
@@ -893,10 +894,13 @@ def cpu_baseline_cfg5(pairs, budget_s, ticks):
     return ({"value": pops / wall if wall > 0 else None, "unit": "expansions/s", "cores": T, "kind": "port",
              "sample": f"first {n} pairs of rank 0 x {ticks} ticks (same call sequence as the GPU run), find_path "
                        f"only, {T} threads with one private planner each (oracle/hastar_oracle.cpp, -O3)",
-             "tick_ms_one_core_per_pair": float(tick_max.mean()) if n else None,
+             # the timed ticks (as the GPU's tick_ms; ticks before `warm` are its warm-up)
+             "tick_ms_one_core_per_pair": float(tick_max[warm:].mean()) if n else None,
+             "tick_max_ms": [float(x) for x in tick_max] if n else None,
+             "tick_ms_one_core_per_pair_all_ticks": float(tick_max.mean()) if n else None,
              # the same ticks on this box's T host threads: each tick's replayed pairs list-scheduled
              # longest first over T cores (a tick of 64 pairs on 16 threads takes at least 4 pairs' time)
-             f"tick_ms_{T}_threads": float(np.mean([makespan(m, T) for m in per_tick])) if n else None}, replay)
+             f"tick_ms_{T}_threads": float(np.mean([makespan(m, T) for m in per_tick[warm:]])) if n else None}, replay)
 
 
 def parity_sample(cfgs, gpu, qids, gpu_last=None, replans=1):
