@@ -68,6 +68,17 @@ def step_balance(planners):
             "longest_search_start_ms": float((t[li, 0] - t[:, 0].min()) * 1e-5)}
 
 
+def cold_tail(t, pops, qids, k=6):
+    """The k searches of a step that ended last: query, pops, start and end (ms from the step's
+    first start), and the slot that ended it (>= the pool's arena count: a head arena)."""
+    if t is None:
+        return None
+    t0 = t[:, 0].min()
+    idx = np.argsort(-t[:, 1], kind="stable")[:k]
+    return [{"query": int(qids[i]), "pops": int(pops[i]), "start_ms": float((t[i, 0] - t0) * 1e-5),
+             "end_ms": float((t[i, 1] - t0) * 1e-5), "slot": int(t[i, 2])} for i in idx]
+
+
 def step_diag(planners, res):
     """One step's schedule: span of the searches, the split launch's event times, and the start
     offset / duration (ms) of the searches on the latency CUs (arenas 0 .. head_cus - 1) and of
@@ -289,6 +300,8 @@ def main():
     r0 = step()
     cold_s = time.perf_counter() - t0
     cold_handoffs = planners[0].handoffs()
+    # what bounded the cold step: its last-ending searches (start, end, slot, pops), host-side
+    cold_t = np.array([p.timing() for p in planners], dtype=np.float64) if rank == 0 else None
     progress("cold first step done")
     # the first step's outcome of a stratified sample (every 64th query and the 8 with the most
     # pops), paths included, for the bit-exact check against the oracle after the timed region
@@ -297,6 +310,7 @@ def main():
     cold_sample = {i: r0.result(i) for i in strat} if (rank == 0 and not args.no_cpu_baseline) else None
     cold_all = (r0.stats.copy(), r0.cost.copy(), r0.ok.copy()) if (rank == 0 and args.parity_all) else None
     cold_pops = int(r0.stats["pops"].sum())
+    r0_pops = r0.stats["pops"].copy()
     cold_s, cold_pops_all = reduce_over_ranks(dist, cold_s, cold_pops, f"cuda:{device}")
     for _ in range(max(args.warmup - 1, 0)):
         step()
@@ -421,6 +435,7 @@ def main():
             "kernel_ms_per_step": [float(k) for k in kernel_ms],
             **({"step_diag": diag} if diag else {}),
             "cold_first_step": {"value": cold_pops_all / cold_s, "ms": cold_s * 1e3, "handoffs": cold_handoffs,
+                                "last_to_end": cold_tail(cold_t, r0_pops, qids),
                                 "note": "first launch of the batch: no longest-first history (the library orders the "
                                         "queue by its cold key: boxes near the start-goal route, hastar.h "
                                         "hastar_set_cost_hint); the device pool was reserved at setup "
