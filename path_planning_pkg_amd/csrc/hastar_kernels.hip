@@ -727,9 +727,11 @@ __device__ __forceinline__ int alloc_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr) {
 struct Pend {
   uint32_t lo, hi;  // lane j: entry j of this pop (lo = node | insert << 31, hi = pred | at << 16)
   int n;            // entries pending (wave-uniform, in a VGPR)
-  int logn;         // entries in the log; < 0: the tree is live (no deferral)
+  int logn;         // entries in the log
 };
-__device__ __forceinline__ bool pend_on(const Pend& pd) { return __builtin_amdgcn_readfirstlane(pd.logn) >= 0; }
+// (deferral is always on: a replay leaves logn = 0 and logging goes on, so the tree-mode
+// branches behind pend_on are never taken and compile away)
+__device__ __forceinline__ bool pend_on(const Pend&) { return true; }
 __device__ __forceinline__ void pend_add(Pend& pd, int lane, int x, bool ins, int pred, int at) {
   const bool me = lane == pd.n;
   pd.lo = me ? ((uint32_t)x | (ins ? 0x80000000u : 0u)) : pd.lo;
