@@ -1,7 +1,8 @@
 // Dubins.h — drop-in planning::Dubins<T> (reference include/path_planning_pkg/Dubins.h:
 // 21-60, lib/Dubins.cpp), computed on the MI355X through include/hastar_units.h.
 // T = float is bit-exact with the reference (the search kernel's glibc float ports);
-// T = double runs ports of glibc 2.35's double libm for the CSC words: bit-exact as well.
+// T = double runs ports of glibc 2.35's double libm for the CSC words: bit-exact as well
+// (for |angles| < 2^27 * pi/2, where the ports' sin/cos need no __branred reduction).
 // Like the reference object, the last call's word and parameters are kept (get_path_type).
 #ifndef DUBINS
 #define DUBINS

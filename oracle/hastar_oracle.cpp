@@ -26,6 +26,10 @@
 //   * transcendental calls go to the host glibc libm, like the reference.
 // Build: oracle/Makefile (g++ -O3 -ffp-contract=off, x86-64 baseline ISA; -O3 as the
 // reference's CMakeLists.txt:128 build, so the CPU timing proxy uses the same optimisation).
+// -DORC_LEAN (build/libhastar_oracle_lean.so): the TIMING build of bench.py's cpu_baseline — the
+// same containers, comparator and arithmetic, with the checker's bookkeeping the reference does
+// not do compiled out (pop and closed-set digests, successor / shot / inner-search counters; the
+// pop count stays).  Its results (path, cost, success, pops) are the full build's.
 #include <atomic>
 #include <cmath>
 #include <cfloat>
@@ -594,7 +598,9 @@ template <class T> struct Planner {
   // AStar::a_star_search(start, get_cost_only) (AStar.cpp:118-186) from the soft-reset start
   T a_star(int si, int sj, bool cost_only) {
     nm_f[(size_t)si * N + sj] = nm_h[(size_t)si * N + sj];  // Node2D::soft_reset
+#ifndef ORC_LEAN
     st.astar_searches++;
+#endif
     cl2.clear();
     op2.clear();
     op2.insert(N2<T>{si, sj, 0, nm_f[(size_t)si * N + sj], nullptr});
@@ -612,7 +618,9 @@ template <class T> struct Planner {
       auto it = op2.begin();
       const N2<T>* cur = &*cl2.insert(*it).first;
       op2.erase(it);
+#ifndef ORC_LEAN
       st.astar_pops++;
+#endif
       if (cur->x == astar_goal.x && cur->y == astar_goal.y) {
         astar_goal = *cur;
         if (cost_only) memoise(astar_goal.f, &astar_goal);
@@ -699,7 +707,9 @@ template <class T> struct Planner {
       s.cy = cj;
       out.push_back(s);
     }
+#ifndef ORC_LEAN
     st.successors += (long long)out.size();
+#endif
     return slow;
   }
   // Grid3D::check_path (Grid3D.cpp:78-93)
@@ -732,8 +742,10 @@ template <class T> struct Planner {
       const N3<T>* cur = &*cl3.insert(*it).first;
       op3.erase(it);
       st.pops++;
+#ifndef ORC_LEAN
       dig = mix64(dig ^ (((uint64_t)(uint32_t)cur->cx << 40) | ((uint64_t)(uint32_t)cur->cy << 16) |
                          (uint64_t)(uint32_t)cur->bin)) + gbits(cur->g);
+#endif
       if (cur->cx == goal_node.cx && cur->cy == goal_node.cy) {
         terminal = *cur;
         out = {terminal.g, true};
@@ -741,7 +753,9 @@ template <class T> struct Planner {
       }
       if (shot_allowed) {
         if (++counter == interval) {
+#ifndef ORC_LEAN
           st.shots++;
+#endif
           auto pr = dub.path(cur->pose, goal_node.pose, shot_path, shot_curv);
           if (!pr.second && free_path(shot_path)) {
             terminal = *cur->prev;
@@ -776,8 +790,10 @@ template <class T> struct Planner {
     st.pop_digest = dig;
     st.closed_size = (long long)cl3.size();
     uint64_t cd = 0;
+#ifndef ORC_LEAN
     for (const auto& n : cl3)
       cd += mix64(((uint64_t)(uint32_t)n.cx << 40) | ((uint64_t)(uint32_t)n.cy << 16) | (uint64_t)(uint32_t)n.bin);
+#endif
     st.closed_digest = cd;
     st.via_shot = shot_ok ? 1 : 0;
     if (st.status != 0) out = {std::numeric_limits<T>::max(), false};

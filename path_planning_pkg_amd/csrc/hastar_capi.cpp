@@ -2050,8 +2050,18 @@ int hastar_find_path_batch(const hastar_handle* hs, int n, const float* vel, con
         }
         return wide ? launch_search_wide(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, DC.d_next, hard_pops, st)
                     : launch_search(DC.d_descs, n, DC.d_arenas, slots, DC.d_order, n_prio, DC.d_next, hard_pops, st);
-      }))
+      })) {
+    // a failed split launch must not leave the board enabled: later launches through the same
+    // pool arenas (resumes, unsplit batches) would post offers no latency wave claims.  The
+    // header is cleared synchronously, whatever state the streams are in (best effort: the
+    // launch's own error is the one reported).
+    if (split1) {
+      (void)hipDeviceSynchronize();
+      (void)hipMemset(DC.d_board, 0, offsetof(HandoffBoard, state));
+      (void)hipDeviceSynchronize();
+    }
     return r;
+  }
   if (split1) {
     // the board is read back and disabled before any other launch (resume passes run the
     // batch kernel without it)

@@ -126,11 +126,23 @@ int arena_alloc(hastar64_handle h) {
                bdc = al256((size_t)h->dub_cap * sizeof(double)), bch = al256((size_t)closed3 * sizeof(int)),
                bg = 256;
   const size_t total = b3 + bc + bs + b2 + bcell + bd + bdc + bch + bg;
-  // the new arena is allocated before the old one is freed: when it cannot be, the planner keeps
-  // its current arena and the device descriptor's pointers into it (the caller restores the caps)
+  // the new arena is allocated before the old one is freed, so that a failed growth leaves the
+  // planner its current arena; when both do not fit at once, the old one is freed first and the
+  // allocation retried (peak = the larger arena alone).  If that fails too, h->arena is null and
+  // the caller restores the caps and carves the old size again (arena_restore).
   void* fresh = nullptr;
-  if (hipMalloc(&fresh, total) != hipSuccess)
-    return fail64(HASTAR_EOVERFLOW, "search arena of " + std::to_string(total >> 20) + " MiB cannot be allocated");
+  if (hipMalloc(&fresh, total) != hipSuccess) {
+    (void)hipGetLastError();
+    if (!h->arena)
+      return fail64(HASTAR_EOVERFLOW, "search arena of " + std::to_string(total >> 20) + " MiB cannot be allocated");
+    HIPCHK64(hipStreamSynchronize(h->st));
+    hipFree(h->arena);
+    h->arena = nullptr;
+    if (hipMalloc(&fresh, total) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail64(HASTAR_EOVERFLOW, "search arena of " + std::to_string(total >> 20) + " MiB cannot be allocated");
+    }
+  }
   HIPCHK64(hipStreamSynchronize(h->st));
   if (h->arena) hipFree(h->arena);
   h->arena = fresh;
@@ -532,11 +544,14 @@ int hastar64_find_path(hastar64_handle h, double vel, const double start[3], dou
     ++h->reruns;
     if (int rc = arena_alloc(h)) {  // no larger arena: the reference's failure pair, status EOVERFLOW
       status = rc;
-      // the planner keeps its current arena (arena_alloc frees it only after a larger one is
-      // allocated), so it stays usable with the capacities that arena was carved for
+      // the planner keeps the capacities of its current arena; arena_alloc kept that arena unless
+      // it had to free it to retry, and then it is carved again at the old size
       h->pops_cap = was_pops;
       h->astar_cap = was_astar;
       h->dub_cap = was_dub;
+      if (!h->arena) {
+        if (int rc2 = arena_alloc(h)) status = rc2;
+      }
       break;
     }
   }

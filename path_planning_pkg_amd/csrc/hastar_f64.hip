@@ -22,8 +22,9 @@
 //
 // Expressions keep the reference's double arithmetic (-ffp-contract=off).  sin, cos, atan2, acos
 // and hypot are ports of glibc 2.35's routines (hastar_libm64.h), bit for bit the host libm's on
-// every argument sampled, so this planner reproduces the reference bit for bit
-// (include/hastar_f64.h).
+// every argument sampled in the planner's ranges (sin/cos: |x| < 2^27 * pi/2, beyond which
+// glibc's __branred reduction is not ported; the planner's angles are wrapped to [-pi, pi]), so
+// this planner reproduces the reference bit for bit (include/hastar_f64.h).
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include "hastar_device.h"

@@ -2559,7 +2559,15 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void hastar_search_wide_kernel(
     // split over this kernel and the batch kernel, whose counter starts after the head)
     // a split launch's latency CU prefers a long search the batch kernel offers (HandoffBoard)
     // to a new one from the queue, and once the queue is drained it waits for offers while
-    // batch-kernel waves still run (bounded: 30 s without one, so every wave reaches its end)
+    // batch-kernel waves still run (bounded: 30 s without one, so every wave reaches its end).
+    // No progress depends on the two kernels being co-resident, which HIP does not promise:
+    //  - bulk_active counts batch waves that have STARTED and not yet ended (the batch kernel's
+    //    entry and exit); a batch wave not yet resident is not counted, so a latency wave that sees 0
+    //    leaves (it gives up offers it could have taken, never waits for an absent wave);
+    //  - the claimer's wait for READY / CANCELLED is on an offer a running batch wave posted,
+    //    and that wave answers within 64 of its pops or at its search's end;
+    //  - the 30-s bound only guards a batch wave that stopped counting itself out (a fault).
+    // The host cannot signal the wait: it regains control only when both kernels have ended.
     GAS HandoffBoard* const hb = first_static ? gp(A.board) : nullptr;
     const bool handoffs = hb != nullptr && hb->enabled != 0;
     for (bool first = true;; first = false) {

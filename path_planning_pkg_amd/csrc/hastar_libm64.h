@@ -16,7 +16,12 @@
 // (tools/extract_glibc_{atan,acos}_table.py: the table points of Gal's accurate-table method cannot
 // be recomputed); sin/cos's table and constants are recomputed (tools/gen_libm64_tables.py).
 // Result: bit for bit the host glibc on 2e8 device samples per function and 5e7 host samples
-// (tests/test_libm64_ports.py, profiles/r05_libm64_gm64.jsonl).  Every operation is an IEEE basic
+// (tests/test_libm64_ports.py, profiles/r05_libm64_gm64.jsonl).
+// Bit-exact range: atan2, acos and hypot on every argument (glibc 2.35's e_atan2.c / e_asin.c
+// have no slow paths left); sin and cos for |x| < 0x419921FB'00000000 (~1.05e8, 2^27 * pi/2).
+// Beyond that glibc reduces with __branred (multi-precision pi/2), which is NOT ported: these
+// fall back to ::sin / ::cos, i.e. ocml on the device (not bit-exact there), glibc on the host.
+// The planner only calls sin/cos on headings wrapped to [-pi, pi] and on arc angles below 2 pi.  Every operation is an IEEE basic
 // operation or an explicit fma and the build has -ffp-contract=off, so device and host agree.
 // glibc is LGPL-2.1 (NOTICE).
 #pragma once

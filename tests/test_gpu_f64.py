@@ -3,14 +3,14 @@ oracle's double instantiation (oracle/hastar_oracle.cpp, Planner<double>).
 
 The reference instantiates both classes for double (HybridAStar.cpp:285-286,
 VelocityGenerator.cpp:88-89) and its LocalPlanner<double> calls them (local_planner.cpp:378-500).
-The device's sin, cos, atan2 and hypot are ports of the host glibc 2.35's (csrc/hastar_libm64.h;
-0 mismatches in 2e8 samples each, tools/libm64_fingerprint.hip, and tests/test_libm64_ports.py
-on the host); its acos is correctly rounded, which glibc's is on all but ~0.1 % of arguments.  So
-the bar here is bit equality: success, cost bits, pop count and digest, the closed set, path
-and curvature bits, and the memo after the search.  (acos enters only the RSL/LSR Dubins words:
-a heuristic value a glibc misrounding changes moves an f by one ulp, which changes nothing unless
-it creates or breaks an exact f tie; a shot through such a word would change its length's last
-bit.  No case below meets either.)  Parity is unpinned at the reference: the reference holds no
+The device's sin, cos, atan2, acos and hypot are ports of the host glibc 2.35's own routines
+(csrc/hastar_libm64.h: the FMA variants __sin_fma / __cos_fma / __ieee754_atan2_fma /
+__ieee754_acos_fma and e_hypot.c; 0 mismatches in 2e8 device samples each,
+tools/libm64_fingerprint.hip, and tests/test_libm64_ports.py on the host).  They are bit-exact
+for every finite argument except sin/cos of |x| >= 2^27 * pi/2 (~1.05e8), where glibc's
+__branred reduction is not ported; the planner's angles are wrapped to [-pi, pi].  So the bar
+here is bit equality: success, cost bits, pop count and digest, the closed set, path and
+curvature bits, and the memo after the search.  Parity is unpinned at the reference: the reference holds no
 double fixture for the planner (its double golden vectors, utils/dubins_paths.py:6 and
 utils/vehicle_mode.py:12, pin the Dubins / VehicleModel units, tests/test_cxx_units.py); the
 oracle's float instantiation of the same template is pinned by the reference's golden path.

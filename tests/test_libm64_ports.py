@@ -53,8 +53,36 @@ int main(int argc, char** argv) {
 """
 
 
+def _host_is_glibc235_x86_fma():
+    """The ports (and the tables read from libm.so.6) are glibc 2.35's x86-64 FMA variants: on
+    another glibc, a non-x86 host or a CPU without FMA the host libm runs other code, and a
+    comparison with it would measure that difference, not the ports."""
+    import ctypes
+    import platform
+    if platform.machine() not in ("x86_64", "AMD64"):
+        return False, f"host is {platform.machine()}, not x86-64"
+    try:
+        libc = ctypes.CDLL("libc.so.6")
+        libc.gnu_get_libc_version.restype = ctypes.c_char_p
+        ver = libc.gnu_get_libc_version().decode()
+    except (OSError, AttributeError):
+        return False, "not glibc"
+    if ver != "2.35":
+        return False, f"glibc {ver}, the ports are of 2.35"
+    try:
+        flags = Path("/proc/cpuinfo").read_text()
+    except OSError:
+        return False, "no /proc/cpuinfo"
+    if " fma" not in flags:
+        return False, "CPU without FMA (glibc dispatches to its non-FMA variants)"
+    return True, ""
+
+
 @pytest.fixture(scope="module")
 def ports(tmp_path_factory):
+    ok, why = _host_is_glibc235_x86_fma()
+    if not ok:
+        pytest.skip(why)
     d = tmp_path_factory.mktemp("libm64")
     (d / "t.cpp").write_text(SRC)
     exe = d / "t"

@@ -1,7 +1,9 @@
 """The cpu_baseline proxy, stated: the oracle restatement's find_path wall time on
-the survey's cfg1/cfg3 seeds, best of R fresh instances, single thread, in this container, beside
-the compiled reference's timings that BASELINE.md records for the same inputs (61 / 115 ms at
-1024^2 seeds 1 / 3; 0.95 ms at 256^2 seed 1).
+the survey's cfg1/cfg3 seeds, best of R fresh instances, single thread, in this container — the
+checker build and the lean timing build (-DORC_LEAN, bench.py's cpu_baseline) interleaved rep by
+rep, so both see the same host load — beside the compiled reference's timings that BASELINE.md
+records for the same inputs (taken in the survey's session; the reference itself is unbuildable
+under this build's rules: it needs a Boost stand-in header).
 
   python tools/cpu_proxy_timing.py [--reps 7]     -> one JSON line per case
 """
@@ -22,14 +24,23 @@ ap.add_argument("--reps", type=int, default=7)
 args = ap.parse_args()
 for (N, bins, K, seed) in [(256, 36, 10, 1), (512, 72, 50, 1), (512, 72, 50, 2), (1024, 72, 200, 1), (1024, 72, 200, 3)]:
     cfg, proto = synthetic_ref(N, bins, K, seed)
-    walls, pops = [], None
+    walls = {False: [], True: []}
+    res = {}
     for _ in range(args.reps):
-        o = OraclePlanner(cfg)
-        drive(o, proto)
-        r = o.find_path(proto["vel"], proto["start"])
-        walls.append(r["wall_ms"])
-        pops = r["stats"]["pops"]
-        del o
-    print(json.dumps(dict(grid=N, bins=bins, K=K, seed=seed, pops=pops, oracle_best_ms=round(min(walls), 3),
-                          oracle_median_ms=round(sorted(walls)[len(walls) // 2], 3), reps=args.reps,
-                          reference_ms=REF.get((N, seed)), host_cpus=os.cpu_count())), flush=True)
+        for lean in (False, True):
+            o = OraclePlanner(cfg, lean=lean)
+            drive(o, proto)
+            r = o.find_path(proto["vel"], proto["start"])
+            walls[lean].append(r["wall_ms"])
+            res[lean] = (r["stats"]["pops"], float(r["cost"]), bool(r["ok"]))
+            o.close()
+    assert res[False] == res[True], res  # the lean build plans the same search
+    best = {k: min(v) for k, v in walls.items()}
+    ref = REF.get((N, seed))
+    print(json.dumps(dict(grid=N, bins=bins, K=K, seed=seed, pops=res[False][0], oracle_best_ms=round(best[False], 3),
+                          oracle_median_ms=round(sorted(walls[False])[len(walls[False]) // 2], 3),
+                          lean_best_ms=round(best[True], 3),
+                          lean_median_ms=round(sorted(walls[True])[len(walls[True]) // 2], 3),
+                          lean_vs_full=round(best[True] / best[False], 3), reps=args.reps, reference_ms=ref,
+                          lean_vs_reference=round(best[True] / ref, 3) if ref else None, host_cpus=os.cpu_count())),
+          flush=True)
