@@ -51,6 +51,11 @@ namespace orc {
 // Optional pop limit for census tools (0 = none, the reference's behaviour): a search that
 // reaches it stops with stats.status = HASTAR_EOVERFLOW and is reported as failed.
 long long g_max_pops = 0;
+#ifdef ORC_OUTER_STATS
+// analysis build (tools/outer_shape_stats.py): how often the OUTER open set's tree shape can
+// decide a find / insert (a node of the same key on the "wrong" side of the probe f)
+long long g_oshape[16];
+#endif
 #ifdef ORC_SHAPE_STATS
 long long g_shape[16];
 bool g_search_unsafe;       // the current inner search met a shape-dependent find/insert
@@ -721,9 +726,36 @@ template <class T> struct Planner {
     return true;
   }
 
+#ifdef ORC_OUTER_STATS
+  bool g_oevent = false;
+  void outer_ins_stat(const N3<T>& s) {
+    int nsame = 0;
+    bool gt = false;
+    for (const auto& n : op3)
+      if (n.cx == s.cx && n.cy == s.cy && n.bin == s.bin) {
+        ++nsame;
+        gt |= n.f > s.f;
+      }
+    g_oshape[3]++;
+    g_oshape[4] += gt;
+    g_oshape[5] += nsame > 1;
+    if ((gt || nsame > 1) && !g_oevent) { g_oevent = true; g_oshape[7] += st.pops; }
+  }
+#endif
   // ----------------------------------------------------------------- search
   // HybridAStar::hybrid_a_star_search (HybridAStar.cpp:93-199)
   std::pair<T, bool> search(const N3<T>& start) {
+#ifdef ORC_OUTER_STATS
+    g_oevent = false;
+    struct OEnd {
+      Planner* p;
+      ~OEnd() {
+        g_oshape[10]++;
+        if (!p->g_oevent) g_oshape[7] += p->st.pops;  // a search without event: all its pops
+        else g_oshape[11]++;
+      }
+    } oend_{this};
+#endif
     int counter = 0, interval = shot_interval;
     bool shot_allowed = false;
     shot_ok = false;
@@ -768,14 +800,38 @@ template <class T> struct Planner {
         }
       }
       shot_allowed = expand(*cur, nb);
+#ifdef ORC_OUTER_STATS
+      g_oshape[6]++;
+      if ((long long)op3.size() > g_oshape[8]) g_oshape[8] = (long long)op3.size();
+#endif
       for (auto& s : nb) {
         if (cl3.find(s) != cl3.end()) continue;
+#ifdef ORC_OUTER_STATS
+        {
+          int nsame = 0;
+          bool lt = false;
+          for (const auto& n : op3)
+            if (n.cx == s.cx && n.cy == s.cy && n.bin == s.bin) {
+              ++nsame;
+              lt |= n.f < s.g;
+            }
+          g_oshape[0]++;
+          g_oshape[1] += nsame > 0;
+          g_oshape[2] += lt;
+          g_oshape[5] += nsame > 1;
+          g_oshape[9] += !op3.empty() && s.g > op3.begin()->f;
+          if ((lt || nsame > 1) && !g_oevent) { g_oevent = true; g_oshape[7] += st.pops; }
+        }
+#endif
         auto hit = op3.find(s);
         if (hit == op3.end()) {
           T h1 = holonomic(s.cx, s.cy);
           T h2 = dub.shortest(s.pose, goal_node.pose);
           s.f += stl_max(h1, h2);
           s.prev = cur;
+#ifdef ORC_OUTER_STATS
+          outer_ins_stat(s);
+#endif
           op3.insert(s);
         } else if (s.g < hit->g) {
           op3.erase(hit);
@@ -783,6 +839,9 @@ template <class T> struct Planner {
           T h2 = dub.shortest(s.pose, goal_node.pose);
           s.f += stl_max(h1, h2);
           s.prev = cur;
+#ifdef ORC_OUTER_STATS
+          outer_ins_stat(s);
+#endif
           op3.insert(s);
         }
       }
@@ -876,6 +935,11 @@ void orc_decay(void* h) { static_cast<OP*>(h)->decay(); }
 void orc_get_obstacles(void* h, float* out) {
   auto* P = static_cast<OP*>(h);
   std::memcpy(out, P->occ.data(), P->occ.size() * sizeof(float));
+}
+// test hook: overwrite the log-odds map (arbitrary values exercise the relocation's winners)
+void orc_set_obstacles(void* h, const float* in) {
+  auto* P = static_cast<OP*>(h);
+  std::memcpy(P->occ.data(), in, P->occ.size() * sizeof(float));
 }
 void orc_get_memo(void* h, float* f_out, unsigned char* visited_out) {
   auto* P = static_cast<OP*>(h);
@@ -1240,6 +1304,11 @@ extern "C" void orc_run_batch_threads(void* const* hs, int n, const float* vel, 
   out[3] = (double)n * replans;
 }
 
+#ifdef ORC_OUTER_STATS
+extern "C" void orc_outer_stats(long long* out) {
+  for (int q = 0; q < 16; ++q) out[q] = orc::g_oshape[q], orc::g_oshape[q] = 0;
+}
+#endif
 #ifdef ORC_SHAPE_STATS
 extern "C" void orc_shape_stats(long long* out) {
   for (int q = 0; q < 16; ++q) out[q] = orc::g_shape[q], orc::g_shape[q] = 0;

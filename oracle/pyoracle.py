@@ -42,6 +42,7 @@ def lib(lean=False):
         L.orc_update_boxes.argtypes = [vp, fp, fp, C.c_int, C.c_float]
         L.orc_update_lines.argtypes = [vp, fp, fp, C.c_int, C.c_float]
         L.orc_get_obstacles.argtypes = [vp, fp]
+        L.orc_set_obstacles.argtypes = [vp, fp]
         L.orc_get_memo.argtypes = [vp, fp, C.POINTER(C.c_ubyte)]
         L.orc_apf_count.argtypes = [vp]
         L.orc_get_apf.argtypes = [vp, fp]
@@ -136,6 +137,11 @@ class OraclePlanner:
         out = np.empty((self.N, self.N), np.float32)
         self._L.orc_get_obstacles(self.h, fptr(out))
         return out
+
+    def set_obstacles(self, occ):
+        """Test hook: overwrite the log-odds map."""
+        a = _f32(occ, (self.N, self.N))
+        self._L.orc_set_obstacles(self.h, fptr(a))
 
     def get_memo(self):
         f = np.empty((self.N, self.N), np.float32)

@@ -980,6 +980,41 @@ static int update_boxes_legacy(hastar_handle h, const float* boxes, const float*
 static int update_boxes_impl(const hastar_handle* hs, int n, const float* boxes, const float* conf, const int* counts,
                              float apf_added_radius);
 
+// Relocate the maps of `items` (distinct maps; DC.mu held) in chunks that share one scratch
+// allocation: every destination finds its winning source by inverting the rotation
+// (k_relocate_invert_batch, no claim table), then the chunk is copied back.  A chunk's scratch
+// maps total <= HASTAR_RELOC_CHUNK_MB (default 256 MB; 16 MB-1 GB measured within 2 % of each
+// other from 32 MB up, profiles/r06g_reloc_chunk_sweep.txt).  HASTAR_RELOC=claim selects the
+// round-5 passes (atomic claim, gather, copy; <= 1 GiB of claim tables) for A/B measurements.
+static int relocate_maps(DeviceCtx& DC, std::vector<RelocItem>& items, size_t NNmax) {
+  const int n = (int)items.size();
+  if (n == 0) return HASTAR_OK;
+  static const bool claim = [] {
+    const char* e = std::getenv("HASTAR_RELOC");
+    return e && std::string(e) == "claim";
+  }();
+  static const size_t chunk_bytes = [] {
+    const char* e = std::getenv("HASTAR_RELOC_CHUNK_MB");
+    return (size_t)(e ? std::max(1, std::atoi(e)) : 256) << 20;
+  }();
+  const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, chunk_bytes / (claim ? 8 * NNmax : 4 * NNmax)));
+  if (int rc = bscratch_acquire(DC, (size_t)chunk, NNmax)) return rc;
+  if (int rc = stage_acquire(DC, (size_t)n * sizeof(RelocItem))) return rc;
+  float* tmp0 = reinterpret_cast<float*>(DC.bscratch);
+  int* win0 = reinterpret_cast<int*>(DC.bscratch + DC.bs_maps * DC.bs_nn * 4);
+  for (int i = 0; i < n; ++i) {
+    items[i].tmp = tmp0 + (size_t)(i % chunk) * DC.bs_nn;
+    items[i].winner = win0 + (size_t)(i % chunk) * DC.bs_nn;
+  }
+  HIPCHK(hipMemcpyAsync(DC.stage, items.data(), (size_t)n * sizeof(RelocItem), hipMemcpyHostToDevice, DC.stream));
+  const RelocItem* d_items = reinterpret_cast<const RelocItem*>(DC.stage);
+  for (int c0 = 0; c0 < n; c0 += chunk) {
+    if (claim) HIPCHK(launch_relocate_batch(d_items + c0, std::min(chunk, n - c0), NNmax, DC.stream));
+    else HIPCHK(launch_relocate_invert(d_items + c0, std::min(chunk, n - c0), NNmax, DC.stream));
+  }
+  return HASTAR_OK;
+}
+
 int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3]) {
   if (!h || !goal || !start) return fail(HASTAR_EINVAL, "null argument");
   HIPCHK(hipSetDevice(h->device));
@@ -987,11 +1022,8 @@ int hastar_update_goal(hastar_handle h, const float goal[3], const float start[3
   PlannerDev& D = h->desc;
   const RelocPrep rp = goal_prep(h, goal, start);
   std::lock_guard<std::mutex> lk(DC.mu);
-  const size_t NN = (size_t)D.N * D.N;
-  if (int rc = scratch_acquire(DC, NN)) return rc;
-  HIPCHK(launch_relocate(D.N, rp.c, rp.s, rp.ox, rp.oy, D.occ, DC.tmp, DC.winner, DC.stream));
-  HIPCHK(hipMemcpyAsync(D.occ, DC.tmp, NN * sizeof(float), hipMemcpyDeviceToDevice, DC.stream));
-  return HASTAR_OK;
+  std::vector<RelocItem> items{RelocItem{D.occ, nullptr, nullptr, D.N, rp.c, rp.s, rp.ox, rp.oy, 0}};
+  return relocate_maps(DC, items, (size_t)D.N * D.N);
 }
 
 static RelocPrep goal_prep(hastar_handle h, const float goal[3], const float start[3]) {
@@ -1331,25 +1363,19 @@ int hastar_update_goal_batch(const hastar_handle* hs, int n, const float* goals,
   }
   HIPCHK(hipSetDevice(dev));
   DeviceCtx& DC = *hs[0]->dc;
-  std::vector<RelocItem> items(n);
+  // a planner named k times is relocated k times, in order (as k single calls): round r takes
+  // each planner's r-th occurrence, so the maps of one launch are distinct
+  std::vector<std::vector<RelocItem>> rounds;
+  std::unordered_map<const float*, int> seen;
   for (int i = 0; i < n; ++i) {
     const RelocPrep rp = goal_prep(hs[i], goals + 3 * i, starts + 3 * i);
-    items[i] = RelocItem{hs[i]->desc.occ, nullptr, nullptr, hs[i]->desc.N, rp.c, rp.s, rp.ox, rp.oy, 0};
+    const int r = seen[hs[i]->desc.occ]++;
+    if ((int)rounds.size() <= r) rounds.emplace_back();
+    rounds[(size_t)r].push_back(RelocItem{hs[i]->desc.occ, nullptr, nullptr, hs[i]->desc.N, rp.c, rp.s, rp.ox, rp.oy, 0});
   }
   std::lock_guard<std::mutex> lk(DC.mu);
-  const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, ((size_t)1 << 30) / (8 * NNmax)));
-  if (int rc = bscratch_acquire(DC, (size_t)chunk, NNmax)) return rc;
-  float* tmp0 = reinterpret_cast<float*>(DC.bscratch);
-  int* win0 = reinterpret_cast<int*>(DC.bscratch + DC.bs_maps * DC.bs_nn * 4);
-  if (int rc = stage_acquire(DC, (size_t)n * sizeof(RelocItem))) return rc;
-  for (int i = 0; i < n; ++i) {
-    items[i].tmp = tmp0 + (size_t)(i % chunk) * DC.bs_nn;
-    items[i].winner = win0 + (size_t)(i % chunk) * DC.bs_nn;
-  }
-  HIPCHK(hipMemcpyAsync(DC.stage, items.data(), (size_t)n * sizeof(RelocItem), hipMemcpyHostToDevice, DC.stream));
-  const RelocItem* d_items = reinterpret_cast<const RelocItem*>(DC.stage);
-  for (int c0 = 0; c0 < n; c0 += chunk)
-    HIPCHK(launch_relocate_batch(d_items + c0, std::min(chunk, n - c0), NNmax, DC.stream));
+  for (auto& items : rounds)
+    if (int rc = relocate_maps(DC, items, NNmax)) return rc;
   return HASTAR_OK;
 }
 

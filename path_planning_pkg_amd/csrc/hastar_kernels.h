@@ -30,8 +30,6 @@ hipError_t launch_init_nodemap(const PlannerDev& P, hipStream_t st);
 hipError_t launch_init_nodemap_batch(const PlannerDev& P, char* base, size_t stride, int n, hipStream_t st);
 hipError_t launch_clear_bitmaps(uint32_t* const* ptrs, int n, size_t words, hipStream_t st);
 hipError_t launch_decay(float* occ, size_t NN, float lp_free, float lp_min, float lp_max, hipStream_t st);
-hipError_t launch_relocate(int N, float c, float s, float ox, float oy, const float* src, float* dst, int* winner,
-                           hipStream_t st);
 hipError_t launch_raster_boxes(float* occ, int* cnt, int N, const int* rp, const float* dl, const int* ids, int nid,
                                float c, float s, float lp_min, float lp_max, int row0, int row1, hipStream_t st);
 hipError_t launch_raster_lines(float* occ, int* cnt, int N, int n45, int n2, float res, const float* lp,
@@ -39,6 +37,7 @@ hipError_t launch_raster_lines(float* occ, int* cnt, int N, int n45, int n2, flo
                                float lp_max, int row0, int row1, hipStream_t st);
 hipError_t launch_decay_batch(const DecayItem* items, int n, size_t max_cells, hipStream_t st);
 hipError_t launch_relocate_batch(const RelocItem* items, int n, size_t max_cells, hipStream_t st);
+hipError_t launch_relocate_invert(const RelocItem* items, int n, size_t max_cells, hipStream_t st);
 hipError_t launch_raster_boxes_batch(const RasterMap* maps, const RasterBox* boxes, int nbox, hipStream_t st);
 hipError_t launch_copy_batch(const CopyItem* items, int n, const float* src, hipStream_t st);
 struct VelParams { float max_velocity, coast_velocity, max_lat_acc, max_lat_acc_sqr, max_long_acc, max_long_dec; };

@@ -2840,31 +2840,6 @@ __global__ void k_decay(float* __restrict__ occ, size_t NN, float lp_free, float
     occ[t] = stl_max(stl_min(occ[t] + lp_free, lp_max), lp_min);
 }
 
-// Grid3D::relocate_obstacles (Grid3D.cpp:169-203), pass 1: every source cell claims its
-// destination; the reference's row-major loop lets the LAST writer win, i.e. the
-// largest linear source index — atomicMax makes that order-independent.
-__global__ void k_relocate_claim(int N, float c, float s, float ox, float oy, int* __restrict__ winner) {
-  const size_t NN = (size_t)N * N;
-  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x) {
-    const float fi = (float)(int)(t / N), fj = (float)(int)(t % N);
-    float x = fi * c + fj * s;
-    float y = -fi * s + fj * c;
-    x = x + ox;
-    y = y + oy;
-    const int a = trunc_f(roundf(x)), b = trunc_f(roundf(y));
-    if (a > -1 && a < N && b > -1 && b < N) atomicMax(&winner[(size_t)a * N + b], (int)t);
-  }
-}
-// pass 2: gather (cells nobody claimed become 0, the fresh map's value)
-__global__ void k_relocate_gather(size_t NN, const float* __restrict__ src, int* __restrict__ winner,
-                                  float* __restrict__ dst) {
-  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < NN; t += (size_t)gridDim.x * blockDim.x) {
-    const int w = winner[t];
-    dst[t] = (w >= 0) ? src[w] : 0.0f;
-    winner[t] = -1;
-  }
-}
-
 // Grid2D::update_obstacles(boxes) (Grid2D.cpp:99-139).  Boxes are applied in order (one
 // workgroup walks them); inside one box every sub-sample adds the same delta and clamps,
 // so a cell hit m times gets that step m times — counted with atomics, applied once per
@@ -2968,6 +2943,83 @@ __global__ __launch_bounds__(256) void k_relocate_gather_batch(const RelocItem* 
     }
   }
 }
+// ---- relocation by inversion (round 6): no claim table, no atomics ----------------------
+// Every DESTINATION cell finds its winning source itself: the relocation is a rotation by
+// (c, s) plus an offset, so the sources that round to destination (a, b) lie in the preimage
+// of the unit square around (a, b), a unit square around the inverse-rotated point
+// (i*, j*) = R^-1 ((a, b) - o) — within 0.7071 of it per axis, i.e. among the at most 2 x 2
+// lattice points with |i - i*| <= 0.75 and |j - j*| <= 0.75.  Each candidate is tested with the
+// reference's own forward arithmetic (the claim kernel's float expression), and the largest
+// linear source index among the hits wins: the reference's row-major loop writes
+// obstacle_map_new[i_new][j_new] last for the largest i * N + j (Grid3D.cpp:187-197).  The
+// float inverse only chooses candidates (its error, below 1e-3 cell for coordinates under 1e4,
+// is far inside the 0.043 margin); the forward test decides.  It compares in the float domain:
+// static_cast<int>(std::round(x)) == a for a destination a >= 0 holds exactly when
+// a - 0.5 <= x < a + 0.5 (a >= 1) or -0.5 < x < 0.5 (a = 0) — round half away from zero, and
+// a +- 0.5 is exact in float — which is what trunc_f(roundf(x)) == a computes.
+// The gather writes the relocated map into scratch (a destination may take its value from any
+// cell of the old map), and k_relocate_copy_batch copies it back.
+// The 2 x 2 candidates share their products: (i0, i0 + 1) * c and * s, (j0, j0 + 1) * s and * c
+// as packed pairs (v_pk_mul_f32 / v_pk_add_f32 round each lane as the scalar ops do, and
+// -ffp-contract=off keeps every product and sum separately rounded), the tests are evaluated
+// branch-free, and the largest hit in row-major order (i0, j0) < (i0, j0 + 1) < (i0 + 1, j0) <
+// (i0 + 1, j0 + 1) is selected.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int reloc_winner(int a, int b, int N, float c, float s, float ox, float oy) {
+  const float fa = (float)a, fb = (float)b;
+  const float dx = fa - ox, dy = fb - oy;
+  const float is = dx * c - dy * s, js = dx * s + dy * c;  // R^-1 (x - o), candidates only
+  const float fi0 = ceilf(is - 0.75f), fj0 = ceilf(js - 0.75f);
+  const int i0 = (int)fi0, j0 = (int)fj0;
+  const f2v fi = {fi0, fi0 + 1.0f}, fj = {fj0, fj0 + 1.0f};  // exact: integers far below 2^24
+  const f2v cc = {c, c}, ss = {s, s};
+  const f2v ic = fi * cc, is2 = fi * ss, js2 = fj * ss, jc = fj * cc;
+  const f2v oxx = {ox, ox}, oyy = {oy, oy};
+  // x = fi * c + fj * s + ox, y = -fi * s + fj * c + oy, for dj = 0 and dj = 1 (lanes: di)
+  const f2v x0 = (ic + (f2v){js2.x, js2.x}) + oxx, x1 = (ic + (f2v){js2.y, js2.y}) + oxx;
+  const f2v y0 = ((f2v){jc.x, jc.x} - is2) + oyy, y1 = ((f2v){jc.y, jc.y} - is2) + oyy;
+  const float alo = fa - 0.5f, ahi = fa + 0.5f, blo = fb - 0.5f, bhi = fb + 0.5f;
+  const bool a0 = a == 0, b0 = b == 0;
+  auto inx = [&](float x) { return ((x > alo) | (!a0 & (x == alo))) & (x < ahi); };
+  auto iny = [&](float y) { return ((y > blo) | (!b0 & (y == blo))) & (y < bhi); };
+  const bool vi0 = (unsigned)i0 < (unsigned)N, vi1 = (unsigned)(i0 + 1) < (unsigned)N;
+  const bool vj0 = (unsigned)j0 < (unsigned)N, vj1 = (unsigned)(j0 + 1) < (unsigned)N;
+  const bool h00 = vi0 & vj0 & inx(x0.x) & iny(y0.x), h01 = vi0 & vj1 & inx(x1.x) & iny(y1.x);
+  const bool h10 = vi1 & vj0 & inx(x0.y) & iny(y0.y), h11 = vi1 & vj1 & inx(x1.y) & iny(y1.y);
+  const int base = i0 * N + j0;
+  return h11 ? base + N + 1 : h10 ? base + N : h01 ? base + 1 : h00 ? base : -1;
+}
+// Gather of every map of a chunk into its scratch, in 2-D tiles so that one wave's gather stays
+// compact in the source: a wave owns an 8 x 8 destination block (its preimage, a rotated 8 x 8,
+// touches ~11 source rows x 1-2 lines instead of the up to 64 lines of a 64-cell row segment),
+// four waves side by side make a 32-wide row band (8 full 128-B lines written per pass), and a
+// workgroup walks RELOC_TILE_ROWS / 8 such bands.  blockIdx.y walks the items; blockIdx.x is the
+// tile, dealt so that the 8 XCDs (blocks b and b + 8 share one) each take a contiguous band of
+// the map: tiles near each other — whose preimages overlap — share one L2.
+constexpr int RELOC_TILE_ROWS = 32;
+__global__ __launch_bounds__(256) void k_relocate_invert_batch(const RelocItem* __restrict__ items, int n) {
+  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+  for (int q = blockIdx.y; q < n; q += gridDim.y) {
+    const RelocItem it = items[q];
+    const int N = it.N;
+    const int tx = (N + 31) / 32, ty = (N + RELOC_TILE_ROWS - 1) / RELOC_TILE_ROWS;
+    const int per_xcd = (int)gridDim.x / 8;  // gridDim.x is a multiple of 8
+    const int tile = ((int)blockIdx.x & 7) * per_xcd + ((int)blockIdx.x >> 3);
+    const int b = (tile % tx) * 32 + wave * 8 + (lane & 7);
+    const int a_top = (tile / tx) * RELOC_TILE_ROWS + (lane >> 3);
+    if (tile >= tx * ty || b >= N) continue;
+#pragma unroll
+    for (int r = 0; r < RELOC_TILE_ROWS; r += 8) {
+      const int a = a_top + r;
+      if (a < N) {
+        const int src = reloc_winner(a, b, N, it.c, it.s, it.ox, it.oy);
+        const float v = src >= 0 ? ((const GAS float*)it.occ)[src] : 0.0f;  // unclaimed: the fresh map's 0
+        ((GAS float*)it.tmp)[(size_t)a * N + b] = v;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_relocate_copy_batch(const RelocItem* __restrict__ items, int n) {
   for (int q = blockIdx.y; q < n; q += gridDim.y) {
     const RelocItem it = items[q];
@@ -3320,14 +3372,6 @@ hipError_t launch_decay(float* occ, size_t NN, float fr, float mn, float mx, hip
   hipLaunchKernelGGL(k_decay, dim3(blocks), dim3(256), 0, st, occ, NN, fr, mn, mx);
   return hipGetLastError();
 }
-hipError_t launch_relocate(int N, float c, float s, float ox, float oy, const float* src, float* dst, int* winner,
-                           hipStream_t st) {
-  const size_t NN = (size_t)N * N;
-  const int blocks = (int)((NN + 255) / 256 < 4096 ? (NN + 255) / 256 : 4096);
-  hipLaunchKernelGGL(k_relocate_claim, dim3(blocks), dim3(256), 0, st, N, c, s, ox, oy, winner);
-  hipLaunchKernelGGL(k_relocate_gather, dim3(blocks), dim3(256), 0, st, NN, src, winner, dst);
-  return hipGetLastError();
-}
 hipError_t launch_raster_boxes(float* occ, int* cnt, int N, const int* rp, const float* dl, const int* ids, int nid,
                                float c, float s, float mn, float mx, int r0, int r1, hipStream_t st) {
   if (nid <= 0) return hipSuccess;
@@ -3348,6 +3392,19 @@ static dim3 batch_grid(int n, size_t cells) {
 hipError_t launch_decay_batch(const DecayItem* items, int n, size_t max_cells, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_decay_batch, batch_grid(n, max_cells), dim3(256), 0, st, items, n);
+  return hipGetLastError();
+}
+// Relocation of n maps by inversion (k_relocate_invert_batch into each item's tmp, then
+// k_relocate_copy_batch back): 16 N^2 bytes per map, no claim table.
+hipError_t launch_relocate_invert(const RelocItem* items, int n, size_t max_cells, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  int N = 1;
+  while ((size_t)N * N < max_cells) ++N;
+  // one workgroup per tile of the largest map, rounded up to a multiple of the 8 XCDs
+  const size_t tiles = (size_t)((N + 31) / 32) * ((N + RELOC_TILE_ROWS - 1) / RELOC_TILE_ROWS);
+  const unsigned bx = (unsigned)((tiles + 7) / 8 * 8);
+  hipLaunchKernelGGL(k_relocate_invert_batch, dim3(bx, (unsigned)std::min(n, 65535)), dim3(256), 0, st, items, n);
+  hipLaunchKernelGGL(k_relocate_copy_batch, batch_grid(n, max_cells), dim3(256), 0, st, items, n);
   return hipGetLastError();
 }
 hipError_t launch_relocate_batch(const RelocItem* items, int n, size_t max_cells, hipStream_t st) {

@@ -19,7 +19,7 @@ for line in sys.stdin:
     if k == 'name': cur = {'name': v}; rows.append(cur)
     else: cur[k] = v
 for r in rows:
-    if 'search' in r['name'] and 'k_' not in r['name']:
+    if (('search' in r['name'] and 'k_' not in r['name']) or 'reloc' in r['name']):
         print(r['name'][:60], 'vgpr', r.get('vgpr_count'), 'agpr', r.get('agpr_count'), 'sgpr', r.get('sgpr_count'), 'sgpr_spill', r.get('sgpr_spill_count'),
               'vgpr_spill', r.get('vgpr_spill_count'), 'scratch', r.get('private_segment_fixed_size'), 'lds', r.get('group_segment_fixed_size'))
 "
