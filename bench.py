@@ -254,7 +254,9 @@ def main():
         if args.backend == "nccl":
             torch.cuda.set_device(local_rank)
         dist.init_process_group(args.backend)
-    device = local_rank
+    # HASTAR_BENCH_DEVICE: put every rank on one device (a multi-rank rehearsal on a one-GPU box,
+    # with --backend gloo); by default rank r uses GPU LOCAL_RANK
+    device = int(os.environ.get("HASTAR_BENCH_DEVICE", local_rank))
     red_dev = f"cuda:{device}" if args.backend == "nccl" and not args.dry_run else "cpu"
     if args.dry_run:
         return run_dry(args, dist, rank, world, red_dev)
@@ -312,7 +314,10 @@ def main():
     # (host-side bookkeeping of the bench, outside the step's time)
     strat = sorted(set(range(0, B, 64)) | set(np.argsort(-r0.stats["pops"], kind="stable")[:8].tolist()))
     cold_sample = {i: r0.result(i) for i in strat} if (rank == 0 and not args.no_cpu_baseline) else None
-    cold_all = (r0.stats.copy(), r0.cost.copy(), r0.ok.copy()) if (rank == 0 and args.parity_all) else None
+    cold_all = None
+    if rank == 0 and args.parity_all:  # every query's outcome, paths as digests of their bits
+        cold_all = (r0.stats.copy(), r0.cost.copy(), r0.ok.copy(),
+                    [path_digest(r0.result(i)) for i in range(B)])
     cold_pops = int(r0.stats["pops"].sum())
     r0_pops = r0.stats["pops"].copy()
     cold_s, cold_pops_all = reduce_over_ranks(dist, cold_s, cold_pops, f"cuda:{device}")
@@ -985,10 +990,19 @@ def parity_sample(cfgs, gpu, qids, gpu_last=None, replans=1):
     return out
 
 
-def parity_all(cfgs, stats, cost, ok, qids):
+def path_digest(r):
+    """A digest of a result's path and curvature bits (parity_all compares these)."""
+    import hashlib
+    h = hashlib.blake2b(digest_size=16)
+    h.update(np.ascontiguousarray(r["path"], np.float32).tobytes())
+    h.update(np.ascontiguousarray(r["curvature"], np.float32).tobytes())
+    return h.digest()
+
+
+def parity_all(cfgs, stats, cost, ok, paths, qids):
     """Every query of the batch (`--parity-all`): the first (cold) step's outcome against the
-    oracle's reset + find_path on the same maps, on the host's threads: success, cost bits and
-    every statistic and digest (paths: parity_sample's stratified subset)."""
+    oracle's reset + find_path on the same maps, on the host's threads: success, cost bits,
+    every statistic and digest, and the path and curvature bits (as 128-bit digests)."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle.pyoracle import OraclePlanner
     from tests.scenarios import drive
@@ -1002,17 +1016,19 @@ def parity_all(cfgs, stats, cost, ok, qids):
         r = o.find_path(cfgs[i][1]["vel"], cfgs[i][1]["start"])
         o.close()
         same = (bool(ok[i]) == bool(r["ok"]) and np.float32(cost[i]).tobytes() == np.float32(r["cost"]).tobytes()
-                and all((int(stats[k][i]) - int(r["stats"][k])) % (1 << 64) == 0 for k in keys))
-        return same, int(r["stats"]["pops"])
+                and all((int(stats[k][i]) - int(r["stats"][k])) % (1 << 64) == 0 for k in keys)
+                and paths[i] == path_digest(r))
+        return same, int(r["stats"]["pops"]), len(r["path"])
 
     t0 = time.perf_counter()
     with ThreadPoolExecutor(cpu_threads()) as ex:
         res = list(ex.map(run, range(len(cfgs))))
-    bad = [int(qids[i]) for i, (same, _) in enumerate(res) if not same]
+    bad = [int(qids[i]) for i, (same, _, _) in enumerate(res) if not same]
     return {"queries": len(cfgs), "bit_exact": not bad, "mismatched_queries": bad[:16], "n_mismatched": len(bad),
-            "pops_checked": int(sum(p for _, p in res)), "oracle_s": time.perf_counter() - t0,
+            "pops_checked": int(sum(p for _, p, _ in res)), "path_poses_checked": int(sum(k for _, _, k in res)),
+            "oracle_s": time.perf_counter() - t0,
             "note": "every query's first (cold) step against the oracle's reset + find_path: success, cost bits, "
-                    "statistics, pop/closed digests"}
+                    "statistics, pop/closed digests, path and curvature bits (digests)"}
 
 
 def cpu_baseline(cfgs, gpu_results, budget_s, replans, lat_ids, sample=None):
