@@ -12,6 +12,8 @@ HybridAStar.cpp:107) does.
 The bar is the one of test_gpu_parity.py: bit-identical pops, successors, A* pops, shots,
 ordered pop digest, closed-set digest, path, curvature and cost.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -300,11 +302,13 @@ def test_cfg4_row_sharded_map_build(gpu, oracle_lib):
 
 # ------------------------------------------------------------------ cfg5 (replans) -----
 def test_cfg5_replan_loop_parity(gpu, oracle_lib):
-    """BASELINE configs[4] at its own size: 1024x1024x72 maps, K = 200 moving boxes, bench
-    pair ids 0..7 (bench.py run_cfg5), 3 batched ticks WITHOUT reset (local_planner.cpp:
-    204-205, 241, 316): memo and stale node-map values carry over between ticks."""
+    """BASELINE configs[4] at its own size: 1024x1024x72 maps, K = 200 moving boxes, ALL 64 bench
+    pairs (ids 0..63, bench.py run_cfg5), 4 batched ticks WITHOUT reset (local_planner.cpp:
+    204-205, 241, 316): memo and stale node-map values carry over between ticks.  The oracle's
+    replays run on host threads (each pair's calls stay in order)."""
+    from concurrent.futures import ThreadPoolExecutor
     pairs = []
-    for q in range(8):
+    for q in range(64):
         pairs += replan_pairs(1024, 72, 200, 1, seed=1000 + q)
     gs, os_ = [], []
     for cfg, proto, _ in pairs:
@@ -312,13 +316,20 @@ def test_cfg5_replan_loop_parity(gpu, oracle_lib):
         gs.append(g)
         os_.append(o)
     bufs = gpu.BatchBuffers(gs, cap=8192)
-    for tick in range(3):
+    for tick in range(4):
         starts = [replan_tick_inputs(proto, v, tick)[0] for _, proto, v in pairs]
         br = gpu.find_path_batch_arrays(gs, [proto["vel"] for _, proto, _ in pairs], starts, buffers=bufs)
-        for i, (o, (_, proto, v)) in enumerate(zip(os_, pairs)):
-            compare_results(br.result(i), o.find_path(proto["vel"], starts[i]), f"cfg5 tick {tick} pair {i}")
+
+        def oracle_tick(i):
+            _, proto, v = pairs[i]
+            r = os_[i].find_path(proto["vel"], starts[i])
+            replan_tick(os_[i], proto, v, tick)
+            return r
+        with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+            ores = list(ex.map(oracle_tick, range(len(pairs))))
+        for i, (_, proto, v) in enumerate(pairs):
+            compare_results(br.result(i), ores[i], f"cfg5 tick {tick} pair {i}")
             replan_tick(gs[i], proto, v, tick)
-            replan_tick(o, proto, v, tick)
 
 
 # ------------------------------------------------- device-resident velocity profile ----
