@@ -71,15 +71,19 @@ def test_deferred_tree_replay_builds_the_same_tree(tmp_path):
 
 def test_relaxed_entry_point_rejects_bad_arguments():
     """hastar_find_path_relaxed_batch validates its arguments before touching a device, and
-    hastar_relaxed_opts has the C layout the ctypes mirror declares (seven 4-byte fields)."""
+    hastar_relaxed_opts has the C layout the ctypes mirror declares (nine 4-byte fields: round 6
+    appended reverse_cost and gear_cost); so does the direction-returning entry point."""
     from path_planning_pkg_amd.capi import HastarRelaxedOpts
     from path_planning_pkg_amd.planner import load_library
     L = load_library()
-    assert C.sizeof(HastarRelaxedOpts) == 28
+    assert C.sizeof(HastarRelaxedOpts) == 36
+    assert HastarRelaxedOpts.reverse_cost.offset == 28 and HastarRelaxedOpts.gear_cost.offset == 32
     f = (C.c_float * 3)()
     i = (C.c_int * 1)()
     rc = L.hastar_find_path_relaxed_batch(None, 0, f, f, f, f, 1, i, f, i, None, None)
     assert rc == -22  # HASTAR_EINVAL
+    rc = L.hastar_find_path_relaxed_batch_dir(None, 0, f, f, f, f, None, 1, i, f, i, None, None)
+    assert rc == -22
 
 
 def test_route_score_cold_order_key():
