@@ -193,10 +193,24 @@ typedef struct hastar_relaxed_opts {
   int h_coarse;    /* the Dijkstra field runs over blocks of h_coarse x h_coarse map cells (1, 2 or 4):
                       a block is passable when any of its cells is, and a cell's heuristic is its
                       block's distance [2] */
+  float reverse_cost; /* > 0: a REVERSING motion model, which the reference does not have
+                         (VehicleModel.cpp:97-101 drives forward only; BASELINE.json configs[2] asks
+                         for "Reeds-Shepp reversals"): every steering also gets its reverse arc, whose
+                         action cost is multiplied by reverse_cost, and the Dubins heuristic and shots
+                         become Reeds-Shepp ones (csrc/hastar_rs.h) whose reverse segments cost
+                         reverse_cost x their length [0: forward only, the reference's model] */
+  float gear_cost;    /* with reverse_cost > 0: metres added at each change of direction [0] */
 } hastar_relaxed_opts;
 int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, const float* vel_init, const float* starts,
                                    float* xyh, float* curv, int cap, int* len, float* cost, int* ok,
                                    hastar_stats* stats, const hastar_relaxed_opts* opts);
+/* The same, plus each pose's direction of travel: dir[i * cap + k] = +1 when pose k of path i
+   was reached driving forward, -1 in reverse (always +1 without reverse_cost; the path's first
+   pose, at the goal end, carries the direction of the motion that reached the goal).  dir may
+   be NULL. */
+int hastar_find_path_relaxed_batch_dir(const hastar_handle* hs, int n, const float* vel_init, const float* starts,
+                                       float* xyh, float* curv, signed char* dir, int cap, int* len, float* cost, int* ok,
+                                       hastar_stats* stats, const hastar_relaxed_opts* opts);
 
 /* get_obstacles() (HybridAStar.cpp:62-65): copies the N x N log-odds map (row i = x cell). */
 int hastar_get_obstacles(hastar_handle h, float* out);

@@ -18,6 +18,13 @@ int hastar_test_math(int fn, const float* a, const float* b, float* out, int n);
 int hastar_test_field(hastar_handle h, const float* poses, int n, float* out);
 /* Dubins::get_shortest_path_length of n start poses to one goal; word = 0 RSR, 1 RSL, 2 LSR, 3 LSL. */
 int hastar_test_dubins_len(float r_min, const float* starts, int n, const float goal[3], float* out, int* word);
+/* The relaxed mode's Reeds-Shepp code (csrc/hastar_rs.h; no reference counterpart): for n start
+   poses and one goal, turning radius r_min: the shortest length (metres), its word (0..17,
+   oracle/reeds_shepp.py WORDS) and 5 signed segment lengths (radius units, seg[5 i ..]), and the
+   grouped-lane length the successor heuristic uses, with groups of 4 and 16 lanes
+   (len_groups[2 i], [2 i + 1]). */
+int hastar_test_reeds_shepp(float r_min, const float* starts, int n, const float goal[3], float* len, int* word,
+                            float* seg, float* len_groups);
 /* Dubins::get_shortest_path from start to the handle's goal pose (grid frame), sampled. */
 int hastar_test_dubins_path(hastar_handle h, const float start[3], float* xyh, float* curv, int cap, int* n,
                             float* length, int* first_arc_gt_90);

@@ -78,6 +78,8 @@ class HastarRelaxedOpts(C.Structure):
         ("h_weight", C.c_float),
         ("reuse_heuristic", C.c_int),
         ("h_coarse", C.c_int),
+        ("reverse_cost", C.c_float),
+        ("gear_cost", C.c_float),
     ]
 
 

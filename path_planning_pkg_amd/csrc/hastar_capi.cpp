@@ -255,6 +255,8 @@ struct DeviceCtx {
   int r_asked = 0;  // workgroups the pool was sized for (fewer when HBM capped it)
   RelaxField* d_rfields = nullptr;   // per-planner heuristic fields of a relaxed batch
   size_t rfields_cap = 0;
+  signed char* d_dir = nullptr;      // per-pose directions of a relaxed batch (hastar_find_path_relaxed_batch_dir)
+  size_t dir_cap = 0;
 };
 
 // A larger arena that continues one parked search (hastar_find_path_batch).
@@ -2384,6 +2386,13 @@ int relax_acquire(DeviceCtx& D, int N, int nodes, int want) {
 extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, const float* vel, const float* starts,
                                               float* xyh, float* curv, int cap, int* len, float* cost, int* ok,
                                               hastar_stats* stats, const hastar_relaxed_opts* opts) {
+  return hastar_find_path_relaxed_batch_dir(hs, n, vel, starts, xyh, curv, nullptr, cap, len, cost, ok, stats, opts);
+}
+
+extern "C" int hastar_find_path_relaxed_batch_dir(const hastar_handle* hs, int n, const float* vel, const float* starts,
+                                                  float* xyh, float* curv, signed char* dir, int cap, int* len,
+                                                  float* cost, int* ok, hastar_stats* stats,
+                                                  const hastar_relaxed_opts* opts) {
   if (!hs || n <= 0 || !vel || !starts || !len || !cost || !ok || cap < 0 || (cap > 0 && (!xyh || !curv)))
     return fail(HASTAR_EINVAL, "bad argument");
   const int dev = hs[0] ? hs[0]->device : -1;
@@ -2400,6 +2409,10 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
   rp.h_weight = opts && opts->h_weight > 0.0f ? opts->h_weight : 1.35f;
   rp.h_coarse = opts && opts->h_coarse > 0 ? opts->h_coarse : 2;
   if (rp.h_coarse != 1 && rp.h_coarse != 2 && rp.h_coarse != 4) return fail(HASTAR_EINVAL, "h_coarse must be 1, 2 or 4");
+  rp.rev_cost = opts && opts->reverse_cost > 0.0f ? opts->reverse_cost : 0.0f;
+  rp.gear_cost = opts && opts->reverse_cost > 0.0f && opts->gear_cost > 0.0f ? opts->gear_cost : 0.0f;
+  if (opts && (!(opts->reverse_cost >= 0.0f) || !(opts->gear_cost >= 0.0f)))
+    return fail(HASTAR_EINVAL, "reverse_cost and gear_cost must be >= 0");
   const int nodes = opts && opts->max_nodes > 0 ? opts->max_nodes : (1 << 18);
   HIPCHK(hipSetDevice(dev));
   DeviceCtx& DC = *hs[0]->dc;
@@ -2443,6 +2456,25 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
     HIPCHK(hipMemcpyAsync(DC.d_rfields, fields.data(), (size_t)n * sizeof(RelaxField), hipMemcpyHostToDevice, st));
   }
   rp.progress = relaxed_progress();
+  // per-pose directions: a device slab of n x (the largest output buffer), copied out below
+  int dstride = 0;
+  if (dir && cap > 0) {
+    for (int i = 0; i < n; ++i) dstride = std::max(dstride, hs[i]->desc.out_cap);
+    const size_t bytes = (size_t)n * dstride;
+    if (bytes > DC.dir_cap) {
+      HIPCHK(hipStreamSynchronize(st));
+      if (DC.d_dir) hipFree(DC.d_dir);
+      DC.d_dir = nullptr;
+      DC.dir_cap = 0;
+      if (hipMalloc(reinterpret_cast<void**>(&DC.d_dir), bytes) != hipSuccess) {
+        DC.d_dir = nullptr;
+        return fail(HASTAR_ENOMEM, "relaxed directions: hipMalloc failed");
+      }
+      DC.dir_cap = bytes;
+    }
+    rp.dir_out = DC.d_dir;
+    rp.dir_stride = dstride;
+  }
   HIPCHK(hipEventRecord(DC.ev0, st));
   HIPCHK(launch_relaxed(DC.d_descs, n, DC.d_rarenas, std::min(want, DC.n_rarenas), DC.d_next, rp,
                         reuse ? DC.d_rfields : nullptr, st));
@@ -2460,7 +2492,16 @@ extern "C" int hastar_find_path_relaxed_batch(const hastar_handle* hs, int n, co
   float ms = 0.0f;
   hipEventElapsedTime(&ms, DC.ev0, DC.ev1);
   g_last_ms = ms;
-  return finish_batch(DC, hs, n, xyh, curv, cap, len, cost, ok, stats, false);
+  const int rc = finish_batch(DC, hs, n, xyh, curv, cap, len, cost, ok, stats, false);
+  if (rp.dir_out) {
+    std::vector<signed char> hd((size_t)n * dstride);
+    HIPCHK(hipMemcpy(hd.data(), DC.d_dir, hd.size(), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) {
+      const int k = std::min(std::min(len[i], cap), dstride);
+      std::memcpy(dir + (size_t)i * cap, hd.data() + (size_t)i * dstride, (size_t)std::max(k, 0));
+    }
+  }
+  return rc;
 }
 
 extern "C" {
@@ -2865,6 +2906,31 @@ int hastar_test_dubins_len(float r, const float* starts, int n, const float goal
   HIPCHK(hipMemcpy(word, dw, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
   hipFree(ds);
   hipFree(dout);
+  hipFree(dw);
+  return HASTAR_OK;
+}
+
+int hastar_test_reeds_shepp(float r, const float* starts, int n, const float goal[3], float* len, int* word, float* seg,
+                            float* len_groups) {
+  if (n <= 0) return HASTAR_OK;
+  if (!starts || !goal || !len || !word || !seg || !len_groups || !(r > 0.0f)) return fail(HASTAR_EINVAL, "bad argument");
+  float *ds = nullptr, *dl = nullptr, *dseg = nullptr, *dg = nullptr;
+  int* dw = nullptr;
+  HIPCHK(dalloc(&ds, (size_t)n * 3));
+  HIPCHK(dalloc(&dl, (size_t)n));
+  HIPCHK(dalloc(&dseg, (size_t)n * 5));
+  HIPCHK(dalloc(&dg, (size_t)n * 2));
+  HIPCHK(dalloc(&dw, (size_t)n));
+  HIPCHK(hipMemcpy(ds, starts, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(launch_test_rs(r, ds, n, goal[0], goal[1], goal[2], dl, dw, dseg, dg, nullptr));
+  HIPCHK(hipMemcpy(len, dl, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(word, dw, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(seg, dseg, (size_t)n * 5 * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(len_groups, dg, (size_t)n * 2 * sizeof(float), hipMemcpyDeviceToHost));
+  hipFree(ds);
+  hipFree(dl);
+  hipFree(dseg);
+  hipFree(dg);
   hipFree(dw);
   return HASTAR_OK;
 }

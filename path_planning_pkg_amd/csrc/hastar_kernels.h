@@ -18,6 +18,8 @@ int search_slots_per_cu();
 hipError_t launch_relaxed(const PlannerDev* d_descs, int n, const RelaxArena* d_arenas, int n_arenas, int* d_next,
                           const RelaxParams& rp, RelaxField* d_fields, hipStream_t st);
 int relaxed_waves();
+hipError_t launch_test_rs(float r, const float* starts, int n, float gx, float gy, float gh, float* len, int* word,
+                          float* seg, float* len_groups, hipStream_t st);
 hipError_t launch_grid3d_neighbors(const PlannerDev* d_desc, const float node[5], int nci, int nbin, float* out,
                                    int* cells, int cap, int* count, int* neglect, hipStream_t st);
 hipError_t launch_grid3d_check_path(const PlannerDev* d_desc, const float* xyh, int n, int* is_free, hipStream_t st);

@@ -300,6 +300,13 @@ struct RelaxParams {
   float h_weight;   // f = g + h_weight x max(h, Dubins length) (1: the reference's f)
   int h_coarse;     // the Dijkstra field's block side in map cells (1, 2 or 4)
   unsigned* progress;  // debug (HASTAR_RELAXED_PROGRESS): per-wave phase words in host memory, or null
+  // reversing motion model (round 6; hastar_relaxed_opts::reverse_cost): rev_cost > 0 adds the
+  // reverse arcs (action cost x rev_cost) and makes the heuristic and the shots Reeds-Shepp
+  // (hastar_rs.h); 0 keeps the reference's forward model
+  float rev_cost;
+  float gear_cost;      // added to a motion or shot segment that changes the direction of travel (m)
+  signed char* dir_out; // per-pose direction (+1 forward, -1 reverse) of planner i's path at dir_out + i * dir_stride, or null
+  int dir_stride;
 };
 
 }  // namespace hastar

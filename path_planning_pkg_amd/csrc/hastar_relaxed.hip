@@ -26,6 +26,7 @@
 
 #include "hastar_device.h"
 #include "hastar_kernels.h"
+#include "hastar_rs.h"
 
 namespace hastar {
 
@@ -346,14 +347,87 @@ __device__ __forceinline__ float relaxed_h(const PlannerDev& P, const float* dis
 // closed set and the lazy A* (the heuristic is the Dijkstra field).  Every decision is keyed by
 // values (g, f and the node's tie), never by the order in which the round's wavefronts run, so
 // a query gives the same path on every run.
+// RS sampling of a Reeds-Shepp shot (reversing model): poses every P.step metres of arc along
+// the path's segments from (x0, y0, h0), sample 0 the shooter's own pose; curv[i] carries the
+// segment's curvature with the sign of its direction of travel (-0.0f: a reverse straight);
+// sample 0 carries d_start, the direction that reached the shooter.
+// Returns the sample count, -1 when the scratch is too small, -2 at the first blocked chunk.
+__device__ inline int rs_sample(const PlannerDev& P, const RSPath& rp, float x0, float y0, float h0, float d_start,
+                                GAS float* xyh, GAS float* curv, int cap, int lane) {
+  const float r = P.r_min, st = P.step;
+  int cnt[5], base[5];
+  float sx[5], sy[5], sh[5];
+  int n = 1;
+  float x = x0, y = y0, h = h0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int kind = rs_kind(rp.word, k);
+    const float a = rp.seg[k];
+    const bool on = kind != RS_N && fabsf(a) > 1e-6f;
+    cnt[k] = on ? max(1, (int)ceilf(fabsf(a) * r / st)) : 0;
+    base[k] = n;
+    n += cnt[k];
+    sx[k] = x;
+    sy[k] = y;
+    sh[k] = h;
+    if (on) rs_step(kind, r, x, y, h, a, &x, &y, &h);
+  }
+  if (n > cap) return -1;
+  for (int b0 = 0; b0 < n; b0 += 64) {
+    const int i = b0 + lane;
+    bool bad = false;
+    if (i < n) {
+      float px = x0, py = y0, ph = h0, kc = 0.0f, d = d_start;
+      if (i > 0) {
+        // the segment holding sample i (constant indices after unrolling: no private arrays)
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+          if (cnt[q] > 0 && i >= base[q] && i < base[q] + cnt[q]) {
+            const int kind = rs_kind(rp.word, q);
+            const float a = rp.seg[q] * (float)(i - base[q] + 1) / (float)cnt[q];
+            rs_step(kind, r, sx[q], sy[q], sh[q], a, &px, &py, &ph);
+            kc = kind == RS_S ? 0.0f : 1.0f / r;
+            d = rp.seg[q] < 0.0f ? -1.0f : 1.0f;
+          }
+        }
+      } else {
+        kc = rs_kind(rp.word, 0) == RS_S ? 0.0f : 1.0f / r;
+      }
+      xyh[3 * i] = px;
+      xyh[3 * i + 1] = py;
+      xyh[3 * i + 2] = wrap_pi_f(ph);
+      curv[i] = copysignf(kc, d);
+      bad = sample_blocked(P, px, py);
+    }
+    if (__ballot(bad)) return -2;
+  }
+  return n;
+}
+// the cost of a Reeds-Shepp shot from a node travelling in direction cdir (1: reverse): forward
+// arc length, reverse arc length x rev_cost, and gear_cost per change of direction
+__device__ __forceinline__ float rs_cost(const RSPath& p, float r, float rev_cost, float gear_cost, int cdir) {
+  float c = 0.0f;
+  int d = cdir;
+  for (int k = 0; k < 5; ++k) {
+    const float a = p.seg[k];
+    if (rs_kind(p.word, k) == RS_N || fabsf(a) <= 1e-6f) continue;
+    const int dk = a < 0.0f ? 1 : 0;
+    c += fabsf(a) * r * (dk ? rev_cost : 1.0f) + (dk != d ? gear_cost : 0.0f);
+    d = dk;
+  }
+  return c;
+}
+
 __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, ApfStage& apfs,
                                const GoalC& GC, const float* dist, int hk, float hlim, int hs_x, int hs_y, float hw, int idx,
-                               int lane, uint2* list_n) {
+                               int lane, uint2* list_n, const RelaxParams& rp) {
+  const bool rev = rp.rev_cost > 0.0f;
   const Node3 cur = gload(&A.nodes[idx]);
   const uint32_t key = ufu(cur.key), tie = ufu((uint32_t)cur.r);
   const float cg = uff(cur.g), cf = uff(cur.f), cxp = uff(cur.x), cyp = uff(cur.y), chd = uff(cur.h),
               cvm = uff(cur.vmin);
   const int cci = ufi((int)(cur.cc >> 8));
+  const int cdir = ufi((int)(cur.cc & 1u));  // 1: the node was reached in reverse
   const int cx = key3_x(key), cy = key3_y(key), cbin = key3_bin(key);
   if (lane == 0) atomicAdd(&S.pops, 1);
   // goal test (Node3D::operator==: the cell only, Node3D.h:42).  The stages below run under
@@ -374,16 +448,24 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
   shot = ufi(shot);
   if (shot >= 0) {
     if (lane == 0) atomicAdd(&S.shots, 1);
-    int word = 0;
-    float prm[4];
     const float r = P.r_min;
-    const float L = dubins_shortest(r, cxp, cyp, chd, P.goal_x, P.goal_y, P.goal_h, &word, prm);
-    const Centres C = dubins_centres(r, cxp, cyp, chd, P.goal_x, P.goal_y, P.goal_h);
     GAS float* xyh = gp(A.dub_xyh) + (size_t)shot * A.dub_cap * 3;
     GAS float* curv = gp(A.dub_curv) + (size_t)shot * A.dub_cap;
-    // sampled and checked chunk by chunk: a blocked shot stops at its first blocked chunk
-    const int first_arc_long = ufi(fabsf(prm[1]) > (float)M_PI_2 ? 1 : 0);
-    const int n = first_arc_long ? -1 : ufi(dubins_sample<1>(P, C, word, prm, xyh, curv, A.dub_cap, lane));
+    float L;
+    int n;
+    if (rev) {  // Reeds-Shepp shot: the shortest of its 44 candidates, sampled and checked
+      const RSPath rsp = rs_best(r, cxp, cyp, chd, P.goal_x, P.goal_y, P.goal_h, lane);
+      L = rs_cost(rsp, r, rp.rev_cost, rp.gear_cost, cdir);
+      n = rsp.L < RS_INF ? ufi(rs_sample(P, rsp, cxp, cyp, chd, cdir ? -1.0f : 1.0f, xyh, curv, A.dub_cap, lane)) : -1;
+    } else {
+      int word = 0;
+      float prm[4];
+      L = dubins_shortest(r, cxp, cyp, chd, P.goal_x, P.goal_y, P.goal_h, &word, prm);
+      const Centres C = dubins_centres(r, cxp, cyp, chd, P.goal_x, P.goal_y, P.goal_h);
+      // sampled and checked chunk by chunk: a blocked shot stops at its first blocked chunk
+      const int first_arc_long = ufi(fabsf(prm[1]) > (float)M_PI_2 ? 1 : 0);
+      n = first_arc_long ? -1 : ufi(dubins_sample<1>(P, C, word, prm, xyh, curv, A.dub_cap, lane));
+    }
     wave_lds_sync();
     if (n > 0) {
       const int term = ufi(cur.prev);
@@ -397,18 +479,26 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
   }
   done = ufi(done);
   if (done) return;
-  // successors (VehicleModel.cpp:63-105) in groups of gs lanes, as in the exact kernel
+  // successors (VehicleModel.cpp:63-105) in groups of gs lanes, as in the exact kernel; with
+  // the reversing model every steering also gets a reverse arc (candidates span .. 2 span - 1)
   const int span = 2 * P.na + 1;
-  const int gsh = span <= 4 ? 4 : 2, gs = 1 << gsh;
+  const int gsh = (span <= 4 && !rev) ? 4 : 2, gs = 1 << gsh;
   int lo = cci - P.na;
   lo = lo < 0 ? 0 : lo;
   const int ca = lane >> gsh, sub = lane & (gs - 1);
-  const int ai = lo + ca;
-  bool cand = ca < span && ai < P.nsteer;
+  const bool back = rev && ca >= span;
+  const int ai = lo + (back ? ca - span : ca);
+  bool cand = ca < (rev ? 2 * span : span) && ai < P.nsteer;
   const int ia = cand ? ai : lo;
   const float cabs = gp(P.curv_abs)[ia];
-  const GAS float* ofs = &gp(P.off)[2 * ((size_t)ia * (P.bins + 1) + cbin)];
-  const float ofx = ofs[0], ofy = ofs[1], odth = gp(P.dth)[ia], oact = gp(P.act_cost)[ia];
+  const float odth = gp(P.dth)[ia];
+  // a reverse arc is a forward arc driven backwards: it starts at the heading h0 = h - dth whose
+  // forward arc ends at h, and moves by minus that arc's offset (the offset of h0's bin)
+  const float h_rev = wrap_pi_f(chd - odth);
+  const int obin = back ? heading_bin(h_rev, P.prec) : cbin;
+  const GAS float* ofs = &gp(P.off)[2 * ((size_t)ia * (P.bins + 1) + obin)];
+  const float ofx = ofs[0], ofy = ofs[1];
+  const float oact = gp(P.act_cost)[ia] * (back ? rp.rev_cost : 1.0f) + ((back ? 1 : 0) != cdir ? rp.gear_cost : 0.0f);
   float vm = 0.0f;
   if (cand && !allowed) {
     const float lat = cvm * cabs;
@@ -420,9 +510,9 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
   int sbin = 0, scx = 0, scy = 0;
   bool inb = false;
   if (cand) {
-    sx = cxp + ofx;
-    sy = cyp + ofy;
-    sh = wrap_pi_f(chd + odth);
+    sx = back ? cxp - ofx : cxp + ofx;
+    sy = back ? cyp - ofy : cyp + ofy;
+    sh = back ? h_rev : wrap_pi_f(chd + odth);
     sg = cg + oact;
     sbin = heading_bin(sh, P.prec);
     scx = trunc_f(sx / P.res);
@@ -436,7 +526,8 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
     occv = gp(P.occ)[cell];
     h2 = relaxed_h(P, dist, hk, scx, scy, hlim, hs_x, hs_y);
   }
-  const float dub = cand_dubins(P.r_min, GC, P.goal_h, sx, sy, sh, gs, lane);
+  const float dub = rev ? rs_length_group(P.r_min, sx, sy, sh, P.goal_x, P.goal_y, P.goal_h, gs, lane)
+                        : cand_dubins(P.r_min, GC, P.goal_h, sx, sy, sh, gs, lane);
   const float fc = apf_fused(P, apfs, cxp, cyp, sx, sy, sh, __ballot(lead), gs, lane);
   const bool kept = lead && occv < P.thr;
   const uint64_t km = __ballot(kept);
@@ -446,7 +537,7 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
     const float f = g + hw * stl_max(h2, dub);
     const uint32_t skey = key3(scx, scy, sbin);
     // equal-g offers for one key resolve by this tie, a hash of (parent key, action)
-    const uint32_t stie = rx_hash(key * 0x9e3779b1u + (uint32_t)ai);
+    const uint32_t stie = rx_hash(key * 0x9e3779b1u + (uint32_t)ai + (back ? 0x10000u : 0u));
     bool full = false;
     uint32_t tslot = 0;
     if (table_lower(A, skey, ((unsigned long long)__float_as_uint(g) << 32) | stie, &full, &tslot)) {
@@ -459,7 +550,7 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
         d.l = (int)tslot;
         d.r = (int)stie;
         d.p = NIL;
-        d.cc = (uint32_t)(lo + ca) << 8;
+        d.cc = ((uint32_t)ai << 8) | (back ? 1u : 0u);
         d.g = g;
         d.vmin = vm;
         d.x = sx;
@@ -477,7 +568,7 @@ __device__ __forceinline__ void relaxed_expand(const PlannerDev& P, const RelaxA
 }
 
 __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShared& S, const RelaxParams& rp,
-                            RelaxField* F, BucketEntry* bl) {
+                            RelaxField* F, BucketEntry* bl, int pi) {
   const int tid = threadIdx.x, NT = blockDim.x, wv = tid >> 6, lane = tid & 63;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   RPROG(0, 1);
@@ -652,7 +743,7 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
       if (e >= nE) break;
       RPROG(0, 5);
       RPROG(3, e);
-      relaxed_expand(P, A, S, S.apf[wv], GC, dist, rp.h_coarse, hlim, hs_x, hs_y, rp.h_weight, LE[e], lane, LA);
+      relaxed_expand(P, A, S, S.apf[wv], GC, dist, rp.h_coarse, hlim, hs_x, hs_y, rp.h_weight, LE[e], lane, LA, rp);
     }
     RPROG(0, 6);
     block_sync();
@@ -743,15 +834,19 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
         const GAS float* dcurv = gp(A.dub_curv) + (size_t)sw * A.dub_cap;
         const float cs = P.rot_c, sn = P.rot_s, ang = -P.grid_heading;
         path_len = dub_n + L;
+        signed char* dout = rp.dir_out ? rp.dir_out + (size_t)pi * rp.dir_stride : nullptr;
         for (int k = lane; k < path_len; k += 64) {
           float px, py, ph, kc = 0.0f;
           bool has_curv = true;
+          int dir = 1;
           if (k < dub_n) {
             const int q = dub_n - 1 - k;
             px = dxyh[3 * q];
             py = dxyh[3 * q + 1];
             ph = dxyh[3 * q + 2];
             kc = dcurv[q];
+            dir = signbit(kc) ? -1 : 1;  // a Reeds-Shepp sample's direction (rs_sample)
+            kc = fabsf(kc);
           } else {
             const int m = k - dub_n;
             const Node3 nd = gload(&A.nodes[A.chain[m]]);
@@ -759,8 +854,10 @@ __device__ void relaxed_one(const PlannerDev& P, const RelaxArena& A, RelaxShare
             py = nd.y;
             ph = nd.h;
             kc = gp(P.curv_abs)[nd.cc >> 8];
+            dir = (nd.cc & 1u) ? -1 : 1;
             has_curv = (m < L - 1);
           }
+          if (dout && k < rp.dir_stride) dout[k] = (signed char)dir;
           const float x0 = px - P.goal_x, y0 = py - P.goal_y;
           float xr = x0 * cs + y0 * sn;
           float yr = -x0 * sn + y0 * cs;
@@ -849,7 +946,7 @@ __global__ __launch_bounds__(RW * 64) void k_relaxed_search(const PlannerDev* __
     const int pi = S.planner;
     block_sync();
     if (pi >= n) break;
-    relaxed_one(descs[pi], A, S, rp, fields ? &fields[pi] : nullptr, relax_dyn_lds);
+    relaxed_one(descs[pi], A, S, rp, fields ? &fields[pi] : nullptr, relax_dyn_lds, pi);
   }
 }
 
@@ -873,5 +970,32 @@ hipError_t launch_relaxed(const PlannerDev* d_descs, int n, const RelaxArena* d_
   return hipGetLastError();
 }
 int relaxed_waves() { return RW; }
+
+// unit test of the Reeds-Shepp code (hastar_test_reeds_shepp): one wavefront per start pose:
+// rs_best's length (metres), word and segments (radius units), and rs_length_group's length with
+// groups of 4 and of 16 lanes
+__global__ __launch_bounds__(64) void k_test_rs(float r, const float* __restrict__ starts, int n, float gx, float gy,
+                                                float gh, float* __restrict__ len, int* __restrict__ word,
+                                                float* __restrict__ seg, float* __restrict__ len_groups) {
+  const int lane = (int)threadIdx.x, i = (int)blockIdx.x;
+  if (i >= n) return;
+  const float sx = starts[3 * i], sy = starts[3 * i + 1], sh = starts[3 * i + 2];
+  const RSPath p = rs_best(r, sx, sy, sh, gx, gy, gh, lane);
+  const float l4 = rs_length_group(r, sx, sy, sh, gx, gy, gh, 4, lane);
+  const float l16 = rs_length_group(r, sx, sy, sh, gx, gy, gh, 16, lane);
+  if (lane == 0) {
+    len[i] = p.L * r;
+    word[i] = p.word;
+    for (int k = 0; k < 5; ++k) seg[5 * i + k] = p.seg[k];
+    len_groups[2 * i] = l4;
+    len_groups[2 * i + 1] = l16;
+  }
+}
+hipError_t launch_test_rs(float r, const float* starts, int n, float gx, float gy, float gh, float* len, int* word,
+                          float* seg, float* len_groups, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_test_rs, dim3((unsigned)n), dim3(64), 0, st, r, starts, n, gx, gy, gh, len, word, seg, len_groups);
+  return hipGetLastError();
+}
 
 }  // namespace hastar

@@ -63,6 +63,10 @@ def load_library():
                                          C.POINTER(HastarStats)]
     L.hastar_find_path_relaxed_batch.argtypes = [C.POINTER(C.c_void_p), C.c_int, fp, fp, fp, fp, C.c_int, ip, fp,
                                                  ip, C.POINTER(HastarStats), C.POINTER(HastarRelaxedOpts)]
+    L.hastar_find_path_relaxed_batch_dir.argtypes = [C.POINTER(C.c_void_p), C.c_int, fp, fp, fp, fp, C.c_void_p,
+                                                     C.c_int, ip, fp, ip, C.POINTER(HastarStats),
+                                                     C.POINTER(HastarRelaxedOpts)]
+    L.hastar_test_reeds_shepp.argtypes = [C.c_float, fp, C.c_int, fp, fp, ip, fp, fp]
     L.hastar_get_obstacles.argtypes = [vp, fp]
     L.hastar_grid_size.argtypes = [vp]
     L.hastar_set_row_window.argtypes = [vp, C.c_int, C.c_int]
@@ -584,8 +588,10 @@ def find_path_batch(planners, vels, starts, cap=4096, relaxed=None):
                                       iptr(ok), stats)
     else:
         opts = HastarRelaxedOpts(**relaxed)
-        rc = L.hastar_find_path_relaxed_batch(hs, n, fptr(v), fptr(s), fptr(xyh), fptr(curv), cap, iptr(ln),
-                                              fptr(cost), iptr(ok), stats, C.byref(opts))
+        dirs = np.zeros((n, cap), np.int8)
+        rc = L.hastar_find_path_relaxed_batch_dir(hs, n, fptr(v), fptr(s), fptr(xyh), fptr(curv),
+                                                  dirs.ctypes.data_as(C.c_void_p), cap, iptr(ln), fptr(cost),
+                                                  iptr(ok), stats, C.byref(opts))
     if rc not in (HASTAR_EOVERFLOW, HASTAR_ENOSPC):  # per-planner outcomes are in stats[i]["status"]
         _check(rc)
     ms = float(L.hastar_last_search_ms())
@@ -599,6 +605,8 @@ def find_path_batch(planners, vels, starts, cap=4096, relaxed=None):
         else:
             path, cv = xyh[i, :k].copy(), curv[i, :k].copy()
         out.append(dict(cost=float(cost[i]), ok=bool(ok[i]), path=path, curvature=cv, stats=st))
+        if relaxed is not None and k <= cap:  # each pose's direction of travel (+1 / -1)
+            out[-1]["direction"] = dirs[i, :k].copy()
     return out, ms
 
 
@@ -609,6 +617,21 @@ def gpu_math(fn, a, b=None):
     out = np.empty_like(a)
     _check(load_library().hastar_test_math(fn, fptr(a), fptr(bb), fptr(out), len(a)))
     return out
+
+
+def gpu_reeds_shepp(r_min, starts, goal):
+    """The relaxed mode's Reeds-Shepp code on the GPU (hastar_test_reeds_shepp): per start pose
+    the shortest length (m), word, 5 segment lengths (radius units) and the grouped-lane lengths
+    (groups of 4 and 16 lanes)."""
+    s = _f32(starts, (-1, 3))
+    n = len(s)
+    ln = np.empty(n, np.float32)
+    word = np.empty(n, np.int32)
+    seg = np.empty((n, 5), np.float32)
+    grp = np.empty((n, 2), np.float32)
+    _check(load_library().hastar_test_reeds_shepp(float(r_min), fptr(s), n, fptr(_f32(goal)), fptr(ln), iptr(word),
+                                                  fptr(seg), fptr(grp)))
+    return ln, word, seg, grp
 
 
 def gpu_dubins_len(r_min, starts, goal):

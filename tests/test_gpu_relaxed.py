@@ -259,3 +259,84 @@ def test_relaxed_is_deterministic(gpu):
             assert r["stats"]["pops"] == r0["stats"]["pops"] and r["stats"]["pop_digest"] == r0["stats"]["pop_digest"]
             assert np.float32(r["cost"]).view(np.uint32) == np.float32(r0["cost"]).view(np.uint32), f"case {i}"
             assert r["path"].shape == r0["path"].shape and (r["path"].view(np.uint32) == r0["path"].view(np.uint32)).all()
+
+
+# ------------------------------------------------------ reversing model (round 6) -------
+# hastar_relaxed_opts::reverse_cost > 0: reverse arcs plus Reeds-Shepp heuristic and shots
+# (csrc/hastar_rs.h).  The reference has no reversing model (VehicleModel.cpp:97-101), so this
+# is "parity unpinned": the device's Reeds-Shepp code is checked against the CPU restatement
+# (oracle/reeds_shepp.py) and the paths for validity and for a consistent direction of travel.
+REV = dict(reverse_cost=1.5, gear_cost=1.0)
+
+
+def test_reeds_shepp_device_matches_restatement(gpu):
+    """hastar_test_reeds_shepp over 3000 random start poses and one goal: the device's shortest
+    length equals the double-precision restatement's to float precision, its word's segments
+    integrate to the goal, and the grouped-lane lengths (groups of 4 and 16, as the successor
+    heuristic runs them) equal the wave-wide minimum."""
+    from oracle import reeds_shepp as rs
+    rng = np.random.default_rng(11)
+    r = 4.3
+    goal = np.array([3.0, -2.0, 0.7], np.float32)
+    starts = np.column_stack([rng.uniform(-40, 40, 3000), rng.uniform(-40, 40, 3000),
+                              rng.uniform(-math.pi, math.pi, 3000)]).astype(np.float32)
+    starts[:8] = [[3.0, -2.0, 0.7], [3.0, -2.0, -2.4], [-5.0, -2.0, 0.7], [13.0, -2.0, 0.7],
+                  [3.0, 6.0, 0.7], [3.5, -2.1, 0.69], [3.0, -2.0, 3.1], [0.0, 0.0, 0.0]]
+    ln, word, seg, grp = gpu.gpu_reeds_shepp(r, starts, goal)
+    for i, s in enumerate(starts.astype(np.float64)):
+        ref = rs.length(tuple(s), tuple(goal.astype(np.float64)), r)
+        assert ln[i] == pytest.approx(ref, rel=2e-4, abs=2e-3), (i, s, ln[i], ref)
+        x, y, phi = rs.to_local(tuple(s), tuple(goal.astype(np.float64)), r)
+        ex, ey, eh = rs.integrate(int(word[i]), [float(v) for v in seg[i]])
+        assert max(abs(ex - x), abs(ey - y), abs(rs.mod2pi(eh - phi))) < 2e-3 * max(1.0, math.hypot(x, y)), (i, s)
+        assert abs(sum(abs(float(v)) for v in seg[i]) * r - ln[i]) < 1e-3 * max(1.0, ln[i])
+    assert np.allclose(grp[:, 0], ln, rtol=1e-6, atol=1e-5) and np.allclose(grp[:, 1], ln, rtol=1e-6, atol=1e-5)
+    assert len(set(word.tolist())) >= 12, sorted(set(word.tolist()))
+
+
+def _check_directions(r, what):
+    """Each pose's direction (+1 / -1) must agree with its motion: pose k is reached from pose
+    k + 1 (the path runs goal -> start), forward when the step points along pose k's heading."""
+    d = r["direction"]
+    p = r["path"].astype(np.float64)
+    assert set(np.unique(d).tolist()) <= {-1, 1}, f"{what}: directions {np.unique(d)}"
+    step = p[:-1, :2] - p[1:, :2]
+    along = step[:, 0] * np.cos(p[:-1, 2]) + step[:, 1] * np.sin(p[:-1, 2])
+    moving = np.hypot(step[:, 0], step[:, 1]) > 1e-3
+    bad = moving & (np.sign(along) != d[:-1])
+    assert not bad.any(), f"{what}: {bad.sum()} poses whose direction disagrees with their motion"
+
+
+def test_relaxed_reversals_valid(gpu, oracle_lib):
+    """With reversals: valid paths (free, continuous, start to goal) on synthetic and cfg3
+    cases, each pose's direction consistent with its motion, and the forward model's behaviour
+    unchanged when reverse_cost is 0 (every direction +1)."""
+    cases = [synthetic(256, 36, 40, s) for s in (1, 2, 3)] + [synthetic(1024, 72, 200, seed=q + 1) for q in (0, 3)]
+    rel, _ = _run_case(gpu, oracle_lib, cases, "reversals", relaxed=REV)
+    for i, r in enumerate(rel):
+        if r["ok"]:
+            _check_directions(r, f"reversals {i}")
+    fwd, _ = _run_case(gpu, oracle_lib, cases[:2], "forward")
+    assert all((r["direction"] == 1).all() for r in fwd if r["ok"])
+
+
+def test_relaxed_reverses_to_a_goal_behind(gpu):
+    """A goal 12 m straight behind the start, in the open: the forward model must turn around,
+    the reversing model backs up.  The reversing path must contain reverse poses and cost less
+    than the forward model's; both must be valid."""
+    cfg, proto = synthetic(256, 36, 0, 1)
+    proto = dict(proto, goal=[0.0, 0.0, 0.0], start=[12.0, 0.0, 0.0])
+    g = gpu.HybridAStar(cfg)
+    drive(g, proto)
+    p = cfg.values
+    N, res, step = p["grid_size"], p["grid_resolution"], p["step_size"]
+    thr = np.float32(math.log(p["obstacle_threshold"] / (1.0 - p["obstacle_threshold"])))
+    fwd = gpu.find_path_batch([g], [proto["vel"]], [proto["start"]], cap=16384, relaxed={})[0][0]
+    rev = gpu.find_path_batch([g], [proto["vel"]], [proto["start"]], cap=16384, relaxed=dict(REV))[0][0]
+    for r, tag in ((fwd, "forward"), (rev, "reversing")):
+        check_valid(r, g.get_obstacles(), thr, proto, N, res, 3.0 * step + 1e-3, f"goal behind, {tag}")
+    _check_directions(rev, "goal behind")
+    print(f"goal behind: forward cost {fwd['cost']:.2f} ({len(fwd['path'])} poses), reversing "
+          f"{rev['cost']:.2f} ({len(rev['path'])} poses, {(rev['direction'] < 0).sum()} reverse)")
+    assert (rev["direction"] < 0).any()
+    assert rev["cost"] < fwd["cost"]
