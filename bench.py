@@ -208,6 +208,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-relaxed", action="store_true", help="cfg5: skip the relaxed-mode comparison")
     ap.add_argument("--relaxed-batch-nodes", type=int, default=1 << 16,
                     help="relaxed batch: node capacity per search (hastar_relaxed_opts.max_nodes)")
+    ap.add_argument("--relaxed-reverse-cost", type=float, default=1.5,
+                    help="relaxed batch leg: also run it with the reversing model at this reverse cost (0: skip)")
+    ap.add_argument("--relaxed-gear-cost", type=float, default=1.0, help="... and this gear-change cost (m)")
     ap.add_argument("--relaxed-batch", type=int, default=4096,
                     help="cfg3/cfg4: queries of the batch also planned in one relaxed call (query rate)")
     ap.add_argument("--dump-timings", default=None,
@@ -699,6 +702,24 @@ def relaxed_latency_phase(gpu, planners, vels, starts, last, ids, qids, args, ex
                  "cost_ratio_vs_exact_mean": float(np.mean(br)) if br else None,
                  "cost_ratio_vs_exact_max": float(np.max(br)) if br else None,
                  "workgroups": groups, "arena_mib": arena_mib, "max_nodes": args.relaxed_batch_nodes}
+        if args.relaxed_reverse_cost > 0:
+            # BASELINE.json configs[2] names "Reeds-Shepp reversals enabled": the same batch with the
+            # relaxed mode's reversing model (the reference itself drives forward only)
+            ropts = dict(bopts, reverse_cost=args.relaxed_reverse_cost, gear_cost=args.relaxed_gear_cost)
+            rr, rms = gpu.find_path_batch(planners[:nb], vels[:nb], starts[:nb], cap=8192, relaxed=ropts)
+            rrat = [float(r["cost"]) / float(last.cost[i]) for i, r in enumerate(rr) if r["ok"] and last.ok[i]]
+            rev_poses = sum(int((r["direction"] < 0).sum()) for r in rr if r["ok"] and "direction" in r)
+            all_poses = sum(len(r["path"]) for r in rr if r["ok"])
+            batch["reversing"] = {
+                "reverse_cost": args.relaxed_reverse_cost, "gear_cost": args.relaxed_gear_cost, "kernel_ms": rms,
+                "queries_per_s": nb / (rms * 1e-3), "ok": sum(int(r["ok"]) for r in rr),
+                "status": sorted({int(r["stats"]["status"]) for r in rr}),
+                "cost_ratio_vs_exact_mean": float(np.mean(rrat)) if rrat else None,
+                "cost_ratio_vs_exact_max": float(np.max(rrat)) if rrat else None,
+                "paths_with_reverse": sum(int((r["direction"] < 0).any()) for r in rr if r["ok"] and "direction" in r),
+                "reverse_pose_fraction": rev_poses / max(all_poses, 1),
+                "note": "reverse arcs (action cost x reverse_cost), Reeds-Shepp heuristic and shots "
+                        "(csrc/hastar_rs.h); costs relative to the exact forward-only result"}
     return {"batch": batch, "queries": [qids[i] for i in ids], "gpu_ms": ms, "gpu_median_ms": float(np.median(ms)) if ms else None,
             "exact_gpu_ms_same_queries": exact_ms, "ok": ok, "exact_ok": int(sum(int(last.ok[i]) for i in ids)),
             "cost_ratio_vs_exact": ratios, "expansions": exp, "opts": opts,
