@@ -256,7 +256,10 @@ def main():
         dist = dist_mod
         if args.backend == "nccl":
             torch.cuda.set_device(local_rank)
-        dist.init_process_group(args.backend)
+        # rank 0 checks parity on the host after the timed region while the others wait at the
+        # closing barrier: a generous timeout
+        import datetime
+        dist.init_process_group(args.backend, timeout=datetime.timedelta(minutes=30))
     # HASTAR_BENCH_DEVICE: put every rank on one device (a multi-rank rehearsal on a one-GPU box,
     # with --backend gloo); by default rank r uses GPU LOCAL_RANK
     device = int(os.environ.get("HASTAR_BENCH_DEVICE", local_rank))
@@ -495,10 +498,11 @@ def main():
             if cold_all is not None:
                 progress("parity of every query")
                 out["parity_all"] = parity_all(cfgs, *cold_all, qids)
-            progress("cpu baseline")
-            cb = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps, lat_ids, sample)
-            out["cpu_baseline"] = cb
-            out["plan_latency_ms"]["cpu_same_queries_median"] = cb.pop("latency_same_queries_ms", None)
+            if world == 1:  # the CPU baseline is an N = 1 figure (rank 0 of a one-GPU run)
+                progress("cpu baseline")
+                cb = cpu_baseline(cfgs, last, args.cpu_seconds, args.warmup + args.steps, lat_ids, sample)
+                out["cpu_baseline"] = cb
+                out["plan_latency_ms"]["cpu_same_queries_median"] = cb.pop("latency_same_queries_ms", None)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
