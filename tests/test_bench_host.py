@@ -109,7 +109,8 @@ def test_parity_sample_replays_every_replan_for_the_last_step():
 
 def test_parity_all_checks_every_query():
     """bench.parity_all (--parity-all): every query's cold-step statistics, digests (compared
-    modulo 2^64, whatever the integer width they arrive in), success and cost bits."""
+    modulo 2^64, whatever the integer width they arrive in), success, cost bits and the digest of
+    its path and curvature bits."""
     import numpy as np
     import bench
     from oracle.pyoracle import OraclePlanner
@@ -119,6 +120,7 @@ def test_parity_all_checks_every_query():
             "closed_digest", "via_shot")
     st = np.zeros(2, dtype=[(k, "i8") for k in keys])
     cost, ok = np.zeros(2, np.float32), np.zeros(2, np.int32)
+    paths = []
     for i, (cfg, proto) in enumerate(cfgs):
         o = OraclePlanner(cfg)
         drive(o, proto)
@@ -128,7 +130,13 @@ def test_parity_all_checks_every_query():
         for k in keys:
             st[k][i] = np.uint64(r["stats"][k]).astype(np.int64)
         cost[i], ok[i] = r["cost"], r["ok"]
-    assert bench.parity_all(cfgs, st, cost, ok, [5, 6])["bit_exact"]
+        paths.append(bench.path_digest(r))
+    res = bench.parity_all(cfgs, st, cost, ok, paths, [5, 6])
+    assert res["bit_exact"] and res["path_poses_checked"] > 0
     st["closed_digest"][1] ^= 1
-    r = bench.parity_all(cfgs, st, cost, ok, [5, 6])
+    r = bench.parity_all(cfgs, st, cost, ok, paths, [5, 6])
     assert r["mismatched_queries"] == [6] and r["n_mismatched"] == 1
+    st["closed_digest"][1] ^= 1
+    paths[0] = bench.path_digest(dict(path=np.zeros((1, 3), np.float32), curvature=np.zeros(1, np.float32)))
+    r = bench.parity_all(cfgs, st, cost, ok, paths, [5, 6])
+    assert r["mismatched_queries"] == [5] and r["n_mismatched"] == 1
