@@ -99,9 +99,13 @@ def step_diag(planners, res):
     on_cu = Counter(cu_key)
 
     def row(i):  # start offset ms, duration ms, arena, planner index, pops, inner A* pops, XCC, SE, SH, CU,
-        x, se, sh, cu = cu_key[i]  # searches on the instruction-cache partner CU in this step
+        x, se, sh, cu = cu_key[i]  # searches on the instruction-cache partner CU in this step, shader MHz
+        cyc = planners[i].cycles()  # [38], [39]: s_memtime at the search's start and end (0 if parked)
+        mhz = (cyc[39] - cyc[38]) / ((t[i, 1] - t[i, 0]) * 1e-8) / 1e6 if (cyc[39] > cyc[38] and int(st["parks"][i]) == 0
+                                                                       and t[i, 1] > t[i, 0]) else None
         return [round(float((t[i, 0] - t0) * 1e-5), 1), round(float(dur[i]), 1), int(t[i, 2]), int(i),
-                int(st["pops"][i]), int(st["astar_pops"][i]), x, se, sh, cu, on_cu[(x, se, sh, cu ^ 1)]]
+                int(st["pops"][i]), int(st["astar_pops"][i]), x, se, sh, cu, on_cu[(x, se, sh, cu ^ 1)],
+                round(mhz, 1) if mhz else None]
     return {"kernel_ms": float(res.kernel_ms), "span_ms": float((t[:, 1].max() - t0) * 1e-5),
             "split_ms": planners[0].split_ms(), "head": [row(i) for i in first], "longest": row(li)}
 
