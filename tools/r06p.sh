@@ -1,6 +1,8 @@
 # round-6 GPU iteration p: the split-launch outlier with per-search shader clocks (experimental
 # build path_planning_pkg_amd/lib_clk: s_memtime at each search's start and end in cycles[38..39];
-# the stamps cost the latency kernel 3-4 %, so they stay out of the product build)
+# the stamps cost the latency kernel 3-4 %, so they stay out of the product build).  lib_clk is
+# hastar_kernels.hip with tools/clk_stamps.patch applied, compiled as the Makefile does and linked
+# with the product build's other objects.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r06p; mkdir -p $O
