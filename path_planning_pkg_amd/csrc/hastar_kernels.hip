@@ -25,6 +25,10 @@ namespace hastar {
 constexpr int MAXS = 16;   // max steering actions (checked at create)
 static_assert(64 / 4 >= MAXS, "4 lanes per candidate action must cover MAXS actions");
 
+// block-placement hints: the inner A*'s rare paths (end of search, duplicates, shape-dependent
+// walks, overflows) out of the straight-line common path
+#define HASTAR_LIKELY(x) __builtin_expect(!!(x), 1)
+#define HASTAR_UNLIKELY(x) __builtin_expect(!!(x), 0)
 // Diagnostic build only (-DHASTAR_STAMPS): cycles per phase of the search loop,
 // 0 pop+closed insert, 1 successors+APF+Dubins, 2 open/closed bookkeeping, 3 holonomic A*,
 // 4 Dubins shot, 5 reconstruct+stats, 6 whole loop, 7 A* in HBM mode, 8-12 LDS A* pop /
@@ -475,6 +479,10 @@ __device__ __forceinline__ void ring_shift(AStarLdsT<CF>& L, int head, int from,
   static_assert(RING_CH >= 4, "ring_shift's specialised chunk counts");
   // the chunk count is wave-uniform: one straight-line copy per count (the short shifts of a
   // small open set do not test the chunks they do not have)
+  if (HASTAR_LIKELY(cnt <= 64)) {  // the common short shift near an end of the ring
+    ring_shift_n<CF, 1, true>(L, head, from, cnt, dir, lane);
+    return;
+  }
   switch ((cnt + 63) >> 6) {
     case 1: ring_shift_n<CF, 1, true>(L, head, from, cnt, dir, lane); break;
     case 2: ring_shift_n<CF, 2, true>(L, head, from, cnt, dir, lane); break;
@@ -643,7 +651,7 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     }
     c.apops++;
     if (G) c.apops_g++;
-    if (tx == P.goal_cx && ty == P.goal_cy) {
+    if (HASTAR_UNLIKELY(tx == P.goal_cx && ty == P.goal_cy)) {
       const float fgoal = g0 + euclid_h(P, tx, ty);  // the record's f (Node2D: f = g + h)
       if (c.cost_only) memoise(c, fgoal, ci);
       *result = fgoal;
@@ -654,7 +662,7 @@ __device__ __forceinline__ bool astar_loop(SearchCtx& c, Tree& tr, int adx, int 
     for (int k = 0; k < nact; ++k) {
       if (!((vmask >> k) & 1ull)) continue;
       const float kcost = rl_f(acost, k);
-      if ((vismask >> k) & 1ull) {
+      if (HASTAR_UNLIKELY((vismask >> k) & 1ull)) {
         const float tot = rl_f(nf, k) + g0 + kcost;
         STAMP_T t_m = STAMP_NOW();
         memoise(c, tot, ci);
@@ -709,7 +717,7 @@ __device__ __forceinline__ int alloc_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr) {
     c.ps2.free = __builtin_amdgcn_readfirstlane(__float_as_int(tr.s->kf[i].f));
     return i;
   }
-  if (c.ps2.next >= CF::CAP) return NIL;
+  if (HASTAR_UNLIKELY(c.ps2.next >= CF::CAP)) return NIL;
   return c.ps2.next++;
 }
 
@@ -794,12 +802,12 @@ __device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AS
   int parent = 0;
   bool left = true;
   bool logged = false;
-  if (sc.cnt >= 2 || (sc.cnt == 1 && sc.f > fn)) {  // a node of this cell lies right of fn
+  if (HASTAR_UNLIKELY(sc.cnt >= 2 || (sc.cnt == 1 && sc.f > fn))) {  // a node of this cell lies right of fn
     if (pend_on(pd)) pend_replay(c, tr, L, pd);  // the walk needs the tree
     parent = tr.insert_pos(key, fn, &left);
     if (parent == -2) return true;
   } else {
-    if ((rb.at != NIL && rb.at_f == fn) || (rb.pred != NIL && rb.pred == sc.idx)) return true;  // dropped
+    if (HASTAR_UNLIKELY((rb.at != NIL && rb.at_f == fn) || (rb.pred != NIL && rb.pred == sc.idx))) return true;  // dropped
     if (pend_on(pd)) {
       logged = true;  // its place is its rank neighbours: linked when the log is replayed
     } else if (rg.n == 0) {
@@ -817,7 +825,7 @@ __device__ __forceinline__ bool insert_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr, AS
     }
   }
   const int n = alloc_lds(c, tr);
-  if (n == NIL) return false;
+  if (HASTAR_UNLIKELY(n == NIL)) return false;
   tr.payload(n, key, fn, gn, prev);
   STAMP_T t_l = STAMP_NOW();
   if (logged) pend_add(pd, c.lane, n, true, rg.n == 0 ? NIL : rb.pred, rg.n == 0 ? NIL : rb.at);
@@ -890,8 +898,8 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
   // pop's entries (1 + 2 per neighbour)
   const int log_lim = c.A->open2_cap * (int)(sizeof(Node2) / 8) - (1 + 2 * 8);
   while (rg.n > 0) {
-    if (c.ps2.next + 8 > lim) return false;
-    if (pend_on(pd) && __builtin_amdgcn_readfirstlane(pd.logn) > log_lim) pend_replay(c, tr, L, pd);
+    if (HASTAR_UNLIKELY(c.ps2.next + 8 > lim)) return false;
+    if (pend_on(pd) && HASTAR_UNLIKELY(__builtin_amdgcn_readfirstlane(pd.logn) > log_lim)) pend_replay(c, tr, L, pd);
     STAMP_T t_pop = STAMP_NOW();
     const int b = pend_on(pd) ? ((int)L.ring[rg.head] & (CF::CAP - 1)) : tr.begin();
     const Quad top = tr.quad(b);
@@ -1015,7 +1023,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
       SameCell sc{0, NIL, 0.0f};
       if (hint != 0xffffffffu) {
         dup = (hint >> 16) & 1u;
-        if (dup) {
+        if (HASTAR_UNLIKELY(dup)) {
           sc = same_cell(L, c.ps2.next, key, lane);
         } else {
           const int y = (int)(hint & 0xffffu);  // = lane k's hy
@@ -1035,7 +1043,7 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
         hit = sc.idx;
       } else {
         rank2(L, rg, fprobe, fn, lane, ra, rb);
-        if (sc.cnt >= 2 || (sc.cnt == 1 && sc.f < fprobe)) {
+        if (HASTAR_UNLIKELY(sc.cnt >= 2 || (sc.cnt == 1 && sc.f < fprobe))) {
           if (pend_on(pd)) pend_replay(c, tr, L, pd);
           hit = tr.find(key, fprobe);  // shape-dependent: the exact tree walk
         } else if (ra.at != NIL && (ra.at_f == fprobe || ra.at == sc.idx)) {
@@ -1044,10 +1052,10 @@ __device__ __forceinline__ bool astar_loop_lds(SearchCtx& c, RBT<LdsAcc<CF>>& tr
         }
       }
       STAMP_ADD(9, t_f);
-      if (hit == 0) {
+      if (HASTAR_LIKELY(hit == 0)) {
         STAMP_T t_i = STAMP_NOW();
         int nn;
-        if (!insert_lds(c, tr, L, rg, key, fn, gn, ci, sc, rb, &nn, pd)) { c.status = -75; *result = FLT_MAX; return true; }
+        if (HASTAR_UNLIKELY(!insert_lds(c, tr, L, rg, key, fn, gn, ci, sc, rb, &nn, pd))) { c.status = -75; *result = FLT_MAX; return true; }
         if (lane == k) {  // Node2D::set_accumulated_cost; the cell's nm_f is written even
           st_on = true;   // when the insert is dropped (AStar.cpp:172-183)
           st_cell = (uint32_t)ki * (uint32_t)c.N + (uint32_t)kj;
@@ -1157,7 +1165,7 @@ __device__ __forceinline__ float holonomic(SearchCtx& c, AStarLdsT<CF>& L, int s
   }
   float result = FLT_MAX;
   STAMP_ADD(35, t_hs);
-  if (astar_loop_lds(c, tl, L, rg, adx, ady, acost, &result, pd)) return result;
+  if (HASTAR_LIKELY(astar_loop_lds(c, tl, L, rg, adx, ady, acost, &result, pd))) return result;
   if (pend_on(pd)) pend_replay(c, tl, L, pd);  // the migration copies the tree (into open2: the log is read first)
   // migrate the LDS tree to HBM nodes (identical indices) and continue there
   c.amigr++;
@@ -1206,9 +1214,9 @@ __device__ __forceinline__ bool insert3(SearchCtx& c, OT& o3, const Succ& s, flo
   const int pos = o3.insert_pos(key, f, &left);
   STAMP_ADD(19, tw);
   if (where) where[0] = NIL;
-  if (pos == -2) return true;
+  if (HASTAR_UNLIKELY(pos == -2)) return true;
   const int n = tpool_alloc(o3, c.ps3, cap);
-  if (n == NIL) return false;
+  if (HASTAR_UNLIKELY(n == NIL)) return false;
   if (where) {
     where[0] = n;
     where[1] = pos;
@@ -1795,16 +1803,16 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
   const int gsh = span <= 4 ? 4 : 2, gs = 1 << gsh;
 #endif
   while (!o3.empty()) {
-    if (hard_pops > 0 && c.pops >= hard_pops) { c.status = -75; break; }
+    if (HASTAR_UNLIKELY(hard_pops > 0 && c.pops >= hard_pops)) { c.status = -75; break; }
     // one more pop needs a closed record and at most `span` open nodes (the pop frees one)
-    if (c.n_closed3 + 1 >= closed_lim || c.ps3.next + span + 1 > open_lim_t) {
+    if (HASTAR_UNLIKELY(c.n_closed3 + 1 >= closed_lim || c.ps3.next + span + 1 > open_lim_t)) {
       if (kLdsOuter) return LOOP_MIGRATE;  // the HBM loop continues (and parks if it must)
       parked = true;
       break;
     }
     if constexpr (!kPrep) {  // batch kernel: a free latency CU may take this search over
 #ifndef BISECT_NOPOLL
-      if ((c.pops & 63u) == 0u && ho_poll(c)) return LOOP_HANDOFF;
+      if (HASTAR_UNLIKELY((c.pops & 63u) == 0u) && HASTAR_UNLIKELY(ho_poll(c))) return LOOP_HANDOFF;
 #endif
     }
     STAMP_T tp = STAMP_NOW();
@@ -1839,7 +1847,7 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     tpool_free(o3, c.ps3, b);
     bool fresh;
     const int ci = closed3_insert(c, top, &fresh, ph, p0);
-    if (ci == NIL) { c.status = -75; break; }
+    if (HASTAR_UNLIKELY(ci == NIL)) { c.status = -75; break; }
     // a duplicate key expands the OLD record; a new record is the popped node itself
     Closed3 cur;
     if (fresh) {
@@ -1871,14 +1879,14 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
     }
     STAMP_ADD(0, tp);
     // goal test: Node3D::operator== compares the cell only (Node3D.h:42)
-    if (cx == P.goal_cx && cy == P.goal_cy) {
+    if (HASTAR_UNLIKELY(cx == P.goal_cx && cy == P.goal_cy)) {
       terminal = ci;
       cost = cur.g;
       ok = 1;
       break;
     }
     if (shot_allowed) {
-      if (++counter == interval) {
+      if (HASTAR_UNLIKELY(++counter == interval)) {
         STAMP_T tsh = STAMP_NOW();
         c.shots++;
         int word = 0;
@@ -1893,9 +1901,9 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
         const int n = first_arc_long
                           ? dubins_sample<2>(P, C, word, prm, gp(A.dub_xyh), gp(A.dub_curv), A.dub_cap, lane)
                           : dubins_sample<1>(P, C, word, prm, gp(A.dub_xyh), gp(A.dub_curv), A.dub_cap, lane);
-        if (n == -1) { c.status = -75; break; }
+        if (HASTAR_UNLIKELY(n == -1)) { c.status = -75; break; }
         wave_lds_sync();
-        if (!first_arc_long && n > 0) {
+        if (HASTAR_UNLIKELY(!first_arc_long && n > 0)) {
           terminal = cur.prev;
           cost = cur.g + L;
           ok = 1;
@@ -2063,8 +2071,8 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
       }
       STAMP_ADD(13, tf3);
       const bool repl = hit != 0 && s.g < o3.G(hit);
-      if (hit == 0 || repl) {
-        if (repl) {
+      if (HASTAR_LIKELY(hit == 0 || repl)) {
+        if (HASTAR_UNLIKELY(repl)) {
           STAMP_T tu3 = STAMP_NOW();
           o3.unlink(hit);
           tpool_free(o3, c.ps3, hit);
@@ -2085,15 +2093,15 @@ __device__ __forceinline__ int search_loop(SearchCtx& c, OT& o3, ApfStage& apfs,
         STAMP_ADD(3, ta);
         const float f = s.g + stl_max(h1, s.dub);
         STAMP_T ti3 = STAMP_NOW();
-        if (!insert3(c, o3, s, f, ci, open_cap)) { fail = true; break; }
+        if (HASTAR_UNLIKELY(!insert3(c, o3, s, f, ci, open_cap))) { fail = true; break; }
         STAMP_ADD(14, ti3);
       }
-      if (c.status != 0) break;
+      if (HASTAR_UNLIKELY(c.status != 0)) break;
     }
     wave_lds_sync();
     STAMP_ADD(2, tb);
-    if (fail) c.status = -75;
-    if (c.status != 0) break;
+    if (HASTAR_UNLIKELY(fail)) c.status = -75;
+    if (HASTAR_UNLIKELY(c.status != 0)) break;
   }
   return parked ? LOOP_PARKED : LOOP_DONE;
 }
