@@ -51,6 +51,11 @@ namespace orc {
 // Optional pop limit for census tools (0 = none, the reference's behaviour): a search that
 // reaches it stops with stats.status = HASTAR_EOVERFLOW and is reported as failed.
 long long g_max_pops = 0;
+#ifdef ORC_BRANCH_STATS
+// analysis build (tools/branch_stats.py): how often the inner A*'s per-neighbour branches go
+// each way (valid neighbours, closed, find hits, replacements, inserts, closed re-pops)
+long long g_br[8];
+#endif
 #ifdef ORC_OUTER_STATS
 // analysis build (tools/outer_shape_stats.py): how often the OUTER open set's tree shape can
 // decide a find / insert (a node of the same key on the "wrong" side of the probe f)
@@ -621,7 +626,14 @@ template <class T> struct Planner {
       g_search_pops++;
 #endif
       auto it = op2.begin();
+#ifdef ORC_BRANCH_STATS
+      const auto ins_r = cl2.insert(*it);
+      const N2<T>* cur = &*ins_r.first;
+      g_br[6]++;
+      g_br[7] += !ins_r.second;  // the popped cell was closed already
+#else
       const N2<T>* cur = &*cl2.insert(*it).first;
+#endif
       op2.erase(it);
 #ifndef ORC_LEAN
       st.astar_pops++;
@@ -642,12 +654,27 @@ template <class T> struct Planner {
           return tot;
         }
         N2<T> probe{i, j, 0, nm_f[c], nullptr};
+#ifdef ORC_BRANCH_STATS
+        g_br[0]++;
+        if (cl2.find(probe) != cl2.end()) { g_br[1]++; continue; }
+#else
         if (cl2.find(probe) != cl2.end()) continue;
+#endif
 #ifdef ORC_SHAPE_STATS
         shape_probe(op2, i, j, nm_f[c], g0 + act_cost[k] + nm_h[c]);
 #endif
         auto hit = op2.find(probe);
         const T gn = g0 + act_cost[k];
+#ifdef ORC_BRANCH_STATS
+        g_br[2] += hit != op2.end();
+        g_br[3] += hit != op2.end() && gn < hit->g;
+        g_br[4] += hit == op2.end();
+        {  // an open node of this cell exists (the kernel's cell hint)
+          bool any = false;
+          for (const auto& n : op2) any |= (n.x == i && n.y == j);
+          g_br[5] += any;
+        }
+#endif
         if (hit == op2.end()) {
           nm_f[c] = gn + nm_h[c];  // Node2D::set_accumulated_cost
           op2.insert(N2<T>{i, j, gn, nm_f[c], cur});
@@ -1304,6 +1331,11 @@ extern "C" void orc_run_batch_threads(void* const* hs, int n, const float* vel, 
   out[3] = (double)n * replans;
 }
 
+#ifdef ORC_BRANCH_STATS
+extern "C" void orc_branch_stats(long long* out) {
+  for (int q = 0; q < 8; ++q) out[q] = orc::g_br[q], orc::g_br[q] = 0;
+}
+#endif
 #ifdef ORC_OUTER_STATS
 extern "C" void orc_outer_stats(long long* out) {
   for (int q = 0; q < 16; ++q) out[q] = orc::g_oshape[q], orc::g_oshape[q] = 0;
