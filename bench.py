@@ -666,12 +666,57 @@ def map_build_phase(args, gpu, dist, torch, rank, world, device):
         flag = torch.tensor([0 if same else 1], device=f"cuda:{device}")
         dist.all_reduce(flag)
         same = int(flag[0]) == 0
+    field = field_phase(shd[0], dist, torch, rank, world, device)
     for p in loc + shd:
         p.close()
     N = args.grid
     return {"maps": M, "grid": N, "ranks": world, "local_ms_per_map": t_loc, "sharded_ms_per_map": t_shd,
             "allgather_bytes_per_map": N * N * 4, "parity": bool(same),
-            "protocol": "update_goal + 5 x {decay, 200 boxes} per map (tests/scenarios.py::drive)"}
+            "protocol": "update_goal + 5 x {decay, 200 boxes} per map (tests/scenarios.py::drive)",
+            "heuristic_field": field}
+
+
+def field_phase(p, dist, torch, rank, world, device, standins=4):
+    """cfg4's heuristic precompute (BASELINE.json configs[3]; include/hastar.h:
+    hastar_heuristic_field): the backward grid-distance field of the first map, (a) whole on every
+    rank, (b) row-sharded over the job's ranks with edge-row all-gathers
+    (shard.py:heuristic_field_sharded), and on one rank (c) with `standins` stand-in ranks on
+    the one GPU.  Times are max over ranks; `parity`: (b) and (c) equal (a) bit for bit."""
+    from path_planning_pkg_amd.shard import heuristic_field_sharded, heuristic_field_standins
+    N = p.N
+    dev = f"cuda:{device}"
+    out = torch.empty(N * N, dtype=torch.float32, device=dev)
+    torch.cuda.synchronize(device)
+    p.heuristic_field(out.data_ptr())  # warm-up
+
+    def timed(fn):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize(device)
+        el, _ = reduce_over_ranks(dist, time.perf_counter() - t0, 0, dev)
+        return el * 1e3, r
+
+    t_one, passes = timed(lambda: p.heuristic_field(out.data_ptr()))
+    t_shd, (full, rounds, spasses) = timed(lambda: heuristic_field_sharded(p, rank, world, dev))
+    same = bool(torch.equal(full.view(torch.int32), out.view(torch.int32)))
+    res = {"grid": N, "one_gpu_ms": t_one, "passes": passes, "finite_cells": int(torch.isfinite(out).sum()),
+           "ranks": world, "sharded_ms": t_shd, "exchange_rounds": rounds, "sharded_passes": spasses}
+    if world == 1:
+        t_st, (sfull, srounds, _) = timed(lambda: heuristic_field_standins(p, standins, torch.device(dev)))
+        same = same and bool(torch.equal(sfull.view(torch.int32), out.view(torch.int32)))
+        res.update(standin_ranks=standins, standin_ms=t_st, standin_rounds=srounds)
+    if dist:
+        flag = torch.tensor([0 if same else 1], device=dev)
+        dist.all_reduce(flag)
+        same = int(flag[0]) == 0
+    res["parity"] = same
+    res["note"] = ("backward 8-connected grid distance to the goal over the free cells (csrc/hastar_field.hip); "
+                   "sharded: row blocks + edge-row all-gathers until no block edge changes; bit-equal by construction "
+                   "(the field's equations have one solution) and by this check")
+    return res
 
 
 def relaxed_latency_phase(gpu, planners, vels, starts, last, ids, qids, args, exact_ms, exact_qps):

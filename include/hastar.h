@@ -228,6 +228,30 @@ int hastar_set_row_window(hastar_handle h, int row0, int row1);
 int hastar_export_rows(hastar_handle h, int row0, int row1, float* dst_device);
 int hastar_import_rows(hastar_handle h, int row0, int row1, const float* src_device);
 
+/* ---- the backward grid-distance field to the goal, row-sharded (BASELINE.json north_star:
+ * "Grid2D heuristic fill ... backward-Dijkstra heuristic precompute shards across GPUs"; no
+ * reference counterpart: the reference computes the same distances lazily, cell by cell, in
+ * AStar::find_path(int, int), AStar.cpp:100-186, over Grid2D.cpp:22-40's moves) ----
+ * field(v) = min over neighbours u that can be expanded (the goal cell, or log-odds < the
+ * occupancy threshold) of field(u) + move cost (act cost axis / diagonal, 4 or 8 moves), in
+ * float; field(goal) = 0; +inf where nothing reaches.  The system has one solution, so the
+ * result does not depend on how the rows are split (csrc/hastar_field.hip).
+ * hastar_heuristic_field writes the whole N x N field (row i = x cell) to a DEVICE buffer.
+ * hastar_field_rows relaxes rows [r0, r1) of a DEVICE buffer of (r1 - r0 + 2) x N floats
+ * (halo row r0 - 1, the block, halo row r1) until it is stable for its halo rows: init = 1
+ * fills it (+inf, the goal 0) first; otherwise halo_changed bit 0 / bit 1 say that the upper /
+ * lower halo row was overwritten since the last call.  *changed: bit 0 any cell, bit 1 row
+ * r0, bit 2 row r1 - 1 changed; *passes: relaxation passes queued, in batches of 8 (either
+ * may be NULL).  Ranks exchange their first / last rows into their neighbours' halos and call
+ * again until no rank's edge rows change (path_planning_pkg_amd/shard.py:heuristic_field_sharded).
+ * hastar_relaxed_set_field installs a whole field (DEVICE, N x N) as the planner's relaxed-mode
+ * heuristic: relaxed calls with reuse_heuristic = 1 and h_coarse = 1 use it until
+ * hastar_reset or hastar_update_goal. */
+int hastar_heuristic_field(hastar_handle h, float* dst_device, int* passes);
+int hastar_field_rows(hastar_handle h, float* field_device, int r0, int r1, int init, int halo_changed, int* changed,
+                      int* passes);
+int hastar_relaxed_set_field(hastar_handle h, const float* src_device);
+
 /* ---- VelocityGenerator<float> (post-search path products) ----
  * Replaces VelocityGenerator<T>::VelocityGenerator (VelocityGenerator.cpp:7-15) and
  * generate_velocity_profile (VelocityGenerator.cpp:19-84), called by local_planner.cpp:323,

@@ -36,6 +36,7 @@
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <queue>
 #include <set>
 #include <unordered_set>
 #include <vector>
@@ -962,6 +963,44 @@ void orc_decay(void* h) { static_cast<OP*>(h)->decay(); }
 void orc_get_obstacles(void* h, float* out) {
   auto* P = static_cast<OP*>(h);
   std::memcpy(out, P->occ.data(), P->occ.size() * sizeof(float));
+}
+// The backward grid-distance field of csrc/hastar_field.hip (include/hastar.h:
+// hastar_heuristic_field), restated as a float Dijkstra from the goal cell (n45, n2): field(v) =
+// min over neighbours u that can be expanded (the goal, or log-odds < thr) of field(u) + the
+// move's cost (act_cost of Grid2D.cpp:22-40's axis / diagonal moves), +inf where nothing reaches.
+// A settled value never falls again (costs > 0, float addition monotone), so this is the least
+// solution of those equations, which is their only one.
+void orc_heuristic_field(void* h, float* out) {
+  auto* P = static_cast<OP*>(h);
+  const int N = P->N;
+  const size_t NN = (size_t)N * N;
+  const float inf = std::numeric_limits<float>::infinity();
+  std::vector<float> d(NN, inf);
+  std::vector<uint8_t> done(NN, 0);
+  using E = std::pair<float, size_t>;
+  std::priority_queue<E, std::vector<E>, std::greater<E>> q;
+  const size_t g = (size_t)P->n45 * N + P->n2;
+  d[g] = 0.0f;
+  q.push({0.0f, g});
+  while (!q.empty()) {
+    const auto [du, u] = q.top();
+    q.pop();
+    if (done[u] || du != d[u]) continue;
+    done[u] = 1;
+    if (!(u == g || P->occ[u] < P->thr)) continue;  // reached, but cannot be expanded
+    const int ui = (int)(u / N), uj = (int)(u % N);
+    for (size_t k = 0; k < P->act_dx.size(); ++k) {
+      const int vi = ui + P->act_dx[k], vj = uj + P->act_dy[k];
+      if (vi < 0 || vi >= N || vj < 0 || vj >= N) continue;
+      const size_t v = (size_t)vi * N + vj;
+      const float c = du + P->act_cost[k];
+      if (c < d[v]) {
+        d[v] = c;
+        q.push({c, v});
+      }
+    }
+  }
+  std::memcpy(out, d.data(), NN * sizeof(float));
 }
 // test hook: overwrite the log-odds map (arbitrary values exercise the relocation's winners)
 void orc_set_obstacles(void* h, const float* in) {

@@ -43,6 +43,7 @@ def lib(lean=False):
         L.orc_update_lines.argtypes = [vp, fp, fp, C.c_int, C.c_float]
         L.orc_get_obstacles.argtypes = [vp, fp]
         L.orc_set_obstacles.argtypes = [vp, fp]
+        L.orc_heuristic_field.argtypes = [vp, fp]
         L.orc_get_memo.argtypes = [vp, fp, C.POINTER(C.c_ubyte)]
         L.orc_apf_count.argtypes = [vp]
         L.orc_get_apf.argtypes = [vp, fp]
@@ -136,6 +137,13 @@ class OraclePlanner:
     def get_obstacles(self):
         out = np.empty((self.N, self.N), np.float32)
         self._L.orc_get_obstacles(self.h, fptr(out))
+        return out
+
+    def heuristic_field(self):
+        """The backward grid-distance field of the current map (orc_heuristic_field: a float
+        Dijkstra from the goal cell), the checker of include/hastar.h's hastar_heuristic_field."""
+        out = np.empty((self.N, self.N), np.float32)
+        self._L.orc_heuristic_field(self.h, fptr(out))
         return out
 
     def set_obstacles(self, occ):

@@ -1613,6 +1613,113 @@ int hastar_import_rows(hastar_handle h, int row0, int row1, const float* src) {
   return HASTAR_OK;
 }
 
+// ---- the backward grid-distance field (csrc/hastar_field.hip; include/hastar.h) ----------
+// Relaxes rows [r0, r1) of the field buffer (r1 - r0 + 2 rows of N floats: halo row r0 - 1,
+// the block, halo row r1) to convergence for its current halo rows.  Caller holds DC.mu.
+static int field_rows_locked(hastar_handle h, float* field, int r0, int r1, int init, int halo_changed, int* changed,
+                             int* passes) {
+  const PlannerDev& D = h->desc;
+  DeviceCtx& DC = *h->dc;
+  hipStream_t st = DC.stream;
+  int ntx = 0, nty = 0;
+  const int nt = field_tiles(D.N, r0, r1, &ntx, &nty);
+  int* buf = nullptr;  // act[nt], nxt[nt], flags, pending
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&buf), (2 * (size_t)nt + 2) * sizeof(int)));
+  struct Release {
+    int* p;
+    ~Release() { hipFree(p); }
+  } release{buf};
+  int* act = buf;
+  int* nxt = buf + nt;
+  int* flags = buf + 2 * nt;
+  int* pending = flags + 1;
+  HIPCHK(hipMemsetAsync(buf, 0, (2 * (size_t)nt + 2) * sizeof(int), st));
+  if (init) {
+    HIPCHK(launch_field_init(field, D.N, r0, r1, D.goal_cx, D.goal_cy, st));
+    HIPCHK(launch_field_activate(act, ntx, nty, 0, pending, st));
+  } else {
+    // a halo row that changed can lower the block's first / last tile row
+    if (halo_changed & 1) HIPCHK(launch_field_activate(act, ntx, nty, 1, pending, st));
+    if (halo_changed & 2) HIPCHK(launch_field_activate(act, ntx, nty, 2, pending, st));
+  }
+  int pend = 0, np = 0;
+  HIPCHK(hipMemcpyAsync(&pend, pending, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  // every pass lowers at least one value or activates nothing, and values only fall through
+  // finitely many floats, so the loop ends; the bound only guards against a broken device.
+  // Passes are queued FIELD_BATCH at a time between host checks: a pass after the last
+  // productive one finds no active tile and ends at once, so only the check's round trip is
+  // saved, not work added.
+  constexpr int FIELD_BATCH = 8;
+  const long long max_passes = 64LL * ((long long)D.N * D.N + 64);
+  while (pend > 0) {
+    if ((np += FIELD_BATCH) > max_passes) return fail(HASTAR_EDEVICE, "field relaxation did not converge");
+    for (int b = 0; b < FIELD_BATCH; ++b) {
+      HIPCHK(hipMemsetAsync(pending, 0, sizeof(int), st));
+      HIPCHK(launch_field_pass(D, field, r0, r1, act, nxt, flags, pending, st));
+      HIPCHK(hipMemsetAsync(act, 0, (size_t)nt * sizeof(int), st));
+      std::swap(act, nxt);
+    }
+    // the last pass's activations: none means the queued passes reached the fixed point
+    HIPCHK(hipMemcpyAsync(&pend, pending, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  int fl = 0;
+  HIPCHK(hipMemcpyAsync(&fl, flags, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (changed) *changed = fl;
+  if (passes) *passes = np;
+  return HASTAR_OK;
+}
+
+int hastar_field_rows(hastar_handle h, float* field, int r0, int r1, int init, int halo_changed, int* changed,
+                      int* passes) {
+  if (!h || !field) return fail(HASTAR_EINVAL, "null argument");
+  if (!h->goal_set) return fail(HASTAR_EINVAL, "update_goal must be called before the field");
+  if (r0 < 0 || r1 <= r0 || r1 > h->desc.N) return fail(HASTAR_EINVAL, "rows must satisfy 0 <= r0 < r1 <= N");
+  HIPCHK(hipSetDevice(h->device));
+  std::lock_guard<std::mutex> lk(h->dc->mu);
+  return field_rows_locked(h, field, r0, r1, init, halo_changed, changed, passes);
+}
+
+int hastar_heuristic_field(hastar_handle h, float* dst, int* passes) {
+  if (!h || !dst) return fail(HASTAR_EINVAL, "null argument");
+  if (!h->goal_set) return fail(HASTAR_EINVAL, "update_goal must be called before the field");
+  HIPCHK(hipSetDevice(h->device));
+  std::lock_guard<std::mutex> lk(h->dc->mu);
+  const size_t N = (size_t)h->desc.N;
+  float* buf = nullptr;  // halo row, N rows, halo row
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&buf), (N + 2) * N * sizeof(float)));
+  struct Release {
+    float* p;
+    ~Release() { hipFree(p); }
+  } release{buf};
+  if (int rc = field_rows_locked(h, buf, 0, (int)N, 1, 0, nullptr, passes)) return rc;
+  HIPCHK(hipMemcpyAsync(dst, buf + N, N * N * sizeof(float), hipMemcpyDeviceToDevice, h->dc->stream));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
+  return HASTAR_OK;
+}
+
+int hastar_relaxed_set_field(hastar_handle h, const float* src) {
+  if (!h || !src) return fail(HASTAR_EINVAL, "null argument");
+  if (!h->goal_set) return fail(HASTAR_EINVAL, "update_goal must be called before the field");
+  HIPCHK(hipSetDevice(h->device));
+  std::lock_guard<std::mutex> lk(h->dc->mu);
+  const size_t NN = (size_t)h->desc.N * h->desc.N;
+  if (!h->rfield && hipMalloc(reinterpret_cast<void**>(&h->rfield), NN * sizeof(float)) != hipSuccess) {
+    h->rfield = nullptr;
+    return fail(HASTAR_ENOMEM, "heuristic field allocation failed");
+  }
+  HIPCHK(hipMemcpyAsync(h->rfield, src, NN * sizeof(float), hipMemcpyDeviceToDevice, h->dc->stream));
+  HIPCHK(hipStreamSynchronize(h->dc->stream));
+  // a full field: every reachable cell settled, no ellipse bound (unreachable cells: h = 0)
+  h->rhlim = 0.0f;
+  h->rstart = 0;
+  h->rcoarse = 1;
+  h->rvalid = true;
+  return HASTAR_OK;
+}
+
 int hastar_get_obstacles(hastar_handle h, float* out) {
   if (!h || !out) return fail(HASTAR_EINVAL, "null argument");
   HIPCHK(hipSetDevice(h->device));

@@ -18,6 +18,12 @@ int search_slots_per_cu();
 hipError_t launch_relaxed(const PlannerDev* d_descs, int n, const RelaxArena* d_arenas, int n_arenas, int* d_next,
                           const RelaxParams& rp, RelaxField* d_fields, hipStream_t st);
 int relaxed_waves();
+// the backward grid-distance field over a block of rows (hastar_field.hip)
+hipError_t launch_field_init(float* f, int N, int r0, int r1, int gi, int gj, hipStream_t st);
+int field_tiles(int N, int r0, int r1, int* ntx, int* nty);
+hipError_t launch_field_activate(int* act, int ntx, int nty, int mode, int* pending, hipStream_t st);
+hipError_t launch_field_pass(const PlannerDev& P, float* f, int r0, int r1, const int* act, int* nxt, int* flags,
+                             int* pending, hipStream_t st);
 hipError_t launch_test_rs(float r, const float* starts, int n, float gx, float gy, float gh, float* len, int* word,
                           float* seg, float* len_groups, hipStream_t st);
 hipError_t launch_grid3d_neighbors(const PlannerDev* d_desc, const float node[5], int nci, int nbin, float* out,

@@ -72,6 +72,9 @@ def load_library():
     L.hastar_set_row_window.argtypes = [vp, C.c_int, C.c_int]
     L.hastar_export_rows.argtypes = [vp, C.c_int, C.c_int, C.c_void_p]
     L.hastar_import_rows.argtypes = [vp, C.c_int, C.c_int, C.c_void_p]
+    L.hastar_heuristic_field.argtypes = [vp, C.c_void_p, ip]
+    L.hastar_field_rows.argtypes = [vp, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, ip, ip]
+    L.hastar_relaxed_set_field.argtypes = [vp, C.c_void_p]
     L.hastar_last_error.restype = C.c_char_p
     L.hastar_last_search_ms.restype = C.c_float
     L.hastar_test_math.argtypes = [C.c_int, fp, fp, fp, C.c_int]
@@ -288,6 +291,27 @@ class HybridAStar:
     def import_rows(self, row0, row1, src_ptr):
         """Overwrite log-odds rows [row0, row1) from the device buffer at `src_ptr`; synchronous."""
         _check(load_library().hastar_import_rows(self.h, int(row0), int(row1), C.c_void_p(int(src_ptr))))
+
+    # ---- the backward grid-distance field (include/hastar.h: hastar_heuristic_field)
+    def heuristic_field(self, dst_ptr):
+        """Write the N x N field to the device buffer at `dst_ptr` (row i = x cell); returns the
+        relaxation passes it took.  Synchronous."""
+        p = C.c_int(0)
+        _check(load_library().hastar_heuristic_field(self.h, C.c_void_p(int(dst_ptr)), C.byref(p)))
+        return p.value
+
+    def field_rows(self, field_ptr, r0, r1, init, halo_changed=0):
+        """Relax rows [r0, r1) of the device buffer at `field_ptr` ((r1 - r0 + 2) x N floats:
+        halo row, block, halo row) until stable for its halos; returns (changed mask, passes)."""
+        ch, p = C.c_int(0), C.c_int(0)
+        _check(load_library().hastar_field_rows(self.h, C.c_void_p(int(field_ptr)), int(r0), int(r1), int(bool(init)),
+                                                int(halo_changed), C.byref(ch), C.byref(p)))
+        return ch.value, p.value
+
+    def relaxed_set_field(self, src_ptr):
+        """Install a whole field (device buffer, N x N) as the relaxed mode's heuristic (used by
+        relaxed calls with reuse_heuristic=1, h_coarse=1 until reset / update_goal)."""
+        _check(load_library().hastar_relaxed_set_field(self.h, C.c_void_p(int(src_ptr))))
 
     # HybridAStar::find_path (HybridAStar.cpp:68-88)
     def find_path(self, vel_init, start, cap=4096):
