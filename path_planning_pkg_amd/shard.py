@@ -111,6 +111,8 @@ def heuristic_field_sharded(planner, rank, world, device, group=None, relax=None
             passes += p
         init = False
         rounds += 1
+        if world == 1:
+            break  # no neighbours: the block's first relaxation is the field
         local = torch.empty(2 * N + 1, dtype=torch.float32, device=device)
         if mine:
             local[:N] = buf[N:2 * N]
